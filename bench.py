@@ -1,0 +1,256 @@
+#!/usr/bin/env python3
+"""bench.py — Gsamples/s + %HBM roofline of the MI355X fixed-point FIR hot path.
+
+Default workload (BASELINE.json configs[1]; configs[3] at --gpus 8): 5-tap int16 -> int32
+FIR-1D (Q4.12 "sharpen" taps [-256,-1024,6656,-1024,-256], 32-bit wrap, round, no
+saturation) over 2^28 synthetic samples PER GPU (weak scaling: 2^31 samples on 8 GPUs),
+inputs resident in HBM before the timed region.  For N > 1 each rank owns one contiguous
+segment and a step includes the 2+2-sample halo exchange over RCCL plus the edge kernel.
+
+Contract: `python bench.py --gpus N --steps K --warmup W` (torchrun for N > 1); rank 0
+prints ONE JSON line.  Extra keys:
+  roofline      dominant kernel's algorithmic bytes / its mean duration (HIP events on the
+                stream it runs on), vs the 8.0 TB/s HBM3E peak; `traffic` = PMC HBM bytes per
+                launch from the committed rocprofv3 summary in profiles/ (null if absent)
+  cpu_baseline  the C oracle (oracle/fir_oracle.c, OpenMP) on this host's cores, same input
+  parity        every rank's full output compared bit-exactly with the C oracle
+Other workloads (`--workload cplx_i16 | fir2d_u8`) measure configs[2] / configs[4].
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+for _p in (ROOT, ROOT / "warmup-fir-filter_amd"):
+    if str(_p) not in sys.path:
+        sys.path.insert(0, str(_p))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import fir_hip  # noqa: E402
+from fir_hip import sharded, torch_ops  # noqa: E402
+
+METRIC = "Gsamples/s + %HBM-roofline, 5-tap int16 FIR-1D, 2^28 samples @1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+SEED = 20260227
+SHARPEN5 = [-256, -1024, 6656, -1024, -256]  # h_coeff_5tap_map["sharpen"] in Q4.12
+SIMPLE_LP3 = [1024, 2048, 1024]              # h_coeff_3tap_map["simple_lp"] in Q4.12
+SIMPLE_LP5 = [256, 1024, 1536, 1024, 256]    # h_coeff_5tap_map["simple_lp"] in Q4.12
+
+
+def _env_int(name: str, default: int) -> int:
+    v = os.environ.get(name)
+    return int(v) if v not in (None, "") else default
+
+
+def _cpu_threads() -> int:
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return max(1, min(16, _env_int("OMP_NUM_THREADS", n), n))
+
+
+class Workload:
+    """One bench workload: host input, device buffers, one step, the oracle check."""
+
+    def __init__(self, name: str, rank: int, world: int, dev: torch.device, log2n: int):
+        self.name, self.rank, self.world, self.dev = name, rank, world, dev
+        rng = np.random.default_rng(SEED + rank)
+        if name == "fir1d_i16":
+            self.n = 1 << log2n
+            self.taps = torch_ops.Taps(SHARPEN5)
+            self.channels = 1
+            self.x_host = rng.integers(-32768, 32768, self.n, dtype=np.int16)
+            self.bytes_per_unit = 2 + 4
+            self.units = self.n
+            self.unit = "Gsamples/s"
+            self.dtype = "int32 (int16 in, int32 wrap-around acc, int32 out)"
+            self.config = {"workload": "fir1d_int16_int32_5tap_sharpen_q4.12", "samples_per_gpu": self.n,
+                           "total_samples": self.n * world, "taps": 5, "frac_bits": 12, "acc_bits": 32,
+                           "parallelism": f"contiguous shards x{world}, 2+2-sample halo over RCCL" if world > 1
+                           else "single GPU"}
+        elif name == "cplx_i16":
+            self.n = 1 << (log2n - 1)  # complex samples
+            self.taps = torch_ops.Taps(SIMPLE_LP3)
+            self.channels = 2
+            self.x_host = rng.integers(-32768, 32768, 2 * self.n, dtype=np.int16)
+            self.bytes_per_unit = 4 + 8
+            self.units = self.n
+            self.unit = "Gsamples/s (complex)"
+            self.dtype = "int32 (complex int16 in, real Q4.12 taps, complex int32 out)"
+            self.config = {"workload": "fir1d_complex_int16_3tap_simple_lp", "complex_samples_per_gpu": self.n,
+                           "taps": 3, "parallelism": "single GPU" if world == 1 else f"contiguous shards x{world}"}
+        elif name == "fir2d_u8":
+            self.h = self.w = 8192
+            h1 = np.array(SIMPLE_LP5, dtype=np.int64)
+            self.hq2 = (np.outer(h1, h1) // 4096).astype(np.int64)  # unity-gain 5x5 Q4.12
+            self.x_host = rng.integers(0, 256, (self.h, self.w), dtype=np.uint8)
+            self.bytes_per_unit = 1 + 1
+            self.units = self.h * self.w
+            self.unit = "Gpixels/s"
+            self.dtype = "int32 (u8 in, int32 wrap-around acc, u8 saturated out)"
+            self.config = {"workload": "fir2d_u8_5x5_simple_lp_outer_q4.12", "frame": [self.h, self.w],
+                           "parallelism": "single GPU (replicas when N > 1)"}
+        else:
+            raise SystemExit(f"unknown workload {name}")
+        self.x = torch.from_numpy(self.x_host).to(dev)
+        out_dtype = torch.uint8 if name == "fir2d_u8" else torch.int32
+        self.y = torch.empty(self.x.shape, dtype=out_dtype, device=dev)
+        self.left = self.right = None
+
+    def bulk(self):
+        if self.name == "fir2d_u8":
+            torch_ops.fir2d_fixed_dev(self.x, self.hq2, 12, 32, fir_hip.OUT_U8_SAT, out=self.y)
+        else:
+            torch_ops.fir1d_fixed_rows_dev(self.x, self.taps, 12, 32, fir_hip.OUT_I32, self.channels, out=self.y)
+
+    def step(self, ev=None):
+        """One pass of the hot path; `ev` = (start, end) events bracketing the bulk kernel."""
+        sharded_1d = self.world > 1 and self.name != "fir2d_u8"
+        works = []
+        if sharded_1d:
+            self.left, self.right, works = sharded.post_halo_exchange(self.x, self.taps.n, self.channels)
+        if ev is not None:
+            ev[0].record()
+        self.bulk()
+        if ev is not None:
+            ev[1].record()
+        if sharded_1d:
+            sharded.wait_all(works)
+            torch_ops.fir1d_fixed_edges_dev(self.x, self.taps, self.y, self.left, self.right, 12, 32,
+                                            fir_hip.OUT_I32, self.channels)
+
+    def oracle(self, nthreads: int, reps: int = 1):
+        from oracle import c_oracle
+
+        co = c_oracle()
+        out = None
+        for _ in range(reps):
+            if self.name == "fir2d_u8":
+                out = co.fir2d(self.x_host, self.hq2, 12, 32, co.OUT_U8_SAT, nthreads=nthreads)
+            else:
+                hl = None if self.left is None else self.left.cpu().numpy()
+                hr = None if self.right is None else self.right.cpu().numpy()
+                out = co.fir1d_rows(self.x_host, self.taps.h, 12, 32, co.OUT_I32, channels=self.channels,
+                                    halo_left=hl, halo_right=hr, nthreads=nthreads)
+        return out
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", default="fir1d_i16", choices=("fir1d_i16", "cplx_i16", "fir2d_u8"))
+    ap.add_argument("--log2n", type=int, default=28, help="int16 values per GPU (2^28 = BASELINE configs[1])")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0 = skip)")
+    ap.add_argument("--no-parity", action="store_true", help="skip the full-size oracle comparison")
+    args = ap.parse_args()
+
+    rank, world = _env_int("RANK", 0), _env_int("WORLD_SIZE", 1)
+    local_rank = _env_int("LOCAL_RANK", 0)
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    wl = Workload(args.workload, rank, world, dev, args.log2n)
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local_rank])
+
+    for _ in range(args.warmup):
+        wl.step()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        wl.step(events[i])
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = [a.elapsed_time(b) for a, b in events]
+    kern_avg_s = float(np.mean(kern_ms)) / 1e3
+
+    # parity: full output vs the C oracle (every rank, its own segment with the received halos)
+    parity = "skipped"
+    if not args.no_parity:
+        ref = wl.oracle(_cpu_threads())
+        ok = bool(np.array_equal(wl.y.cpu().numpy(), ref))
+        if world > 1:
+            f = torch.tensor([0 if ok else 1], device=dev)
+            dist.all_reduce(f, op=dist.ReduceOp.MAX)
+            ok = int(f.item()) == 0
+        parity = "bit-exact vs C oracle (full output, every rank)" if ok else "MISMATCH"
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        nthr = _cpu_threads()
+        wl.oracle(nthr)  # warm (page-in, thread pool)
+        reps, tc0 = 0, time.perf_counter()
+        while True:
+            wl.oracle(nthr)
+            reps += 1
+            if time.perf_counter() - tc0 >= args.cpu_seconds:
+                break
+        tc = time.perf_counter() - tc0
+        cpu = {"value": round(wl.units * reps / tc / 1e9, 4), "unit": wl.unit, "cores": nthr, "kind": "port",
+               "sample": f"C oracle (oracle/fir_oracle.c, OpenMP {nthr} threads) on the full per-GPU workload "
+                         f"({wl.units} units) x {reps} repetitions, {tc:.1f} s"}
+
+    traffic = None
+    pmc = ROOT / "profiles" / f"pmc_{args.workload}.json"
+    if pmc.exists():
+        try:
+            traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
+        except (ValueError, OSError):
+            traffic = None
+
+    total_units = wl.units * world * args.steps
+    value = total_units / elapsed / 1e9
+    alg_bytes = wl.units * wl.bytes_per_unit
+    achieved = alg_bytes / kern_avg_s / 1e9
+    line = {
+        "metric": METRIC if args.workload == "fir1d_i16" else f"{wl.unit}, {wl.config['workload']}",
+        "value": round(value, 3),
+        "unit": wl.unit,
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": wl.dtype,
+        "data": "synthetic (numpy default_rng seed 20260227 + rank), resident in HBM before timing",
+        "config": wl.config,
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "fir1d_reg_kernel" if args.workload != "fir2d_u8" else "fir2d_reg_kernel",
+                     "kernel_avg_us": round(kern_avg_s * 1e6, 2), "algorithmic_bytes_per_launch": alg_bytes},
+        "cpu_baseline": cpu,
+        "parity": parity,
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if parity != "MISMATCH" else 1
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

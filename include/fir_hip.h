@@ -1,0 +1,109 @@
+/*
+ * fir_hip.h — C ABI of libfir_hip.so, the MI355X (gfx950) fixed-point FIR path.
+ *
+ * Plain C types only (pointers, sizes, ints); no exceptions cross this boundary.
+ * Every entry returns a fir_status; on failure fir_last_error() (thread-local)
+ * holds the message.  Argument validation that the reference performs in Python
+ * (ValueError texts of fir_1d_ref.py:9-33 / fir_1d_fixed_ref.py:39-72) stays in the
+ * Python host layer; these entries only reject structurally impossible calls
+ * (FIR_EINVAL) and report HIP/device failures (FIR_EHIP / FIR_ENODEV).
+ *
+ * Reference interfaces replaced (paths relative to the reference root):
+ *   fir1d_fixed_rows      the per-row loop of fir_1d/sim/vector/gen_fixed_output.py:34-60
+ *                         (_run_fixed_rowwise), each row being a call of
+ *                         fir_1d/model/python/fir_1d_fixed_ref.py:12-130 (fir_1d_fixed_golden)
+ *                         after its host-side prep (:33-81); one call per image instead of
+ *                         one per row.  A single row is the fir_1d_fixed_golden call itself.
+ *   fir1d_fixed_rows_dev  same, device buffers, asynchronous on a caller stream (bench,
+ *                         sharded driver, graph capture).
+ *   fir1d_fixed_edges_dev recomputes the first (L-1-L/2) and last (L/2) outputs of a
+ *                         segment from neighbour halo samples (multi-GPU sharding, SURVEY
+ *                         §8(e)); no reference counterpart (the reference is one process).
+ *   fir2d_fixed[_dev]     fir_2d/model/cpp/CMakeLists.txt is empty in the reference; the
+ *                         2-D semantics are the build's.
+ *   fir1d_ideal_rows[_dev] fir_1d/model/python/fir_1d_ref.py:43-65 (fir_1d_ideal) per row as
+ *                         in fir_1d/sim/vector/gen_ideal_output.py:37-50.
+ *   fir_compare_metrics   fir_1d/sim/vector/gen_3tap_compare_report.py:67-112 (_compute_metrics).
+ *
+ * Arithmetic (all fixed entries): y[n] = stage(round(wrap_acc(sum_k hq[k] * x[n - k + L/2])))
+ *   wrap_acc: two's-complement wrap to acc_bits (fir_1d_fixed_ref.py:110-115)
+ *   round:    (acc + 2^(frac_bits-1)) >> frac_bits, arithmetic (:118-120)
+ *   stage:    FIR_OUT_U8_SAT clamps to [0,255] (:123-126); FIR_OUT_I32 keeps the int32 value.
+ * Samples outside a row are zero (:99-104) unless halo buffers are supplied.
+ */
+#ifndef FIR_HIP_H
+#define FIR_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FIR_HIP_ABI_VERSION 1
+#define FIR_MAX_TAPS 256 /* 1-D taps; 2-D: tap_rows * tap_cols <= FIR_MAX_TAPS */
+
+typedef enum {
+    FIR_OK = 0,
+    FIR_EINVAL = 1, /* structurally invalid arguments (null pointer, bad enum, size) */
+    FIR_EHIP = 2,   /* a HIP runtime call failed */
+    FIR_ENODEV = 3, /* no usable gfx950 device / device index out of range */
+    FIR_ENOMEM = 4  /* device allocation failed */
+} fir_status;
+
+typedef enum { FIR_IN_U8 = 0, FIR_IN_I16 = 1 } fir_in_dtype;
+typedef enum { FIR_OUT_U8_SAT = 0, FIR_OUT_I32 = 1 } fir_out_stage;
+
+/* Library / device queries. */
+int fir_abi_version(void);
+const char* fir_last_error(void);
+int fir_device_count(int* count);
+
+/* ---- 1-D fixed-point FIR over independent rows (a1, a4, a6, a7) -------------------
+ * x: rows x (width*channels) samples of in_dtype, C-contiguous; channels > 1 means
+ * interleaved channels (complex int16 = 2) filtered independently with the same real
+ * taps.  hq: `taps` quantized coefficients (host memory, int32).  y: same shape, uint8
+ * (FIR_OUT_U8_SAT) or int32 (FIR_OUT_I32).  1 <= frac_bits, 1 <= acc_bits.
+ * Host-pointer form: synchronous (H2D, kernel, D2H) on `device`. */
+int fir1d_fixed_rows(const void* x, int in_dtype, int64_t rows, int64_t width, int channels,
+                     const int32_t* hq, int taps, int frac_bits, int acc_bits, int out_stage,
+                     void* y, int device);
+
+/* Device-pointer form: enqueued on `stream` (hipStream_t; NULL = default stream of the
+ * current device); returns after the launch, not after completion. */
+int fir1d_fixed_rows_dev(const void* x_dev, int in_dtype, int64_t rows, int64_t width,
+                         int channels, const int32_t* hq, int taps, int frac_bits, int acc_bits,
+                         int out_stage, void* y_dev, void* stream);
+
+/* Recompute the first (taps-1-taps/2)*channels and last (taps/2)*channels outputs of a
+ * single-row segment of n*channels samples, reading out-of-segment samples from
+ * halo_left_dev ((taps-1-taps/2)*channels samples preceding the segment) and
+ * halo_right_dev ((taps/2)*channels samples following it); a NULL halo means zeros.
+ * Used after fir1d_fixed_rows_dev when the segment is a shard of a longer signal. */
+int fir1d_fixed_edges_dev(const void* x_dev, int in_dtype, int64_t n, int channels,
+                          const int32_t* hq, int taps, int frac_bits, int acc_bits, int out_stage,
+                          const void* halo_left_dev, const void* halo_right_dev, void* y_dev,
+                          void* stream);
+
+/* ---- 2-D fixed-point FIR (a8) ------------------------------------------------------
+ * y[i,j] = stage(round(wrap(sum_m sum_n hq[m*tap_cols+n] * x[i-m+tap_rows/2][j-n+tap_cols/2])))
+ * x: height x width uint8, zero padded at every frame edge. */
+int fir2d_fixed(const uint8_t* x, int64_t height, int64_t width, const int32_t* hq, int tap_rows,
+                int tap_cols, int frac_bits, int acc_bits, int out_stage, void* y, int device);
+int fir2d_fixed_dev(const uint8_t* x_dev, int64_t height, int64_t width, const int32_t* hq,
+                    int tap_rows, int tap_cols, int frac_bits, int acc_bits, int out_stage,
+                    void* y_dev, void* stream);
+
+/* ---- float64 "ideal" model ----------------------------------------
+ * y[r,n] = sum over k (in k order, products and sums rounded separately, zero terms for
+ * padding) of h[k] * x[r, n - k + taps/2]; no output clamp.  x uint8 rows x width. */
+int fir1d_ideal_rows(const uint8_t* x, int64_t rows, int64_t width, const double* h, int taps,
+                     double* y, int device);
+int fir1d_ideal_rows_dev(const uint8_t* x_dev, int64_t rows, int64_t width, const double* h,
+                         int taps, double* y_dev, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FIR_HIP_H */

@@ -1,0 +1,317 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE model.
+
+Runs only in the build container, where the read-only reference is mounted at
+/root/reference (override with FIR_REFERENCE).  The GPU box never runs this
+script; it only reads the data files written here.  No reference source text
+is copied: the script imports the reference's own functions and stores their
+inputs and outputs as data.
+
+Reference entry points exercised (paths relative to the reference root):
+  fir_1d/model/python/fir_1d_fixed_ref.py:12   fir_1d_fixed_golden
+  fir_1d/model/python/fir_1d_ref.py:43         fir_1d_ideal
+  fir_1d/sim/vector/gen_input_vectors.py:19    _load_image_gray_u8 (Pillow decode)
+  fir_1d/sim/vector/gen_fixed_output.py:34     _run_fixed_rowwise
+  fir_1d/sim/vector/gen_ideal_output.py:37     _run_ideal_rowwise
+  fir_1d/sim/vector/gen_3tap_compare_report.py:67  _compute_metrics
+  fir_1d/sim/vector/h_coeff.py:3-16            coefficient banks
+
+Files written:
+  kat_fixed.json, kat_ideal.json     known-answer + error cases (reference tests' vectors)
+  random_fixed.npz, random_ideal.npz randomized (x, h, frac, acc, coeff) sweeps
+  images_u8.npz                      the 7 decoded golden input images (u8, H x W)
+  image_outputs.json                 sha256 of all 56 fixed + 56 ideal outputs + report metrics
+  small_image_outputs.npz            full fixed/ideal outputs of the two 64x64 cases
+  meta.json                          generator environment
+
+Usage:  python tests/golden/make_golden.py [--jobs 8]
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import math
+import multiprocessing as mp
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+
+REF = Path(os.environ.get("FIR_REFERENCE", "/root/reference"))
+OUT = Path(__file__).resolve().parent
+
+
+def _ref_imports():
+    if str(REF) not in sys.path:
+        sys.path.insert(0, str(REF))
+    from fir_1d.model.python import fir_1d_fixed_ref, fir_1d_ref  # noqa: F401
+    from fir_1d.sim.vector import gen_fixed_output, gen_ideal_output, gen_input_vectors  # noqa: F401
+    from fir_1d.sim.vector import gen_3tap_compare_report, h_coeff  # noqa: F401
+    return fir_1d_fixed_ref, fir_1d_ref, gen_fixed_output, gen_ideal_output, gen_input_vectors, gen_3tap_compare_report, h_coeff
+
+
+def _call(fn, *args, **kw):
+    try:
+        y = fn(*args, **kw)
+        return {"ok": y}
+    except Exception as exc:  # record the exception type and message text
+        return {"error": type(exc).__name__, "message": str(exc)}
+
+
+# ----------------------------------------------------------------------------
+# Known-answer / error cases: the vectors the reference's own tests use
+# (fir_1d/sim/tests/test_1d_fixed.py, test_1d_ideal.py) plus boundary cases.
+# ----------------------------------------------------------------------------
+NAN, INF = float("nan"), float("inf")
+
+KAT_FIXED = [
+    ([10, 20, 30, 40], [0.25, 0.5, 0.25], {}),
+    ([-1.2, 0.5, 1.5, 254.6, 300.2], [1.0], {}),
+    ([255, 255], [7.999755859375], {}),
+    ([255, 255], [-8.0], {}),
+    ([10, NAN, 20], [0.5], {}),
+    ([10, INF, 20], [0.5], {}),
+    ([10, -INF, 20], [0.5], {}),
+    ([10, 20], [NAN], {}),
+    ([10, 20], [INF], {}),
+    ([10, 20], [-INF], {}),
+    ([10, 20], [], {}),
+    ([10, 20], [0.5], {"coeff_bits": 12}),
+    ([10, 20], [0.5], {"frac_bits": 0}),
+    ([10, 20], [0.5], {"frac_bits": -1}),
+    ([10, 20], [0.5], {"acc_bits": 0}),
+    ([10, 20], [0.5], {"acc_bits": -1}),
+    ([10, 20], [7.999755859375], {}),
+    ([10, 20], [8.0], {}),
+    ([10, 20], [1.0], {"frac_bits": 7, "coeff_bits": 8}),
+    ([255, 255, 255, 255], [0.5, 0.25], {}),
+    # extra boundary cases
+    ([], [0.5, 0.25], {}),
+    ([7], [0.25, 0.5, 0.25], {}),
+    ([1, 2], [0.1, 0.2, 0.3, 0.4, 0.5], {}),
+    ([0.49, 0.5, 1.49999, 2.5, 254.5, 255.49, -0.5, -0.51], [1.0], {}),
+    ([255] * 8, [7.999755859375] * 5, {"acc_bits": 16}),
+    ([255] * 8, [-8.0] * 5, {"acc_bits": 12}),
+    ([200, 100, 50, 25], [8.5], {}),
+    ([200, 100, 50, 25], [-8.0000001], {}),
+    ([10, NAN], [NAN], {}),
+    ([10, NAN], [0.5], {"frac_bits": 0}),
+    ([10, 20], [0.5], {"frac_bits": 0, "coeff_bits": 12}),
+    ([10, 20], [0.5, 9.0], {"coeff_bits": 12}),
+    ([10, 20, 30], [1.0], {"frac_bits": 12, "acc_bits": 64, "coeff_bits": 32}),
+    ([255, 255, 255], [7.5, 7.5, 7.5], {"frac_bits": 28, "acc_bits": 40, "coeff_bits": 32}),
+]
+
+KAT_IDEAL = [
+    ([10, 20, 30, 40], [0.25, 0.5, 0.25]),
+    ([3, 7, 11, 15, 19], [0.1, 0.5, 0.3, 0.1]),
+    ([-1.2, 0.49, 0.5, 1.5, 254.6, 300.2], [1.0]),
+    ([255, 255], [5.0]),
+    ([10, NAN, 20], [1.0]),
+    ([10, INF, 20], [1.0]),
+    ([10, -INF, 20], [1.0]),
+    ([10, 20, 30], [NAN]),
+    ([10, 20, 30], [INF]),
+    ([10, 20, 30], [-INF]),
+    ([10, 20, 30], []),
+    ([10, 20, 30], [8.0 + 1e-6]),
+    ([10, 20], [-8.0, 8.0]),
+    ([], [1.0, 2.0]),
+    ([5], [0.2, 0.2, 0.2, 0.2, 0.2]),
+    ([0.1, 0.2, 0.3, 255.0, 17.0], [1 / 3, 1 / 3, 1 / 3]),
+]
+
+
+def _enc_float(v):
+    """JSON-safe exact float: hex string."""
+    return float(v).hex()
+
+
+def gen_kats(fixed_ref, ideal_ref):
+    fixed = []
+    for x, h, kw in KAT_FIXED:
+        r = _call(fixed_ref.fir_1d_fixed_golden, list(x), list(h), **kw)
+        rec = {"x": [_enc_float(v) for v in x], "h": [_enc_float(v) for v in h], "kwargs": kw}
+        if "ok" in r:
+            rec["expect"] = [int(v) for v in r["ok"]]
+        else:
+            rec["error"] = r["error"]
+            rec["message"] = r["message"]
+        fixed.append(rec)
+    ideal = []
+    for x, h in KAT_IDEAL:
+        r = _call(ideal_ref.fir_1d_ideal, list(x), list(h))
+        rec = {"x": [_enc_float(v) for v in x], "h": [_enc_float(v) for v in h]}
+        if "ok" in r:
+            rec["expect"] = [_enc_float(v) for v in r["ok"]]
+        else:
+            rec["error"] = r["error"]
+            rec["message"] = r["message"]
+        ideal.append(rec)
+    (OUT / "kat_fixed.json").write_text(json.dumps(fixed, indent=1) + "\n")
+    (OUT / "kat_ideal.json").write_text(json.dumps(ideal, indent=1) + "\n")
+    return len(fixed), len(ideal)
+
+
+# ----------------------------------------------------------------------------
+# Randomized sweeps
+# ----------------------------------------------------------------------------
+ACC_CHOICES = [1, 2, 7, 8, 12, 16, 17, 20, 24, 28, 31, 32, 33, 40, 48, 63, 64, 70]
+L_CHOICES = [1, 2, 3, 4, 5, 6, 7, 8, 9, 11, 15, 17, 31]
+
+
+def _rand_x(rng, n):
+    kind = rng.integers(0, 4)
+    if kind == 0:
+        return rng.integers(0, 256, n).astype(np.float64)
+    if kind == 1:
+        return rng.uniform(-30.0, 290.0, n)
+    if kind == 2:
+        return np.floor(rng.uniform(-4.0, 260.0, n)) + 0.5  # half-integers: round-half-up ties
+    v = rng.integers(0, 256, n).astype(np.float64)
+    v[rng.random(n) < 0.5] = rng.choice([0.0, 255.0])
+    return v
+
+
+def _rand_h(rng, L, frac, coeff):
+    scale = float(1 << frac)
+    lo = max(-(1 << (coeff - 1)) / scale, -8.0)
+    hi = min(((1 << (coeff - 1)) - 1) / scale, 8.0)
+    kind = rng.integers(0, 4)
+    if kind == 0:
+        h = rng.uniform(lo, hi, L)
+    elif kind == 1:  # exact ties for rint (ties-to-even)
+        k = rng.integers(int(math.ceil(lo * scale)), int(math.floor(hi * scale)), L)
+        h = (k + 0.5) / scale
+        h = np.clip(h, lo, hi)
+    elif kind == 2:  # extremes
+        h = rng.choice([lo, hi, 0.0], L)
+    else:
+        h = rng.uniform(lo, hi, L) * rng.choice([1e-3, 1e-1, 1.0], L)
+    return h
+
+
+def gen_random_fixed(fixed_ref, seed=20260227, cases=3000):
+    rng = np.random.default_rng(seed)
+    xs, hs, ys, params = [], [], [], []
+    for i in range(cases):
+        coeff = int(rng.choice([8, 16, 32]))
+        frac = int(rng.integers(1, 21))
+        if coeff == 32 and rng.random() < 0.3:
+            frac = int(rng.integers(20, 31))
+        acc = int(rng.choice(ACC_CHOICES))
+        L = int(rng.choice(L_CHOICES))
+        n = int(rng.integers(0, 260)) if i % 50 else int(rng.integers(0, 4))
+        x = _rand_x(rng, n)
+        h = _rand_h(rng, L, frac, coeff)
+        r = _call(fixed_ref.fir_1d_fixed_golden, x.tolist(), h.tolist(), frac_bits=frac, acc_bits=acc, coeff_bits=coeff)
+        if "ok" not in r:
+            continue  # out-of-range draws are skipped; error texts are pinned by the KATs
+        xs.append(x)
+        hs.append(h)
+        ys.append(np.asarray(r["ok"], dtype=np.uint8))
+        params.append((frac, acc, coeff))
+    _save_ragged(OUT / "random_fixed.npz", xs, hs, ys, np.array(params, dtype=np.int64))
+    return len(xs)
+
+
+def gen_random_ideal(ideal_ref, seed=20260228, cases=800):
+    rng = np.random.default_rng(seed)
+    xs, hs, ys = [], [], []
+    for i in range(cases):
+        L = int(rng.choice(L_CHOICES))
+        n = int(rng.integers(0, 260)) if i % 50 else int(rng.integers(0, 4))
+        x = _rand_x(rng, n)
+        h = rng.uniform(-8.0, 8.0, L) * rng.choice([1e-2, 1.0], L)
+        r = _call(ideal_ref.fir_1d_ideal, x.tolist(), h.tolist())
+        xs.append(x)
+        hs.append(h)
+        ys.append(np.asarray(r["ok"], dtype=np.float64))
+    _save_ragged(OUT / "random_ideal.npz", xs, hs, ys, np.zeros((len(xs), 0), dtype=np.int64))
+    return len(xs)
+
+
+def _save_ragged(path, xs, hs, ys, params):
+    def cat(parts, dtype):
+        off = np.zeros(len(parts) + 1, dtype=np.int64)
+        off[1:] = np.cumsum([len(p) for p in parts])
+        data = np.concatenate(parts).astype(dtype) if parts else np.zeros(0, dtype)
+        return data, off
+
+    xa, xo = cat(xs, np.float64)
+    ha, ho = cat(hs, np.float64)
+    ya, yo = cat(ys, ys[0].dtype if ys else np.uint8)
+    np.savez_compressed(path, x=xa, x_off=xo, h=ha, h_off=ho, y=ya, y_off=yo, params=params)
+
+
+# ----------------------------------------------------------------------------
+# Golden images: decode, then run the reference row drivers for every filter
+# ----------------------------------------------------------------------------
+def _sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def _image_job(args):
+    stem, tap, name, h = args
+    fixed_ref, ideal_ref, gfo, gio, _, rep, _ = _ref_imports()
+    x = np.load(OUT / "images_u8.npz")[stem]
+    yf = gfo._run_fixed_rowwise(x, h, frac_bits=12, acc_bits=32, coeff_bits=16)
+    yi = gio._run_ideal_rowwise(x, h)
+    metrics = rep._compute_metrics(yi, yf)
+    small = (yf, yi) if x.size <= 64 * 64 else None
+    return stem, tap, name, _sha(yf), _sha(yi), metrics, small
+
+
+def gen_images(jobs):
+    _, _, _, _, giv, _, hc = _ref_imports()
+    files = giv._iter_image_files(REF / "fir_1d" / "sim" / "img")
+    imgs = {}
+    for idx, p in enumerate(files):
+        imgs[f"case_{idx:03d}_{p.stem}"] = giv._load_image_gray_u8(p)
+    np.savez_compressed(OUT / "images_u8.npz", **imgs)
+    inputs = {k: {"shape": list(v.shape), "sha256": _sha(v)} for k, v in imgs.items()}
+
+    work = []
+    for stem in imgs:
+        for tap, bank in (("3tap", hc.h_coeff_3tap_map), ("5tap", hc.h_coeff_5tap_map)):
+            for name, h in bank.items():
+                work.append((stem, tap, name, list(h)))
+    work.sort(key=lambda w: -imgs[w[0]].size)  # big first for load balance
+    with mp.get_context("fork").Pool(jobs) as pool:
+        results = pool.map(_image_job, work, chunksize=1)
+
+    outputs = []
+    small = {}
+    for stem, tap, name, sf, si, metrics, sm in sorted(results):
+        outputs.append({"case_stem": stem, "tap": tap, "coeff_name": name,
+                        "fixed_u8_sha256": sf, "ideal_f64_sha256": si, "metrics": metrics})
+        if sm is not None:
+            small[f"{stem}__{name}_fixed_{tap}"] = sm[0]
+            small[f"{stem}__{name}_ideal_{tap}"] = sm[1]
+    banks = {"3tap": hc.h_coeff_3tap_map, "5tap": hc.h_coeff_5tap_map}
+    (OUT / "image_outputs.json").write_text(json.dumps(
+        {"inputs": inputs, "banks": banks, "outputs": outputs}, indent=1) + "\n")
+    np.savez_compressed(OUT / "small_image_outputs.npz", **small)
+    return len(outputs)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
+    ap.add_argument("--skip-images", action="store_true")
+    args = ap.parse_args()
+    fixed_ref, ideal_ref, *_ = _ref_imports()
+    import PIL
+    meta = {"reference": str(REF), "numpy": np.__version__, "pillow": PIL.__version__,
+            "python": sys.version.split()[0]}
+    print("kats", gen_kats(fixed_ref, ideal_ref))
+    print("random_fixed", gen_random_fixed(fixed_ref))
+    print("random_ideal", gen_random_ideal(ideal_ref))
+    if not args.skip_images:
+        print("images", gen_images(args.jobs))
+    (OUT / "meta.json").write_text(json.dumps(meta, indent=1) + "\n")
+
+
+if __name__ == "__main__":
+    main()

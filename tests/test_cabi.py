@@ -1,0 +1,63 @@
+"""The C-ABI library: it loads, exports exactly what include/fir_hip.h declares, and rejects
+structurally invalid calls with FIR_EINVAL and a message — all without a GPU (no compute
+call is made here)."""
+from __future__ import annotations
+
+import ctypes
+import re
+from pathlib import Path
+
+import pytest
+
+import fir_hip
+
+HEADER = Path(__file__).resolve().parents[1] / "include" / "fir_hip.h"
+
+
+def _declared() -> set[str]:
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    return set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(\w+)\s*\(", text, flags=re.M))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not fir_hip.lib_path().exists():
+        pytest.fail(f"{fir_hip.lib_path()} not built; run `python -c 'import __graft_entry__ as g; g.build()'`")
+    return fir_hip.lib()
+
+
+def test_header_declares_the_binding_table():
+    assert _declared() == set(fir_hip.EXPORTS), "include/fir_hip.h and fir_hip.EXPORTS disagree"
+
+
+def test_library_exports_every_declared_symbol(lib):
+    raw = ctypes.CDLL(str(fir_hip.lib_path()))
+    for name in _declared():
+        assert hasattr(raw, name), name
+
+
+def test_abi_version(lib):
+    assert lib.fir_abi_version() == fir_hip.ABI_VERSION == 1
+
+
+def test_invalid_arguments_are_rejected_without_device(lib):
+    h = (ctypes.c_int32 * 3)(1, 2, 1)
+    rc = lib.fir1d_fixed_rows_dev(None, 7, 1, 16, 1, h, 3, 12, 32, 0, None, None)
+    assert rc == 1 and b"in_dtype" in lib.fir_last_error()
+    rc = lib.fir1d_fixed_rows_dev(None, 0, 1, 16, 1, h, 0, 12, 32, 0, None, None)
+    assert rc == 1 and b"taps" in lib.fir_last_error()
+    rc = lib.fir1d_fixed_rows_dev(None, 0, 1, 16, 1, h, 3, 0, 32, 0, None, None)
+    assert rc == 1 and b"frac_bits" in lib.fir_last_error()
+    rc = lib.fir1d_fixed_rows_dev(None, 0, 1, 16, 1, h, 3, 12, 32, 0, None, None)
+    assert rc == 1 and b"NULL" in lib.fir_last_error()
+    rc = lib.fir2d_fixed_dev(None, 4, 4, h, 0, 3, 12, 32, 0, None, None)
+    assert rc == 1
+    # empty problems are valid no-ops
+    assert lib.fir1d_fixed_rows_dev(None, 0, 0, 16, 1, h, 3, 12, 32, 0, None, None) == 0
+
+
+def test_errors_surface_as_firhiperror():
+    with pytest.raises(fir_hip.FirHipError):
+        fir_hip._taps_i32([])
+    with pytest.raises(fir_hip.FirHipError):
+        fir_hip._taps_i32(list(range(fir_hip.MAX_TAPS + 1)))

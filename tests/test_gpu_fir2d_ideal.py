@@ -1,0 +1,113 @@
+"""GPU parity of the 2-D fixed path and the float64 ideal model (§8(f) 1).
+
+fir_2d has no reference implementation (fir_2d/model/cpp/CMakeLists.txt is empty); its
+semantics are pinned two ways: (1) a 5x5 kernel with only the centre row (column)
+non-zero must equal the reference's row-wise golden model on the image (its transpose),
+using the reference's own golden outputs; (2) general kernels against the C oracle.
+The ideal kernel is pinned bit-for-bit (float64 bytes) to the reference's outputs.
+"""
+from __future__ import annotations
+
+import hashlib
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+import fir_hip
+from conftest import iter_ragged, load_kats
+from fir_1d.model.python.fir_1d_ref import fir_1d_ideal
+from fir_1d.sim.vector.gen_ideal_output import _run_ideal_rowwise
+from fir_1d.sim.vector.h_coeff import h_coeff_3tap_map, h_coeff_5tap_map
+from fir_hip import torch_ops
+from oracle import c_oracle, fir_oracle as fo
+
+DEV = torch.device("cuda:0")
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+# ---- fir_2d ---------------------------------------------------------------------------
+def test_fir2d_centre_row_and_column_pins(images, image_outputs):
+    for o in image_outputs["outputs"]:
+        if o["tap"] != "5tap":
+            continue
+        x = images[o["case_stem"]]
+        h1 = fo.quantize_h(image_outputs["banks"]["5tap"][o["coeff_name"]])
+        k = np.zeros((5, 5), np.int64)
+        k[2] = h1
+        assert _sha(fir_hip.fir2d_fixed(x, k)) == o["fixed_u8_sha256"], o["case_stem"]
+        xt = np.ascontiguousarray(x.T)
+        yt = fir_hip.fir2d_fixed(xt, k.T.copy())
+        assert _sha(np.ascontiguousarray(yt.T)) == o["fixed_u8_sha256"], o["case_stem"]
+
+
+@pytest.mark.parametrize("shape", [(1, 16), (3, 32), (37, 64), (64, 64), (100, 1280), (257, 4096), (5, 16 * 300),
+                                   (33, 17), (40, 4499), (1, 1), (7, 3)])
+@pytest.mark.parametrize("R,C", [(5, 5), (3, 3), (1, 5), (5, 1), (3, 5), (2, 4), (7, 7)])
+def test_fir2d_vs_oracle(shape, R, C):
+    rng = np.random.default_rng(shape[0] * 1000 + shape[1] + R * 10 + C)
+    x = rng.integers(0, 256, shape, dtype=np.uint8)
+    hq = rng.integers(-2048, 2048, (R, C))
+    co = c_oracle()
+    for stage in (fir_hip.OUT_U8_SAT, fir_hip.OUT_I32):
+        assert np.array_equal(fir_hip.fir2d_fixed(x, hq, 12, 32, stage), co.fir2d(x, hq, 12, 32, stage)), stage
+
+
+def test_fir2d_wrap_and_bit_widths():
+    rng = np.random.default_rng(12)
+    x = rng.integers(0, 256, (96, 512), dtype=np.uint8)
+    hq = np.full((5, 5), 8_000_000, dtype=np.int64)  # 25 * 255 * 8e6 = 5.1e10: wraps 32 bits
+    co = c_oracle()
+    for frac, acc in ((12, 32), (12, 24), (20, 32), (12, 40)):
+        assert np.array_equal(fir_hip.fir2d_fixed(x, hq, frac, acc, 1), co.fir2d(x, hq, frac, acc, 1))
+
+
+def test_fir2d_full_frame_8192():
+    """BASELINE configs[4]: 8192 x 8192 u8 frame, 5x5 unity-gain kernel."""
+    x = np.random.default_rng(20260227).integers(0, 256, (8192, 8192), dtype=np.uint8)
+    h1 = np.array([256, 1024, 1536, 1024, 256], dtype=np.int64)
+    hq = np.outer(h1, h1) // 4096
+    y = torch_ops.fir2d_fixed_dev(torch.from_numpy(x).to(DEV), hq)
+    torch.cuda.synchronize()
+    assert np.array_equal(y.cpu().numpy(), c_oracle().fir2d(x, hq))
+
+
+# ---- ideal float64 ---------------------------------------------------------------------
+def test_ideal_reference_unit_cases():
+    # fir_1d/sim/tests/test_1d_ideal.py:8-42 vectors, bit-exact here
+    assert fir_1d_ideal([10, 20, 30, 40], [0.25, 0.5, 0.25]) == [10.0, 20.0, 30.0, 27.5]
+    assert len(fir_1d_ideal([3, 7, 11, 15, 19], [0.1, 0.5, 0.3, 0.1])) == 5
+    assert fir_1d_ideal([-1.2, 0.49, 0.5, 1.5, 254.6, 300.2], [1.0]) == [0.0, 0.0, 1.0, 2.0, 255.0, 255.0]
+    assert fir_1d_ideal([255, 255], [5.0]) == [1275.0, 1275.0]
+    assert len(fir_1d_ideal([10, 20], [-8.0, 8.0])) == 2
+
+
+def test_ideal_known_answers_and_random_sweep_bits():
+    for rec in load_kats("ideal"):
+        if "expect" in rec:
+            assert fir_1d_ideal(rec["x"], rec["h"]) == rec["expect"]
+    for x, h, _, y in iter_ragged("ideal"):
+        got = np.asarray(fir_1d_ideal(x.tolist(), h.tolist()), dtype=np.float64)
+        assert got.tobytes() == y.tobytes()
+
+
+def test_ideal_all_56_image_outputs_bit_exact(images, image_outputs):
+    for o in image_outputs["outputs"]:
+        h = image_outputs["banks"][o["tap"]][o["coeff_name"]]
+        y = _run_ideal_rowwise(images[o["case_stem"]], h)
+        assert _sha(y) == o["ideal_f64_sha256"], (o["case_stem"], o["tap"], o["coeff_name"])
+
+
+def test_ideal_small_images_full_arrays(images):
+    d = np.load(Path(__file__).parent / "golden" / "small_image_outputs.npz")
+    for key in d.files:
+        if "_ideal_" not in key:
+            continue
+        stem, rest = key.split("__")
+        coeff, tap = rest.split("_ideal_")
+        bank = h_coeff_3tap_map if tap == "3tap" else h_coeff_5tap_map
+        assert _run_ideal_rowwise(images[stem], bank[coeff]).tobytes() == d[key].tobytes(), key

@@ -1,0 +1,263 @@
+// capi.hip — the extern "C" boundary of libfir_hip.so (declared in include/fir_hip.h).
+//
+// Host-pointer entries own a per-device cache of device buffers and one non-blocking
+// stream per device (grown on demand, never shrunk; guarded by a per-device mutex, so
+// calls are reentrant across devices and serialised per device).  They are synchronous:
+// H2D copy, kernel, D2H copy, stream synchronise.  Device-pointer entries (_dev) only
+// enqueue on the caller's stream and never allocate or synchronise, so they can be
+// captured in a hipGraph.  No C++ exception crosses the boundary.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "fir_hip.h"
+#include "fir_launch.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t _e = (expr);                                                                \
+        if (_e != hipSuccess) return fail(FIR_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+struct DeviceBuf {
+    void* ptr = nullptr;
+    size_t cap = 0;
+};
+
+struct DeviceState {
+    std::mutex mu;
+    bool init = false;
+    hipStream_t stream = nullptr;
+    DeviceBuf in, out;
+};
+
+std::mutex g_devs_mu;
+std::vector<std::unique_ptr<DeviceState>> g_devs;
+
+int ensure(DeviceBuf& b, size_t bytes) {
+    if (bytes <= b.cap) return FIR_OK;
+    if (b.ptr) (void)hipFree(b.ptr);
+    b.ptr = nullptr;
+    b.cap = 0;
+    size_t want = bytes < (1u << 20) ? (1u << 20) : bytes;
+    hipError_t e = hipMalloc(&b.ptr, want);
+    if (e != hipSuccess) {
+        b.ptr = nullptr;
+        return fail(FIR_ENOMEM, std::string("hipMalloc(") + std::to_string(want) + "): " + hipGetErrorString(e));
+    }
+    b.cap = want;
+    return FIR_OK;
+}
+
+// Validates `device`, makes it current, and returns its state (locked by the caller).
+int device_state(int device, DeviceState** out) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0)
+        return fail(FIR_ENODEV, std::string("no HIP device available: ") + (e != hipSuccess ? hipGetErrorString(e) : "0 devices"));
+    if (device < 0 || device >= n)
+        return fail(FIR_ENODEV, "device " + std::to_string(device) + " out of range (" + std::to_string(n) + " devices)");
+    {
+        std::lock_guard<std::mutex> lk(g_devs_mu);
+        if ((int)g_devs.size() < n) {
+            g_devs.reserve(n);
+            while ((int)g_devs.size() < n) g_devs.emplace_back(new DeviceState());
+        }
+    }
+    HIP_TRY(hipSetDevice(device));
+    *out = g_devs[device].get();
+    return FIR_OK;
+}
+
+int init_locked(DeviceState* st, int device) {
+    if (st->init) return FIR_OK;
+    hipDeviceProp_t p;
+    HIP_TRY(hipGetDeviceProperties(&p, device));
+    if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0)
+        return fail(FIR_ENODEV, std::string("device ") + std::to_string(device) + " is " + p.gcnArchName +
+                                    "; libfir_hip is built for gfx950 (MI355X) only");
+    HIP_TRY(hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking));
+    st->init = true;
+    return FIR_OK;
+}
+
+size_t in_size(int in_dtype) { return in_dtype == FIR_IN_I16 ? 2 : 1; }
+size_t out_size(int stage) { return stage == FIR_OUT_I32 ? 4 : 1; }
+
+// Run `launch(dx, dy, stream)` between an H2D copy of `in_bytes` and a D2H copy of `out_bytes`.
+template <typename F>
+int run_host(int device, const void* x, size_t in_bytes, void* y, size_t out_bytes, F launch) {
+    DeviceState* st = nullptr;
+    int rc = device_state(device, &st);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(st->mu);
+    rc = init_locked(st, device);
+    if (rc) return rc;
+    if ((rc = ensure(st->in, in_bytes)) || (rc = ensure(st->out, out_bytes))) return rc;
+    HIP_TRY(hipMemcpyAsync(st->in.ptr, x, in_bytes, hipMemcpyHostToDevice, st->stream));
+    std::string err;
+    rc = launch(st->in.ptr, st->out.ptr, st->stream, &err);
+    if (rc) {
+        (void)hipStreamSynchronize(st->stream);
+        return fail(rc, err);
+    }
+    HIP_TRY(hipMemcpyAsync(y, st->out.ptr, out_bytes, hipMemcpyDeviceToHost, st->stream));
+    HIP_TRY(hipStreamSynchronize(st->stream));
+    return FIR_OK;
+}
+
+bool mul_ok(int64_t a, int64_t b, int64_t* out) {
+    if (a < 0 || b < 0) return false;
+    if (a != 0 && b > INT64_MAX / a) return false;
+    *out = a * b;
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fir_abi_version(void) { return FIR_HIP_ABI_VERSION; }
+
+const char* fir_last_error(void) { return g_err.c_str(); }
+
+int fir_device_count(int* count) {
+    if (!count) return fail(FIR_EINVAL, "count must not be NULL");
+    *count = 0;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) return fail(FIR_ENODEV, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    *count = n;
+    return FIR_OK;
+}
+
+int fir1d_fixed_rows(const void* x, int in_dtype, int64_t rows, int64_t width, int channels, const int32_t* hq,
+                     int taps, int frac_bits, int acc_bits, int out_stage, void* y, int device) {
+    try {
+        int64_t n = 0, rw = 0;
+        if (channels < 1 || !mul_ok(rows, width, &rw) || !mul_ok(rw, channels, &n))
+            return fail(FIR_EINVAL, "invalid rows/width/channels");
+        if (n == 0) {
+            std::string err;
+            // still validate the scalar arguments
+            int rc = fir::launch_fir1d_rows(nullptr, in_dtype, 0, 0, channels, hq, taps, frac_bits, acc_bits,
+                                            out_stage, nullptr, nullptr, &err);
+            return rc ? fail(rc, err) : FIR_OK;
+        }
+        if (!x || !y) return fail(FIR_EINVAL, "x and y must not be NULL");
+        return run_host(device, x, (size_t)n * in_size(in_dtype), y, (size_t)n * out_size(out_stage),
+                        [&](void* dx, void* dy, hipStream_t s, std::string* err) {
+                            return fir::launch_fir1d_rows(dx, in_dtype, rows, width, channels, hq, taps, frac_bits,
+                                                          acc_bits, out_stage, dy, s, err);
+                        });
+    } catch (const std::exception& ex) {
+        return fail(FIR_EHIP, std::string("internal error: ") + ex.what());
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int fir1d_fixed_rows_dev(const void* x_dev, int in_dtype, int64_t rows, int64_t width, int channels,
+                         const int32_t* hq, int taps, int frac_bits, int acc_bits, int out_stage, void* y_dev,
+                         void* stream) {
+    try {
+        std::string err;
+        int rc = fir::launch_fir1d_rows(x_dev, in_dtype, rows, width, channels, hq, taps, frac_bits, acc_bits,
+                                        out_stage, y_dev, (hipStream_t)stream, &err);
+        return rc ? fail(rc, err) : FIR_OK;
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int fir1d_fixed_edges_dev(const void* x_dev, int in_dtype, int64_t n, int channels, const int32_t* hq, int taps,
+                          int frac_bits, int acc_bits, int out_stage, const void* halo_left_dev,
+                          const void* halo_right_dev, void* y_dev, void* stream) {
+    try {
+        std::string err;
+        int rc = fir::launch_fir1d_edges(x_dev, in_dtype, n, channels, hq, taps, frac_bits, acc_bits, out_stage,
+                                         halo_left_dev, halo_right_dev, y_dev, (hipStream_t)stream, &err);
+        return rc ? fail(rc, err) : FIR_OK;
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int fir2d_fixed(const uint8_t* x, int64_t height, int64_t width, const int32_t* hq, int tap_rows, int tap_cols,
+                int frac_bits, int acc_bits, int out_stage, void* y, int device) {
+    try {
+        int64_t n = 0;
+        if (!mul_ok(height, width, &n)) return fail(FIR_EINVAL, "invalid height/width");
+        if (n == 0) {
+            std::string err;
+            int rc = fir::launch_fir2d(nullptr, 0, 0, hq, tap_rows, tap_cols, frac_bits, acc_bits, out_stage,
+                                       nullptr, nullptr, &err);
+            return rc ? fail(rc, err) : FIR_OK;
+        }
+        if (!x || !y) return fail(FIR_EINVAL, "x and y must not be NULL");
+        return run_host(device, x, (size_t)n, y, (size_t)n * out_size(out_stage),
+                        [&](void* dx, void* dy, hipStream_t s, std::string* err) {
+                            return fir::launch_fir2d((const uint8_t*)dx, height, width, hq, tap_rows, tap_cols,
+                                                     frac_bits, acc_bits, out_stage, dy, s, err);
+                        });
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int fir2d_fixed_dev(const uint8_t* x_dev, int64_t height, int64_t width, const int32_t* hq, int tap_rows,
+                    int tap_cols, int frac_bits, int acc_bits, int out_stage, void* y_dev, void* stream) {
+    try {
+        std::string err;
+        int rc = fir::launch_fir2d(x_dev, height, width, hq, tap_rows, tap_cols, frac_bits, acc_bits, out_stage,
+                                   y_dev, (hipStream_t)stream, &err);
+        return rc ? fail(rc, err) : FIR_OK;
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int fir1d_ideal_rows(const uint8_t* x, int64_t rows, int64_t width, const double* h, int taps, double* y,
+                     int device) {
+    try {
+        int64_t n = 0;
+        if (!mul_ok(rows, width, &n)) return fail(FIR_EINVAL, "invalid rows/width");
+        if (n == 0) {
+            std::string err;
+            int rc = fir::launch_fir1d_ideal(nullptr, 0, 0, h, taps, nullptr, nullptr, &err);
+            return rc ? fail(rc, err) : FIR_OK;
+        }
+        if (!x || !y) return fail(FIR_EINVAL, "x and y must not be NULL");
+        return run_host(device, x, (size_t)n, y, (size_t)n * 8, [&](void* dx, void* dy, hipStream_t s, std::string* err) {
+            return fir::launch_fir1d_ideal((const uint8_t*)dx, rows, width, h, taps, (double*)dy, s, err);
+        });
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int fir1d_ideal_rows_dev(const uint8_t* x_dev, int64_t rows, int64_t width, const double* h, int taps,
+                         double* y_dev, void* stream) {
+    try {
+        std::string err;
+        int rc = fir::launch_fir1d_ideal(x_dev, rows, width, h, taps, y_dev, (hipStream_t)stream, &err);
+        return rc ? fail(rc, err) : FIR_OK;
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,407 @@
+// fir1d.hip — gfx950 kernels for the row-wise 1-D fixed-point FIR.
+//
+// Arithmetic restated from fir_1d/model/python/fir_1d_fixed_ref.py:95-126 (reference root):
+//   acc = sum_k hq[k] * x[n - k + L/2] (zero outside the row), wrapped to acc_bits,
+//   q = (acc + 2^(f-1)) >> f, then saturated to u8 or kept as int32.
+//
+// Two kernels:
+//  * fir1d_reg_kernel  — the hot path.  One thread owns one 16-byte vector of samples
+//    (16 u8 or 8 int16).  The (L-1)-sample halo comes from the neighbouring lanes'
+//    registers through DPP wave shifts (v_mov_b32_dpp wave_shr:1 / wave_shl:1), so each
+//    HBM byte is loaded once; only lanes 0 and 63 of a wave issue one extra 16-byte load
+//    for the neighbouring wave's edge vector (served by L2).  32-bit wrap-around MACs on
+//    v_mul_i32_i24 (taps checked to fit 24 bits on the host), overflow-free rounding,
+//    16-byte stores.  Row edges (images) are handled by a per-thread column test; threads
+//    whose window lies inside one row take the unmasked path.
+//  * fir1d_generic_kernel — every other configuration (any tap count up to FIR_MAX_TAPS,
+//    any acc_bits / frac_bits, unaligned buffers, narrow rows, halo segments): a
+//    workgroup stages an LDS sliding-window tile of 1024 outputs + (L-1)*channels halo
+//    samples, then every thread forms its outputs from LDS with an exact int64 sum.
+#include <algorithm>
+#include <string>
+
+#include "fir_common.h"
+#include "fir_launch.h"
+
+namespace fir {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+template <int L>
+struct TapsN {
+    int32_t h[L];
+};
+
+struct RowGeom {
+    int64_t total;      // samples in the buffer (rows * width * channels)
+    uint32_t rowlen32;  // width * channels, valid when multi_row
+    int multi_row;      // rows > 1 (then total < 2^32 is guaranteed by the host)
+};
+
+// Load vector `v` (VEC samples) into 4 dwords: full 16-byte load when wholly in range,
+// element-wise with zero fill at the ragged end, zeros past the end.
+template <typename InT, bool NT>
+__device__ __forceinline__ void load_vec(const InT* __restrict__ x, int64_t v, int64_t nvec, int64_t total,
+                                         uint32_t (&d)[4]) {
+    constexpr int EPD = InTraits<InT>::kPerDword;
+    constexpr int VEC = 4 * EPD;
+    if (v < nvec) {
+        const u32x4* p = reinterpret_cast<const u32x4*>(x + v * VEC);
+        u32x4 q = NT ? __builtin_nontemporal_load(p) : *p;
+        d[0] = q.x;
+        d[1] = q.y;
+        d[2] = q.z;
+        d[3] = q.w;
+    } else {
+        d[0] = d[1] = d[2] = d[3] = 0;
+        const int64_t base = v * VEC;
+        if (v >= 0 && base < total) {
+            const int n = (int)min((int64_t)VEC, total - base);
+            for (int j = 0; j < n; ++j) {
+                const uint32_t e = (uint32_t)x[base + j] & (EPD == 4 ? 0xFFu : 0xFFFFu);
+                d[j / EPD] |= e << ((32 / EPD) * (j % EPD));
+            }
+        }
+    }
+}
+
+template <typename InT, int STAGE, int L, int CH, bool NT>
+__global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict__ x,
+                                                           typename OutTraits<STAGE>::T* __restrict__ y,
+                                                           RowGeom g, TapsN<L> taps, int shl, int frac) {
+    using IT = InTraits<InT>;
+    constexpr int EPD = IT::kPerDword;
+    constexpr int VEC = 4 * EPD;
+    constexpr int C = L / 2;
+    constexpr int HLE = (L - 1 - C) * CH;  // samples needed left of the vector
+    constexpr int HRE = C * CH;            // samples needed right of the vector
+    static_assert(HLE <= VEC && HRE <= VEC, "halo must fit in one neighbouring vector");
+    constexpr int NDL = (HLE + EPD - 1) / EPD;  // dwords shifted in from lane-1
+    constexpr int NDR = (HRE + EPD - 1) / EPD;  // dwords shifted in from lane+1
+
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t total = g.total;
+    const int64_t nvec = total / VEC;
+    const int64_t g0 = v * VEC;
+
+    uint32_t own[4], hv[4] = {0, 0, 0, 0};
+    load_vec<InT, NT>(x, v, nvec, total, own);
+    // The wave's edge lanes fetch the vectors just outside the wave (L2 hits in steady state).
+    if (lane == 0) {
+        if (NDL > 0 && v > 0) load_vec<InT, false>(x, v - 1, nvec, total, hv);
+    } else if (lane == kWave - 1) {
+        if (NDR > 0) load_vec<InT, false>(x, v + 1, nvec, total, hv);
+    }
+
+    // Window w[0 .. HLE+VEC+HRE): left halo | own samples | right halo.
+    int32_t w[HLE + VEC + HRE];
+    if constexpr (NDL > 0) {
+        uint32_t prev[4];
+#pragma unroll
+        for (int q = 4 - NDL; q < 4; ++q) prev[q] = from_prev_lane(hv[q], own[q]);
+#pragma unroll
+        for (int i = 0; i < HLE; ++i) {
+            constexpr int base = VEC - HLE;
+            w[i] = IT::get(prev[(base + i) / EPD], (base + i) % EPD);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) w[HLE + j] = IT::get(own[j / EPD], j % EPD);
+    if constexpr (NDR > 0) {
+        uint32_t next[4];
+#pragma unroll
+        for (int q = 0; q < NDR; ++q) next[q] = from_next_lane(hv[q], own[q]);
+#pragma unroll
+        for (int i = 0; i < HRE; ++i) w[HLE + VEC + i] = IT::get(next[i / EPD], i % EPD);
+    }
+
+    if (g0 >= total) return;  // after the cross-lane exchange: idle tail lanes just leave
+
+    int64_t col0, rowlen;
+    if (g.multi_row) {
+        rowlen = g.rowlen32;
+        col0 = (uint32_t)g0 % g.rowlen32;
+    } else {
+        rowlen = total;
+        col0 = g0;
+    }
+    const bool interior = col0 >= HLE && col0 + VEC + HRE <= rowlen;
+
+    int32_t q[VEC];
+    if (interior) {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int k = 0; k < L; ++k) acc += (uint32_t)__mul24(taps.h[k], w[HLE + j + (C - k) * CH]);
+            q[j] = round32(acc, shl, frac);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            int64_t cj = col0 + j;
+            if (cj >= rowlen) cj -= rowlen;  // the vector crossed into the next row
+            uint32_t acc = 0;
+#pragma unroll
+            for (int k = 0; k < L; ++k) {
+                const int64_t p = cj + (C - k) * CH;
+                const uint32_t t = (uint32_t)__mul24(taps.h[k], w[HLE + j + (C - k) * CH]);
+                acc += (p >= 0 && p < rowlen) ? t : 0u;
+            }
+            q[j] = round32(acc, shl, frac);
+        }
+    }
+
+    if (v < nvec) {
+        if constexpr (STAGE == FIR_OUT_U8_SAT) {
+            uint32_t o[VEC / 4];
+#pragma unroll
+            for (int i = 0; i < VEC / 4; ++i) {
+                o[i] = (uint32_t)stage_out32<STAGE>(q[4 * i]) | ((uint32_t)stage_out32<STAGE>(q[4 * i + 1]) << 8) |
+                       ((uint32_t)stage_out32<STAGE>(q[4 * i + 2]) << 16) |
+                       ((uint32_t)stage_out32<STAGE>(q[4 * i + 3]) << 24);
+            }
+            if constexpr (VEC == 16) {
+                u32x4 val = {o[0], o[1], o[2], o[3]};
+                u32x4* p = reinterpret_cast<u32x4*>(y + g0);
+                if (NT) __builtin_nontemporal_store(val, p); else *p = val;
+            } else {
+                u32x2 val = {o[0], o[1]};
+                u32x2* p = reinterpret_cast<u32x2*>(y + g0);
+                if (NT) __builtin_nontemporal_store(val, p); else *p = val;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < VEC / 4; ++i) {
+                u32x4 val = {(uint32_t)q[4 * i], (uint32_t)q[4 * i + 1], (uint32_t)q[4 * i + 2], (uint32_t)q[4 * i + 3]};
+                u32x4* p = reinterpret_cast<u32x4*>(y + g0) + i;
+                if (NT) __builtin_nontemporal_store(val, p); else *p = val;
+            }
+        }
+    } else {
+        const int n = (int)min((int64_t)VEC, total - g0);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j)
+            if (j < n) y[g0 + j] = stage_out32<STAGE>(q[j]);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Generic LDS sliding-window kernel.
+constexpr int kGenTile = 1024;
+constexpr int kGenMaxHalo = 1024;  // (L-1) * channels
+
+struct TapsG {
+    int32_t h[FIR_MAX_TAPS];
+};
+
+template <typename InT, int STAGE>
+__global__ __launch_bounds__(kBlock) void fir1d_generic_kernel(const InT* __restrict__ x,
+                                                               typename OutTraits<STAGE>::T* __restrict__ y,
+                                                               int64_t start, int64_t end, int64_t total,
+                                                               int64_t rowlen, int multi_row, int ch,
+                                                               const InT* __restrict__ halo_l,
+                                                               const InT* __restrict__ halo_r, TapsG taps, int L,
+                                                               int frac, int acc_bits) {
+    __shared__ int32_t s_taps[FIR_MAX_TAPS];
+    __shared__ int32_t s_x[kGenTile + kGenMaxHalo];
+    const int c = L / 2;
+    const int HLE = (L - 1 - c) * ch;
+    const int HRE = c * ch;
+    const int64_t t0 = start + (int64_t)blockIdx.x * kGenTile;
+    const int span = kGenTile + HLE + HRE;
+
+    for (int k = threadIdx.x; k < L; k += kBlock) s_taps[k] = taps.h[k];
+    for (int i = threadIdx.x; i < span; i += kBlock) {
+        const int64_t gi = t0 - HLE + i;
+        int32_t val = 0;
+        if (gi >= 0 && gi < total) {
+            val = (int32_t)x[gi];
+        } else if (gi < 0) {
+            if (halo_l && gi >= -HLE) val = (int32_t)halo_l[HLE + gi];
+        } else if (halo_r && gi < total + HRE) {
+            val = (int32_t)halo_r[gi - total];
+        }
+        s_x[i] = val;
+    }
+    __syncthreads();
+
+    for (int i = threadIdx.x; i < kGenTile; i += kBlock) {
+        const int64_t gi = t0 + i;
+        if (gi >= end) break;
+        const int64_t col = multi_row ? gi % rowlen : 0;
+        int64_t acc = 0;
+        for (int k = 0; k < L; ++k) {
+            const int d = (c - k) * ch;
+            int32_t xv = s_x[HLE + i + d];
+            if (multi_row && (col + d < 0 || col + d >= rowlen)) xv = 0;
+            acc += (int64_t)s_taps[k] * xv;
+        }
+        y[gi] = stage_out<STAGE>(round64(acc, frac, acc_bits));
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Host-side launchers.
+
+static bool g_nt_enabled = [] {
+    const char* e = getenv("FIR_HIP_NT");
+    return e == nullptr || e[0] != '0';
+}();
+
+template <typename InT, int STAGE, int L, int CH>
+static hipError_t launch_reg(const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
+                             const int32_t* hq, int frac, int acc_bits, hipStream_t stream) {
+    using OutT = typename OutTraits<STAGE>::T;
+    constexpr int VEC = 4 * InTraits<InT>::kPerDword;
+    RowGeom g;
+    g.total = total;
+    g.rowlen32 = (uint32_t)(rows > 1 ? rowlen : 0);
+    g.multi_row = rows > 1;
+    TapsN<L> t;
+    for (int k = 0; k < L; ++k) t.h[k] = hq[k];
+    const int64_t threads = (total + VEC - 1) / VEC;
+    const int64_t blocks = (threads + kBlock - 1) / kBlock;
+    if (g_nt_enabled) {
+        hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, true>), dim3((unsigned)blocks), dim3(kBlock), 0,
+                           stream, (const InT*)x, (OutT*)y, g, t, 32 - acc_bits, frac);
+    } else {
+        hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, false>), dim3((unsigned)blocks), dim3(kBlock), 0,
+                           stream, (const InT*)x, (OutT*)y, g, t, 32 - acc_bits, frac);
+    }
+    return hipGetLastError();
+}
+
+template <typename InT, int STAGE, int CH>
+static hipError_t launch_reg_taps(int L, const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
+                                  const int32_t* hq, int frac, int acc_bits, hipStream_t s) {
+    switch (L) {
+        case 1: return launch_reg<InT, STAGE, 1, CH>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 2: return launch_reg<InT, STAGE, 2, CH>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 3: return launch_reg<InT, STAGE, 3, CH>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 4: return launch_reg<InT, STAGE, 4, CH>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 5: return launch_reg<InT, STAGE, 5, CH>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 6: return launch_reg<InT, STAGE, 6, CH>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 7: return launch_reg<InT, STAGE, 7, CH>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 8: return launch_reg<InT, STAGE, 8, CH>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 9: return launch_reg<InT, STAGE, 9, CH>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <typename InT, int STAGE>
+static hipError_t launch_generic(const void* x, void* y, int64_t start, int64_t end, int64_t total,
+                                 int64_t rowlen, bool multi_row, int ch, const void* hl, const void* hr,
+                                 const int32_t* hq, int L, int frac, int acc_bits, hipStream_t stream) {
+    using OutT = typename OutTraits<STAGE>::T;
+    if (end <= start) return hipSuccess;
+    TapsG t;
+    for (int k = 0; k < L; ++k) t.h[k] = hq[k];
+    for (int k = L; k < FIR_MAX_TAPS; ++k) t.h[k] = 0;
+    const int64_t blocks = (end - start + kGenTile - 1) / kGenTile;
+    hipLaunchKernelGGL((fir1d_generic_kernel<InT, STAGE>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
+                       (const InT*)x, (OutT*)y, start, end, total, rowlen, multi_row ? 1 : 0, ch, (const InT*)hl,
+                       (const InT*)hr, t, L, frac, acc_bits);
+    return hipGetLastError();
+}
+
+static hipError_t dispatch_generic(int in_dtype, int stage, const void* x, void* y, int64_t start, int64_t end,
+                                   int64_t total, int64_t rowlen, bool multi_row, int ch, const void* hl,
+                                   const void* hr, const int32_t* hq, int L, int frac, int acc_bits,
+                                   hipStream_t s) {
+    if (in_dtype == FIR_IN_U8) {
+        return stage == FIR_OUT_U8_SAT
+                   ? launch_generic<uint8_t, FIR_OUT_U8_SAT>(x, y, start, end, total, rowlen, multi_row, ch, hl,
+                                                             hr, hq, L, frac, acc_bits, s)
+                   : launch_generic<uint8_t, FIR_OUT_I32>(x, y, start, end, total, rowlen, multi_row, ch, hl, hr,
+                                                          hq, L, frac, acc_bits, s);
+    }
+    return stage == FIR_OUT_U8_SAT
+               ? launch_generic<int16_t, FIR_OUT_U8_SAT>(x, y, start, end, total, rowlen, multi_row, ch, hl, hr,
+                                                         hq, L, frac, acc_bits, s)
+               : launch_generic<int16_t, FIR_OUT_I32>(x, y, start, end, total, rowlen, multi_row, ch, hl, hr, hq,
+                                                      L, frac, acc_bits, s);
+}
+
+static int check_common(int in_dtype, int64_t rows, int64_t width, int ch, const int32_t* hq, int L, int frac,
+                        int acc_bits, int stage, std::string* err) {
+    if (in_dtype != FIR_IN_U8 && in_dtype != FIR_IN_I16) return *err = "in_dtype must be FIR_IN_U8 or FIR_IN_I16", FIR_EINVAL;
+    if (stage != FIR_OUT_U8_SAT && stage != FIR_OUT_I32) return *err = "out_stage must be FIR_OUT_U8_SAT or FIR_OUT_I32", FIR_EINVAL;
+    if (rows < 0 || width < 0) return *err = "rows and width must be >= 0", FIR_EINVAL;
+    if (ch < 1) return *err = "channels must be >= 1", FIR_EINVAL;
+    if (!hq) return *err = "hq must not be NULL", FIR_EINVAL;
+    if (L < 1 || L > FIR_MAX_TAPS) return *err = "taps must be in [1, " + std::to_string(FIR_MAX_TAPS) + "]", FIR_EINVAL;
+    if ((int64_t)(L - 1) * ch > kGenMaxHalo) return *err = "(taps-1)*channels exceeds 1024", FIR_EINVAL;
+    if (frac < 1 || acc_bits < 1) return *err = "frac_bits and acc_bits must be >= 1", FIR_EINVAL;
+    return FIR_OK;
+}
+
+int launch_fir1d_rows(const void* x, int in_dtype, int64_t rows, int64_t width, int ch, const int32_t* hq, int L,
+                      int frac, int acc_bits, int stage, void* y, hipStream_t stream, std::string* err) {
+    int rc = check_common(in_dtype, rows, width, ch, hq, L, frac, acc_bits, stage, err);
+    if (rc) return rc;
+    const int64_t rowlen = width * ch;
+    const int64_t total = rows * rowlen;
+    if (total == 0) return FIR_OK;
+    if (!x || !y) return *err = "x and y must not be NULL", FIR_EINVAL;
+
+    const int vec = in_dtype == FIR_IN_U8 ? 16 : 8;
+    const int c = L / 2;
+    bool taps24 = true;
+    for (int k = 0; k < L; ++k) taps24 &= (hq[k] >= -(1 << 23) && hq[k] < (1 << 23));
+    const bool fast = L <= 9 && (ch == 1 || (ch == 2 && in_dtype == FIR_IN_I16)) && acc_bits <= 32 && frac <= 31 &&
+                      taps24 && ((uintptr_t)x % 16 == 0) && ((uintptr_t)y % 16 == 0) &&
+                      (rows == 1 || (rowlen >= vec + (L - 1) * ch && total < ((int64_t)1 << 32)));
+    (void)c;
+    hipError_t e;
+    if (fast) {
+        if (in_dtype == FIR_IN_U8) {
+            e = stage == FIR_OUT_U8_SAT
+                    ? launch_reg_taps<uint8_t, FIR_OUT_U8_SAT, 1>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream)
+                    : launch_reg_taps<uint8_t, FIR_OUT_I32, 1>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
+        } else if (ch == 1) {
+            e = stage == FIR_OUT_U8_SAT
+                    ? launch_reg_taps<int16_t, FIR_OUT_U8_SAT, 1>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream)
+                    : launch_reg_taps<int16_t, FIR_OUT_I32, 1>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
+        } else {
+            e = stage == FIR_OUT_U8_SAT
+                    ? launch_reg_taps<int16_t, FIR_OUT_U8_SAT, 2>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream)
+                    : launch_reg_taps<int16_t, FIR_OUT_I32, 2>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
+        }
+    } else {
+        e = dispatch_generic(in_dtype, stage, x, y, 0, total, total, rowlen, rows > 1, ch, nullptr, nullptr, hq, L,
+                             frac, acc_bits, stream);
+    }
+    if (e != hipSuccess) return *err = std::string("fir1d launch failed: ") + hipGetErrorString(e), FIR_EHIP;
+    return FIR_OK;
+}
+
+int launch_fir1d_edges(const void* x, int in_dtype, int64_t n, int ch, const int32_t* hq, int L, int frac,
+                       int acc_bits, int stage, const void* hl, const void* hr, void* y, hipStream_t stream,
+                       std::string* err) {
+    int rc = check_common(in_dtype, 1, n, ch, hq, L, frac, acc_bits, stage, err);
+    if (rc) return rc;
+    const int64_t total = n * ch;
+    if (total == 0) return FIR_OK;
+    if (!x || !y) return *err = "x and y must not be NULL", FIR_EINVAL;
+    const int c = L / 2;
+    const int64_t hle = (int64_t)(L - 1 - c) * ch, hre = (int64_t)c * ch;
+    hipError_t e = hipSuccess;
+    if (total <= hle + hre) {
+        e = dispatch_generic(in_dtype, stage, x, y, 0, total, total, total, false, ch, hl, hr, hq, L, frac, acc_bits,
+                             stream);
+    } else {
+        if (hle > 0)
+            e = dispatch_generic(in_dtype, stage, x, y, 0, hle, total, total, false, ch, hl, hr, hq, L, frac,
+                                 acc_bits, stream);
+        if (e == hipSuccess && hre > 0)
+            e = dispatch_generic(in_dtype, stage, x, y, total - hre, total, total, total, false, ch, hl, hr, hq, L,
+                                 frac, acc_bits, stream);
+    }
+    if (e != hipSuccess) return *err = std::string("fir1d edge launch failed: ") + hipGetErrorString(e), FIR_EHIP;
+    return FIR_OK;
+}
+
+}  // namespace fir

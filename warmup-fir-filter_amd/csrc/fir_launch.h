@@ -1,0 +1,28 @@
+// fir_launch.h — internal launch functions (C++), wrapped by the C ABI in capi.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+namespace fir {
+
+// Enqueue the row-wise 1-D fixed FIR on `stream`; device pointers.  Returns fir_status.
+int launch_fir1d_rows(const void* x, int in_dtype, int64_t rows, int64_t width, int ch, const int32_t* hq, int L,
+                      int frac, int acc_bits, int stage, void* y, hipStream_t stream, std::string* err);
+
+// Recompute the halo-dependent edge outputs of a single-row segment.
+int launch_fir1d_edges(const void* x, int in_dtype, int64_t n, int ch, const int32_t* hq, int L, int frac,
+                       int acc_bits, int stage, const void* halo_left, const void* halo_right, void* y,
+                       hipStream_t stream, std::string* err);
+
+// 2-D fixed FIR over a uint8 frame.
+int launch_fir2d(const uint8_t* x, int64_t height, int64_t width, const int32_t* hq, int tap_rows, int tap_cols,
+                 int frac, int acc_bits, int stage, void* y, hipStream_t stream, std::string* err);
+
+// float64 ideal model over uint8 rows.
+int launch_fir1d_ideal(const uint8_t* x, int64_t rows, int64_t width, const double* h, int L, double* y,
+                       hipStream_t stream, std::string* err);
+
+}  // namespace fir

@@ -1,0 +1,77 @@
+// ideal.hip — float64 "ideal" model.
+//
+// Restates fir_1d/model/python/fir_1d_ref.py:43-65 per row (as driven by
+// fir_1d/sim/vector/gen_ideal_output.py:37-50): acc = 0.0; for k in order:
+// acc += h[k] * x[n - k + L/2] over in-row samples; no output clamp.  Bit-exactness
+// needs the reference's rounding order: every product and every sum is rounded on its
+// own (__dmul_rn / __dadd_rn, and the library is built with -ffp-contract=off), taps
+// are summed in k order, and out-of-row terms contribute +0.0 (identical to skipping
+// them: the running sum is never -0.0 because samples are >= 0).
+//
+// Layout: a workgroup owns 1024 consecutive outputs of the flat rows x width buffer;
+// the u8 samples of that tile plus the (L-1)-sample halo are staged once in LDS, and
+// each thread writes 4 outputs (8-byte coalesced stores; the f64 output is 8 of the
+// 9 bytes per sample of HBM traffic).
+#include <string>
+
+#include "fir_common.h"
+#include "fir_launch.h"
+
+namespace fir {
+
+constexpr int kIdealTile = 1024;
+
+struct TapsF64 {
+    double h[FIR_MAX_TAPS];
+};
+
+__global__ __launch_bounds__(kBlock) void fir1d_ideal_kernel(const uint8_t* __restrict__ x, double* __restrict__ y,
+                                                             int64_t total, int64_t rowlen, int multi_row,
+                                                             TapsF64 taps, int L) {
+    __shared__ double s_h[FIR_MAX_TAPS];
+    __shared__ int32_t s_x[kIdealTile + FIR_MAX_TAPS];
+    const int c = L / 2;
+    const int HLE = L - 1 - c, HRE = c;
+    const int64_t t0 = (int64_t)blockIdx.x * kIdealTile;
+    const int span = kIdealTile + HLE + HRE;
+    for (int k = threadIdx.x; k < L; k += kBlock) s_h[k] = taps.h[k];
+    for (int i = threadIdx.x; i < span; i += kBlock) {
+        const int64_t gi = t0 - HLE + i;
+        s_x[i] = (gi >= 0 && gi < total) ? (int32_t)x[gi] : 0;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kIdealTile; i += kBlock) {
+        const int64_t gi = t0 + i;
+        if (gi >= total) break;
+        const int64_t col = multi_row ? gi % rowlen : gi;
+        const int64_t rl = multi_row ? rowlen : total;
+        double acc = 0.0;
+        for (int k = 0; k < L; ++k) {
+            const int d = c - k;
+            const bool ok = col + d >= 0 && col + d < rl;
+            const double xv = ok ? (double)s_x[HLE + i + d] : 0.0;
+            acc = __dadd_rn(acc, __dmul_rn(s_h[k], xv));
+        }
+        y[gi] = acc;
+    }
+}
+
+int launch_fir1d_ideal(const uint8_t* x, int64_t rows, int64_t width, const double* h, int L, double* y,
+                       hipStream_t stream, std::string* err) {
+    if (rows < 0 || width < 0) return *err = "rows and width must be >= 0", FIR_EINVAL;
+    if (!h) return *err = "h must not be NULL", FIR_EINVAL;
+    if (L < 1 || L > FIR_MAX_TAPS) return *err = "taps must be in [1, 256]", FIR_EINVAL;
+    const int64_t total = rows * width;
+    if (total == 0) return FIR_OK;
+    if (!x || !y) return *err = "x and y must not be NULL", FIR_EINVAL;
+    TapsF64 t;
+    for (int k = 0; k < FIR_MAX_TAPS; ++k) t.h[k] = k < L ? h[k] : 0.0;
+    const int64_t blocks = (total + kIdealTile - 1) / kIdealTile;
+    hipLaunchKernelGGL(fir1d_ideal_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, x, y, total, width,
+                       rows > 1 ? 1 : 0, t, L);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return *err = std::string("ideal launch failed: ") + hipGetErrorString(e), FIR_EHIP;
+    return FIR_OK;
+}
+
+}  // namespace fir

@@ -1,0 +1,136 @@
+"""Fixed-point output vectors (.npy) for every input image x every coefficient set.
+
+Mirror of the reference stage ``fir_1d/sim/vector/gen_fixed_output.py``: same public
+entry points, keyword arguments, file naming (``{case}__{coeff}_fixed_{3,5}tap_y_u8.npy``
+under ``output_dir/fixed_{3,5}tap``), skip-if-exists / ``overwrite`` behaviour, return
+value (number of files generated) and CLI flags.  The difference is the row driver:
+the reference calls the golden model once per image row (:34-60); here the whole
+image goes to the GPU in one ``fir1d_fixed_rows`` launch (rows are independent and
+zero padding resets at each row edge inside the kernel).
+"""
+from __future__ import annotations
+
+import argparse
+from pathlib import Path
+from time import perf_counter
+
+import numpy as np
+
+import fir_hip
+from fir_1d.model.python.fir_1d_fixed_ref import device_bits, quantize_fixed_taps
+from fir_1d.sim.vector.h_coeff import h_coeff_3tap_map, h_coeff_5tap_map
+
+THIS_FILE = Path(__file__).resolve()
+DEFAULT_INPUT_DIR = THIS_FILE.parent / "input"
+DEFAULT_OUTPUT_DIR = THIS_FILE.parent / "output"
+_IN_SUFFIX = "_x_u8.npy"
+
+
+def _iter_input_npy_files(input_dir: Path) -> list[Path]:
+    return sorted((p for p in input_dir.glob("*.npy") if p.name.endswith(_IN_SUFFIX)),
+                  key=lambda p: p.name.lower())
+
+
+def _load_input_image_u8(path: Path) -> np.ndarray:
+    x = np.load(path)
+    if x.ndim != 2:
+        raise ValueError(f"{path.name}: expected 2D array, got shape={x.shape}")
+    return x if x.dtype == np.uint8 else x.astype(np.uint8)
+
+
+def _case_stem_from_input(path: Path) -> str:
+    return path.name[: -len(_IN_SUFFIX)] if path.name.endswith(_IN_SUFFIX) else path.stem
+
+
+def _run_fixed_rowwise(x_u8: np.ndarray, h: list[float], *, frac_bits: int, acc_bits: int,
+                       coeff_bits: int) -> np.ndarray:
+    """Every row of an H x W uint8 image through the fixed model: one GPU launch."""
+    height, width = x_u8.shape
+    if height == 0:
+        return np.zeros((0, width), dtype=np.uint8)
+    hq = quantize_fixed_taps(h, frac_bits, acc_bits, coeff_bits)
+    f, a = device_bits(frac_bits, acc_bits)
+    y = fir_hip.fir1d_fixed_rows(np.ascontiguousarray(x_u8, dtype=np.uint8), hq, f, a, fir_hip.OUT_U8_SAT)
+    if y.shape != (height, width):
+        raise ValueError(f"Output shape mismatch: expected {(height, width)}, got {y.shape}.")
+    return y
+
+
+def _generate_fixed_outputs_for_tap_map(*, input_dir: Path, out_dir: Path, coeff_map: dict[str, list[float]],
+                                        tap_label: str, frac_bits: int, acc_bits: int, coeff_bits: int,
+                                        overwrite: bool = False) -> int:
+    inputs = _iter_input_npy_files(input_dir)
+    if not inputs:
+        raise FileNotFoundError(f"No input .npy files found in {input_dir}")
+    out_dir.mkdir(parents=True, exist_ok=True)
+    generated = 0
+    for in_path in inputs:
+        x_u8 = _load_input_image_u8(in_path)
+        stem = _case_stem_from_input(in_path)
+        for coeff_name, h in coeff_map.items():
+            out_path = out_dir / f"{stem}__{coeff_name}_fixed_{tap_label}_y_u8.npy"
+            if out_path.exists() and not overwrite:
+                continue
+            np.save(out_path, _run_fixed_rowwise(x_u8, h, frac_bits=frac_bits, acc_bits=acc_bits,
+                                                 coeff_bits=coeff_bits))
+            generated += 1
+    return generated
+
+
+def generate_fixed_3tap_output_vector(input_dir: Path = DEFAULT_INPUT_DIR, output_dir: Path = DEFAULT_OUTPUT_DIR,
+                                      *, frac_bits: int = 12, acc_bits: int = 32, coeff_bits: int = 16,
+                                      overwrite: bool = False) -> int:
+    return _generate_fixed_outputs_for_tap_map(
+        input_dir=Path(input_dir).resolve(), out_dir=Path(output_dir).resolve() / "fixed_3tap",
+        coeff_map=h_coeff_3tap_map, tap_label="3tap", frac_bits=frac_bits, acc_bits=acc_bits,
+        coeff_bits=coeff_bits, overwrite=overwrite)
+
+
+def generate_fixed_5tap_output_vector(input_dir: Path = DEFAULT_INPUT_DIR, output_dir: Path = DEFAULT_OUTPUT_DIR,
+                                      *, frac_bits: int = 12, acc_bits: int = 32, coeff_bits: int = 16,
+                                      overwrite: bool = False) -> int:
+    return _generate_fixed_outputs_for_tap_map(
+        input_dir=Path(input_dir).resolve(), out_dir=Path(output_dir).resolve() / "fixed_5tap",
+        coeff_map=h_coeff_5tap_map, tap_label="5tap", frac_bits=frac_bits, acc_bits=acc_bits,
+        coeff_bits=coeff_bits, overwrite=overwrite)
+
+
+def _build_argparser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(description="Generate FIR 1D fixed output vectors for 3tap/5tap filters (GPU).")
+    ap.add_argument("--input-dir", type=Path, default=DEFAULT_INPUT_DIR)
+    ap.add_argument("--output-dir", type=Path, default=DEFAULT_OUTPUT_DIR)
+    ap.add_argument("--tap", choices=("all", "3", "5"), default="all")
+    ap.add_argument("--frac-bits", type=int, default=12)
+    ap.add_argument("--acc-bits", type=int, default=32)
+    ap.add_argument("--coeff-bits", type=int, default=16)
+    ap.add_argument("--overwrite", action="store_true")
+    return ap
+
+
+def main(argv=None) -> int:
+    t0 = perf_counter()
+    args = _build_argparser().parse_args(argv)
+    in_dir, out_dir = args.input_dir.resolve(), args.output_dir.resolve()
+    counts, expected = {"fixed_3tap": 0, "fixed_5tap": 0}, 0
+    try:
+        kw = dict(input_dir=in_dir, output_dir=out_dir, frac_bits=args.frac_bits, acc_bits=args.acc_bits,
+                  coeff_bits=args.coeff_bits, overwrite=args.overwrite)
+        if args.tap in ("all", "3"):
+            expected += len(_iter_input_npy_files(in_dir)) * len(h_coeff_3tap_map)
+            counts["fixed_3tap"] = generate_fixed_3tap_output_vector(**kw)
+        if args.tap in ("all", "5"):
+            expected += len(_iter_input_npy_files(in_dir)) * len(h_coeff_5tap_map)
+            counts["fixed_5tap"] = generate_fixed_5tap_output_vector(**kw)
+    except Exception as exc:
+        print(f"[FAIL] gen_fixed_output file=gen_fixed_output.py generated=0 skipped=0 failed=1 "
+              f"elapsed={perf_counter() - t0:.2f}s out={out_dir} error=\"{exc}\"")
+        raise
+    total = sum(counts.values())
+    print(f"[OK] gen_fixed_output file=gen_fixed_output.py generated={total} "
+          f"skipped={max(expected - total, 0)} failed=0 elapsed={perf_counter() - t0:.2f}s out={out_dir} "
+          f"fixed_3tap={counts['fixed_3tap']} fixed_5tap={counts['fixed_5tap']}")
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

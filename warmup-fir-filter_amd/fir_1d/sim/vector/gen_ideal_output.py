@@ -1,0 +1,98 @@
+"""Ideal (float64) output vectors (.npy) for every input image x every coefficient set.
+
+Mirror of the reference stage ``fir_1d/sim/vector/gen_ideal_output.py`` (entry points,
+naming ``{case}__{coeff}_ideal_{3,5}tap_y_f64.npy`` under ``output_dir/ideal_{3,5}tap``,
+skip-if-exists, return count, CLI flags).  The per-row loop of the reference
+(:37-50) becomes one ``fir1d_ideal_rows`` launch per image, bit-exact in float64.
+"""
+from __future__ import annotations
+
+import argparse
+from pathlib import Path
+from time import perf_counter
+
+import numpy as np
+
+import fir_hip
+from fir_1d.model.python.fir_1d_ref import _validate_h_coefficients
+from fir_1d.sim.vector.gen_fixed_output import _case_stem_from_input, _iter_input_npy_files, _load_input_image_u8
+from fir_1d.sim.vector.h_coeff import h_coeff_3tap_map, h_coeff_5tap_map
+
+THIS_FILE = Path(__file__).resolve()
+DEFAULT_INPUT_DIR = THIS_FILE.parent / "input"
+DEFAULT_OUTPUT_DIR = THIS_FILE.parent / "output"
+
+
+def _run_ideal_rowwise(x_u8: np.ndarray, h: list[float]) -> np.ndarray:
+    height, width = x_u8.shape
+    if height == 0:
+        return np.zeros((0, width), dtype=np.float64)
+    _validate_h_coefficients(h)
+    if width == 0:
+        return np.zeros((height, 0), dtype=np.float64)
+    return fir_hip.fir1d_ideal_rows(np.ascontiguousarray(x_u8, dtype=np.uint8), [float(v) for v in h])
+
+
+def _generate_ideal_outputs_for_tap_map(*, input_dir: Path, out_dir: Path, coeff_map: dict[str, list[float]],
+                                        tap_label: str, overwrite: bool = False) -> int:
+    inputs = _iter_input_npy_files(input_dir)
+    if not inputs:
+        raise FileNotFoundError(f"No input .npy files found in {input_dir}")
+    out_dir.mkdir(parents=True, exist_ok=True)
+    generated = 0
+    for in_path in inputs:
+        x_u8 = _load_input_image_u8(in_path)
+        stem = _case_stem_from_input(in_path)
+        for coeff_name, h in coeff_map.items():
+            out_path = out_dir / f"{stem}__{coeff_name}_ideal_{tap_label}_y_f64.npy"
+            if out_path.exists() and not overwrite:
+                continue
+            np.save(out_path, _run_ideal_rowwise(x_u8, h))
+            generated += 1
+    return generated
+
+
+def generate_ideal_3tap_output_vector(input_dir: Path = DEFAULT_INPUT_DIR, output_dir: Path = DEFAULT_OUTPUT_DIR,
+                                      *, overwrite: bool = False) -> int:
+    return _generate_ideal_outputs_for_tap_map(
+        input_dir=Path(input_dir).resolve(), out_dir=Path(output_dir).resolve() / "ideal_3tap",
+        coeff_map=h_coeff_3tap_map, tap_label="3tap", overwrite=overwrite)
+
+
+def generate_ideal_5tap_output_vector(input_dir: Path = DEFAULT_INPUT_DIR, output_dir: Path = DEFAULT_OUTPUT_DIR,
+                                      *, overwrite: bool = False) -> int:
+    return _generate_ideal_outputs_for_tap_map(
+        input_dir=Path(input_dir).resolve(), out_dir=Path(output_dir).resolve() / "ideal_5tap",
+        coeff_map=h_coeff_5tap_map, tap_label="5tap", overwrite=overwrite)
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description="Generate FIR 1D ideal output vectors for 3tap/5tap filters (GPU).")
+    ap.add_argument("--input-dir", type=Path, default=DEFAULT_INPUT_DIR)
+    ap.add_argument("--output-dir", type=Path, default=DEFAULT_OUTPUT_DIR)
+    ap.add_argument("--tap", choices=("all", "3", "5"), default="all")
+    ap.add_argument("--overwrite", action="store_true")
+    args = ap.parse_args(argv)
+    t0 = perf_counter()
+    in_dir, out_dir = args.input_dir.resolve(), args.output_dir.resolve()
+    counts, expected = {"ideal_3tap": 0, "ideal_5tap": 0}, 0
+    try:
+        if args.tap in ("all", "3"):
+            expected += len(_iter_input_npy_files(in_dir)) * len(h_coeff_3tap_map)
+            counts["ideal_3tap"] = generate_ideal_3tap_output_vector(in_dir, out_dir, overwrite=args.overwrite)
+        if args.tap in ("all", "5"):
+            expected += len(_iter_input_npy_files(in_dir)) * len(h_coeff_5tap_map)
+            counts["ideal_5tap"] = generate_ideal_5tap_output_vector(in_dir, out_dir, overwrite=args.overwrite)
+    except Exception as exc:
+        print(f"[FAIL] gen_ideal_output file=gen_ideal_output.py generated=0 skipped=0 failed=1 "
+              f"elapsed={perf_counter() - t0:.2f}s out={out_dir} error=\"{exc}\"")
+        raise
+    total = sum(counts.values())
+    print(f"[OK] gen_ideal_output file=gen_ideal_output.py generated={total} "
+          f"skipped={max(expected - total, 0)} failed=0 elapsed={perf_counter() - t0:.2f}s out={out_dir} "
+          f"ideal_3tap={counts['ideal_3tap']} ideal_5tap={counts['ideal_5tap']}")
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,173 @@
+"""ctypes binding of ``libfir_hip.so`` — the MI355X (gfx950) fixed-point FIR path.
+
+The C ABI is declared in ``include/fir_hip.h``.  This module is the only place that
+loads the library; it raises :class:`FirHipError` (a ``RuntimeError``) when the
+library is missing, no gfx950 device is present, or a HIP call fails.  There is no
+CPU fallback: the product path fails loudly rather than computing elsewhere.
+
+Host-array entry points (NumPy in, NumPy out, synchronous):
+    fir1d_fixed_rows, fir2d_fixed, fir1d_ideal_rows
+Device entry points (torch tensors on a HIP device, enqueued on the current stream):
+    see :mod:`fir_hip.torch_ops`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from pathlib import Path
+
+import numpy as np
+
+__all__ = [
+    "FirHipError", "lib", "lib_path", "device_count", "fir1d_fixed_rows", "fir2d_fixed",
+    "fir1d_ideal_rows", "IN_U8", "IN_I16", "OUT_U8_SAT", "OUT_I32", "MAX_TAPS", "EXPORTS",
+]
+
+IN_U8, IN_I16 = 0, 1
+OUT_U8_SAT, OUT_I32 = 0, 1
+MAX_TAPS = 256
+ABI_VERSION = 1
+
+_HERE = Path(__file__).resolve().parent
+
+
+def lib_path() -> Path:
+    return Path(os.environ.get("FIR_HIP_LIB", _HERE / "libfir_hip.so"))
+
+
+class FirHipError(RuntimeError):
+    """A failure inside libfir_hip (missing library, no device, HIP error, bad call)."""
+
+
+_i32, _i64, _vp = ctypes.c_int, ctypes.c_int64, ctypes.c_void_p
+
+# symbol -> (restype, argtypes); mirrors include/fir_hip.h one to one
+EXPORTS = {
+    "fir_abi_version": (_i32, []),
+    "fir_last_error": (ctypes.c_char_p, []),
+    "fir_device_count": (_i32, [ctypes.POINTER(_i32)]),
+    "fir1d_fixed_rows": (_i32, [_vp, _i32, _i64, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _i32]),
+    "fir1d_fixed_rows_dev": (_i32, [_vp, _i32, _i64, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp]),
+    "fir1d_fixed_edges_dev": (_i32, [_vp, _i32, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
+    "fir2d_fixed": (_i32, [_vp, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32]),
+    "fir2d_fixed_dev": (_i32, [_vp, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
+    "fir1d_ideal_rows": (_i32, [_vp, _i64, _i64, _vp, _i32, _vp, _i32]),
+    "fir1d_ideal_rows_dev": (_i32, [_vp, _i64, _i64, _vp, _i32, _vp, _vp]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib() -> ctypes.CDLL:
+    """Load libfir_hip.so once; raise FirHipError if it is missing or mismatched."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = lib_path()
+        if not path.exists():
+            raise FirHipError(
+                f"{path} is not built: run `make -C warmup-fir-filter_amd/csrc` or "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
+        try:
+            handle = ctypes.CDLL(str(path))
+        except OSError as exc:
+            raise FirHipError(f"cannot load {path}: {exc}") from exc
+        for name, (res, args) in EXPORTS.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        ver = handle.fir_abi_version()
+        if ver != ABI_VERSION:
+            raise FirHipError(f"{path}: ABI version {ver}, expected {ABI_VERSION}")
+        _lib = handle
+    return _lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().fir_last_error().decode(errors="replace")
+        raise FirHipError(f"{what} failed (status {rc}): {msg}")
+
+
+def device_count() -> int:
+    n = _i32(0)
+    _check(lib().fir_device_count(ctypes.byref(n)), "fir_device_count")
+    return n.value
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(_vp)
+
+
+def _taps_i32(hq) -> np.ndarray:
+    h = np.ascontiguousarray(np.asarray(hq, dtype=np.int64))
+    if h.ndim != 1 or h.size == 0:
+        raise FirHipError("hq must be a non-empty 1-D array")
+    if h.size > MAX_TAPS:
+        raise FirHipError(f"{h.size} taps exceed the library limit of {MAX_TAPS}")
+    if h.min() < -(1 << 31) or h.max() >= (1 << 31):
+        raise FirHipError("quantized taps must fit in int32")
+    return h.astype(np.int32)
+
+
+def fir1d_fixed_rows(x: np.ndarray, hq, frac_bits: int = 12, acc_bits: int = 32,
+                     out_stage: int = OUT_U8_SAT, channels: int = 1, device: int = 0) -> np.ndarray:
+    """Row-wise same-mode fixed FIR of a uint8/int16 array (last axis = row of
+    width*channels interleaved samples).  Returns uint8 (OUT_U8_SAT) or int32 (OUT_I32)."""
+    x = np.ascontiguousarray(x)
+    if x.dtype == np.uint8:
+        in_dtype = IN_U8
+    elif x.dtype == np.int16:
+        in_dtype = IN_I16
+    else:
+        raise FirHipError(f"x dtype must be uint8 or int16, got {x.dtype}")
+    h = _taps_i32(hq)
+    if x.ndim == 0:
+        x = x.reshape(1)
+    rowlen = x.shape[-1]
+    rows = x.size // rowlen if rowlen else 0
+    if rowlen % channels:
+        raise FirHipError("row length must be a multiple of channels")
+    y = np.empty(x.shape, dtype=np.uint8 if out_stage == OUT_U8_SAT else np.int32)
+    _check(lib().fir1d_fixed_rows(_ptr(x), in_dtype, rows, rowlen // channels, channels, _ptr(h), h.size,
+                                  int(frac_bits), int(acc_bits), int(out_stage), _ptr(y), int(device)),
+           "fir1d_fixed_rows")
+    return y
+
+
+def fir2d_fixed(x: np.ndarray, hq2, frac_bits: int = 12, acc_bits: int = 32, out_stage: int = OUT_U8_SAT,
+                device: int = 0) -> np.ndarray:
+    """2-D same-mode fixed FIR of a uint8 frame with a (R, C) quantized kernel."""
+    x = np.ascontiguousarray(x, dtype=np.uint8)
+    if x.ndim != 2:
+        raise FirHipError("x must be 2-D")
+    h2 = np.asarray(hq2, dtype=np.int64)
+    if h2.ndim != 2:
+        raise FirHipError("hq2 must be 2-D")
+    R, C = h2.shape
+    h = _taps_i32(h2.reshape(-1))
+    y = np.empty(x.shape, dtype=np.uint8 if out_stage == OUT_U8_SAT else np.int32)
+    _check(lib().fir2d_fixed(_ptr(x), x.shape[0], x.shape[1], _ptr(h), R, C, int(frac_bits), int(acc_bits),
+                             int(out_stage), _ptr(y), int(device)), "fir2d_fixed")
+    return y
+
+
+def fir1d_ideal_rows(x_u8: np.ndarray, h, device: int = 0) -> np.ndarray:
+    """float64 ideal model over uint8 rows (last axis)."""
+    x = np.ascontiguousarray(x_u8, dtype=np.uint8)
+    hh = np.ascontiguousarray(np.asarray(h, dtype=np.float64).reshape(-1))
+    if hh.size == 0 or hh.size > MAX_TAPS:
+        raise FirHipError(f"tap count must be in [1, {MAX_TAPS}]")
+    if x.ndim == 0:
+        x = x.reshape(1)
+    width = x.shape[-1]
+    rows = x.size // width if width else 0
+    y = np.empty(x.shape, dtype=np.float64)
+    _check(lib().fir1d_ideal_rows(_ptr(x), rows, width, _ptr(hh), hh.size, _ptr(y), int(device)),
+           "fir1d_ideal_rows")
+    return y

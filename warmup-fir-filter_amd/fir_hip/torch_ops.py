@@ -1,0 +1,127 @@
+"""Device-tensor entry points of libfir_hip (torch tensors already resident in HBM).
+
+PyTorch is plumbing here: it owns device memory, streams and ``torch.distributed``.
+Every call enqueues the HIP kernel on the tensor's current stream through the C ABI
+(``*_dev`` symbols of ``include/fir_hip.h``) and returns without synchronising.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import IN_I16, IN_U8, OUT_I32, OUT_U8_SAT, FirHipError, _check, _taps_i32, lib
+
+_IN = {torch.uint8: IN_U8, torch.int16: IN_I16}
+_OUT_DTYPE = {OUT_U8_SAT: torch.uint8, OUT_I32: torch.int32}
+
+
+class Taps:
+    """Quantized taps kept as a pinned-in-Python int32 array (no per-call conversion)."""
+
+    def __init__(self, hq):
+        self.h = _taps_i32(hq)
+        self.ptr = self.h.ctypes.data_as(ctypes.c_void_p)
+        self.n = int(self.h.size)
+
+
+def _taps(hq) -> Taps:
+    return hq if isinstance(hq, Taps) else Taps(hq)
+
+
+def _stream_ptr(t: torch.Tensor, stream) -> ctypes.c_void_p:
+    s = stream if stream is not None else torch.cuda.current_stream(t.device)
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _check_dev(t: torch.Tensor, name: str) -> None:
+    if not t.is_cuda:
+        raise FirHipError(f"{name} must be a device tensor")
+    if not t.is_contiguous():
+        raise FirHipError(f"{name} must be contiguous")
+
+
+def fir1d_fixed_rows_dev(x: torch.Tensor, hq, frac_bits: int = 12, acc_bits: int = 32,
+                         out_stage: int = OUT_I32, channels: int = 1, out: torch.Tensor | None = None,
+                         stream=None) -> torch.Tensor:
+    """Row-wise 1-D fixed FIR of a uint8/int16 device tensor (last axis = one row of
+    width*channels interleaved samples)."""
+    _check_dev(x, "x")
+    if x.dtype not in _IN:
+        raise FirHipError(f"x dtype must be uint8 or int16, got {x.dtype}")
+    t = _taps(hq)
+    if out is None:
+        out = torch.empty(x.shape, dtype=_OUT_DTYPE[out_stage], device=x.device)
+    _check_dev(out, "out")
+    if out.shape != x.shape or out.dtype != _OUT_DTYPE[out_stage]:
+        raise FirHipError("out must match x's shape and the out_stage dtype")
+    rowlen = x.shape[-1] if x.dim() else 1
+    rows = x.numel() // rowlen if rowlen else 0
+    if rowlen % channels:
+        raise FirHipError("row length must be a multiple of channels")
+    _check(lib().fir1d_fixed_rows_dev(ctypes.c_void_p(x.data_ptr()), _IN[x.dtype], rows, rowlen // channels,
+                                      channels, t.ptr, t.n, int(frac_bits), int(acc_bits), int(out_stage),
+                                      ctypes.c_void_p(out.data_ptr()), _stream_ptr(x, stream)),
+           "fir1d_fixed_rows_dev")
+    return out
+
+
+def fir1d_fixed_edges_dev(x: torch.Tensor, hq, out: torch.Tensor, halo_left: torch.Tensor | None,
+                          halo_right: torch.Tensor | None, frac_bits: int = 12, acc_bits: int = 32,
+                          out_stage: int = OUT_I32, channels: int = 1, stream=None) -> torch.Tensor:
+    """Recompute the halo-dependent edge outputs of a 1-D segment (see fir_hip.h)."""
+    _check_dev(x, "x")
+    _check_dev(out, "out")
+    t = _taps(hq)
+    L = t.n
+    hl_n, hr_n = (L - 1 - L // 2) * channels, (L // 2) * channels
+    for h, n, name in ((halo_left, hl_n, "halo_left"), (halo_right, hr_n, "halo_right")):
+        if h is not None:
+            _check_dev(h, name)
+            if h.dtype != x.dtype or h.numel() != n:
+                raise FirHipError(f"{name} must hold {n} samples of {x.dtype}")
+    if x.numel() % channels:
+        raise FirHipError("segment length must be a multiple of channels")
+    hlp = ctypes.c_void_p(halo_left.data_ptr()) if halo_left is not None and hl_n else None
+    hrp = ctypes.c_void_p(halo_right.data_ptr()) if halo_right is not None and hr_n else None
+    _check(lib().fir1d_fixed_edges_dev(ctypes.c_void_p(x.data_ptr()), _IN[x.dtype], x.numel() // channels, channels,
+                                       t.ptr, t.n, int(frac_bits), int(acc_bits), int(out_stage), hlp, hrp,
+                                       ctypes.c_void_p(out.data_ptr()), _stream_ptr(x, stream)),
+           "fir1d_fixed_edges_dev")
+    return out
+
+
+def fir2d_fixed_dev(x: torch.Tensor, hq2, frac_bits: int = 12, acc_bits: int = 32, out_stage: int = OUT_U8_SAT,
+                    out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    _check_dev(x, "x")
+    if x.dtype != torch.uint8 or x.dim() != 2:
+        raise FirHipError("x must be a 2-D uint8 device tensor")
+    h2 = np.asarray(hq2.h if isinstance(hq2, Taps) else hq2)
+    if h2.ndim != 2:
+        raise FirHipError("hq2 must be 2-D")
+    R, C = h2.shape
+    t = Taps(h2.reshape(-1))
+    if out is None:
+        out = torch.empty(x.shape, dtype=_OUT_DTYPE[out_stage], device=x.device)
+    _check_dev(out, "out")
+    _check(lib().fir2d_fixed_dev(ctypes.c_void_p(x.data_ptr()), x.shape[0], x.shape[1], t.ptr, R, C, int(frac_bits),
+                                 int(acc_bits), int(out_stage), ctypes.c_void_p(out.data_ptr()),
+                                 _stream_ptr(x, stream)), "fir2d_fixed_dev")
+    return out
+
+
+def fir1d_ideal_rows_dev(x: torch.Tensor, h, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    _check_dev(x, "x")
+    if x.dtype != torch.uint8:
+        raise FirHipError("x must be uint8")
+    hh = np.ascontiguousarray(np.asarray(h, dtype=np.float64).reshape(-1))
+    if out is None:
+        out = torch.empty(x.shape, dtype=torch.float64, device=x.device)
+    _check_dev(out, "out")
+    width = x.shape[-1] if x.dim() else 1
+    rows = x.numel() // width if width else 0
+    _check(lib().fir1d_ideal_rows_dev(ctypes.c_void_p(x.data_ptr()), rows, width, hh.ctypes.data_as(ctypes.c_void_p),
+                                      hh.size, ctypes.c_void_p(out.data_ptr()), _stream_ptr(x, stream)),
+           "fir1d_ideal_rows_dev")
+    return out
