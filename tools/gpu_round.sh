@@ -1,0 +1,49 @@
+#!/bin/bash
+# One GPU session: smoke -> pytest -m gpu -> bench -> rocprofv3 kernel stats.
+# Every GPU step has its own time limit; a crash, abort or timeout ends the script.
+# Test failures (pytest rc 1) do not stop the bench.  Usage: tools/gpu_round.sh [tag] [steps...]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-r01}
+shift || true
+STEPS=${*:-"smoke pytest bench prof"}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+run() {  # name seconds cmd...
+    local name=$1 t=$2
+    shift 2
+    echo "== $name: $*"
+    local t0=$(date +%s)
+    timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc ($(( $(date +%s) - t0 ))s)"
+    tail -n 15 "$OUT/$name.log"
+    return $rc
+}
+
+fatal() {  # rc: anything but 0/1 (crash, abort, timeout) ends the session
+    [ "$1" -ne 0 ] && [ "$1" -ne 1 ] && { echo "== stopping after rc=$1"; exit "$1"; }
+    return 0
+}
+
+for s in $STEPS; do
+    case $s in
+        smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; rc=$?; [ $rc -ne 0 ] && exit $rc ;;
+        pytest) run pytest_gpu 700 python -m pytest tests -m gpu -q -p no:cacheprovider -x; fatal $? ;;
+        pytestall) run pytest_gpu 700 python -m pytest tests -m gpu -q -p no:cacheprovider; fatal $? ;;
+        bench) run bench 300 python bench.py; fatal $? ;;
+        benchcplx) run bench_cplx 300 python bench.py --workload cplx_i16 --cpu-seconds 5; fatal $? ;;
+        bench2d) run bench_2d 300 python bench.py --workload fir2d_u8 --cpu-seconds 5; fatal $? ;;
+        prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+                  python bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-parity; fatal $? ;;
+        pmc) for c in FETCH_SIZE WRITE_SIZE; do
+                 run "pmc_$c" 300 rocprofv3 --pmc "$c" --kernel-trace -d "$OUT/pmc_$c" -o run --output-format csv -- \
+                     python bench.py --steps 10 --warmup 2 --cpu-seconds 0 --no-parity; fatal $? || exit
+             done ;;
+        micro) run micro 300 tools/microbench/fir_micro 28 20; fatal $? ;;
+        *) echo "unknown step $s"; exit 2 ;;
+    esac
+done
+echo "== done"

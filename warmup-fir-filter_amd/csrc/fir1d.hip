@@ -5,14 +5,15 @@
 //   q = (acc + 2^(f-1)) >> f, then saturated to u8 or kept as int32.
 //
 // Two kernels:
-//  * fir1d_reg_kernel  — the hot path.  One thread owns one 16-byte vector of samples
-//    (16 u8 or 8 int16).  The (L-1)-sample halo comes from the neighbouring lanes'
-//    registers through DPP wave shifts (v_mov_b32_dpp wave_shr:1 / wave_shl:1), so each
-//    HBM byte is loaded once; only lanes 0 and 63 of a wave issue one extra 16-byte load
-//    for the neighbouring wave's edge vector (served by L2).  32-bit wrap-around MACs on
-//    v_mul_i32_i24 (taps checked to fit 24 bits on the host), overflow-free rounding,
-//    16-byte stores.  Row edges (images) are handled by a per-thread column test; threads
-//    whose window lies inside one row take the unmasked path.
+//  * fir1d_reg_kernel (fir1d_reg.h) — the hot path.  A lane owns one 16-byte vector of
+//    samples (16 u8 or 8 int16); a wave owns kRegU chunks of 64 vectors (1 KiB per load
+//    instruction).  The (L-1)-sample halo comes from the neighbouring lanes' registers by
+//    DPP wave shifts (v_mov_b32_dpp wave_shr:1 / wave_shl:1, wave_ror/rol at chunk seams),
+//    so every HBM byte is loaded once; only lanes 0 and 63 issue one extra 16-byte load for
+//    the adjacent tile's edge vector (an L2 hit).  32-bit wrap-around MACs on
+//    v_mad_i32_i24 (taps checked to fit 24 bits on the host), overflow-free rounding,
+//    16-byte stores.  Row edges (images) are handled by a per-vector column
+//    test; vectors whose window lies inside one row take the unmasked path.
 //  * fir1d_generic_kernel — every other configuration (any tap count up to FIR_MAX_TAPS,
 //    any acc_bits / frac_bits, unaligned buffers, narrow rows, halo segments): a
 //    workgroup stages an LDS sliding-window tile of 1024 outputs + (L-1)*channels halo
@@ -20,173 +21,11 @@
 #include <algorithm>
 #include <string>
 
+#include "fir1d_reg.h"
 #include "fir_common.h"
 #include "fir_launch.h"
 
 namespace fir {
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
-template <int L>
-struct TapsN {
-    int32_t h[L];
-};
-
-struct RowGeom {
-    int64_t total;      // samples in the buffer (rows * width * channels)
-    uint32_t rowlen32;  // width * channels, valid when multi_row
-    int multi_row;      // rows > 1 (then total < 2^32 is guaranteed by the host)
-};
-
-// Load vector `v` (VEC samples) into 4 dwords: full 16-byte load when wholly in range,
-// element-wise with zero fill at the ragged end, zeros past the end.
-template <typename InT, bool NT>
-__device__ __forceinline__ void load_vec(const InT* __restrict__ x, int64_t v, int64_t nvec, int64_t total,
-                                         uint32_t (&d)[4]) {
-    constexpr int EPD = InTraits<InT>::kPerDword;
-    constexpr int VEC = 4 * EPD;
-    if (v < nvec) {
-        const u32x4* p = reinterpret_cast<const u32x4*>(x + v * VEC);
-        u32x4 q = NT ? __builtin_nontemporal_load(p) : *p;
-        d[0] = q.x;
-        d[1] = q.y;
-        d[2] = q.z;
-        d[3] = q.w;
-    } else {
-        d[0] = d[1] = d[2] = d[3] = 0;
-        const int64_t base = v * VEC;
-        if (v >= 0 && base < total) {
-            const int n = (int)min((int64_t)VEC, total - base);
-            for (int j = 0; j < n; ++j) {
-                const uint32_t e = (uint32_t)x[base + j] & (EPD == 4 ? 0xFFu : 0xFFFFu);
-                d[j / EPD] |= e << ((32 / EPD) * (j % EPD));
-            }
-        }
-    }
-}
-
-template <typename InT, int STAGE, int L, int CH, bool NT>
-__global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict__ x,
-                                                           typename OutTraits<STAGE>::T* __restrict__ y,
-                                                           RowGeom g, TapsN<L> taps, int shl, int frac) {
-    using IT = InTraits<InT>;
-    constexpr int EPD = IT::kPerDword;
-    constexpr int VEC = 4 * EPD;
-    constexpr int C = L / 2;
-    constexpr int HLE = (L - 1 - C) * CH;  // samples needed left of the vector
-    constexpr int HRE = C * CH;            // samples needed right of the vector
-    static_assert(HLE <= VEC && HRE <= VEC, "halo must fit in one neighbouring vector");
-    constexpr int NDL = (HLE + EPD - 1) / EPD;  // dwords shifted in from lane-1
-    constexpr int NDR = (HRE + EPD - 1) / EPD;  // dwords shifted in from lane+1
-
-    const int lane = threadIdx.x & (kWave - 1);
-    const int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int64_t total = g.total;
-    const int64_t nvec = total / VEC;
-    const int64_t g0 = v * VEC;
-
-    uint32_t own[4], hv[4] = {0, 0, 0, 0};
-    load_vec<InT, NT>(x, v, nvec, total, own);
-    // The wave's edge lanes fetch the vectors just outside the wave (L2 hits in steady state).
-    if (lane == 0) {
-        if (NDL > 0 && v > 0) load_vec<InT, false>(x, v - 1, nvec, total, hv);
-    } else if (lane == kWave - 1) {
-        if (NDR > 0) load_vec<InT, false>(x, v + 1, nvec, total, hv);
-    }
-
-    // Window w[0 .. HLE+VEC+HRE): left halo | own samples | right halo.
-    int32_t w[HLE + VEC + HRE];
-    if constexpr (NDL > 0) {
-        uint32_t prev[4];
-#pragma unroll
-        for (int q = 4 - NDL; q < 4; ++q) prev[q] = from_prev_lane(hv[q], own[q]);
-#pragma unroll
-        for (int i = 0; i < HLE; ++i) {
-            constexpr int base = VEC - HLE;
-            w[i] = IT::get(prev[(base + i) / EPD], (base + i) % EPD);
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) w[HLE + j] = IT::get(own[j / EPD], j % EPD);
-    if constexpr (NDR > 0) {
-        uint32_t next[4];
-#pragma unroll
-        for (int q = 0; q < NDR; ++q) next[q] = from_next_lane(hv[q], own[q]);
-#pragma unroll
-        for (int i = 0; i < HRE; ++i) w[HLE + VEC + i] = IT::get(next[i / EPD], i % EPD);
-    }
-
-    if (g0 >= total) return;  // after the cross-lane exchange: idle tail lanes just leave
-
-    int64_t col0, rowlen;
-    if (g.multi_row) {
-        rowlen = g.rowlen32;
-        col0 = (uint32_t)g0 % g.rowlen32;
-    } else {
-        rowlen = total;
-        col0 = g0;
-    }
-    const bool interior = col0 >= HLE && col0 + VEC + HRE <= rowlen;
-
-    int32_t q[VEC];
-    if (interior) {
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) {
-            uint32_t acc = 0;
-#pragma unroll
-            for (int k = 0; k < L; ++k) acc += (uint32_t)__mul24(taps.h[k], w[HLE + j + (C - k) * CH]);
-            q[j] = round32(acc, shl, frac);
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) {
-            int64_t cj = col0 + j;
-            if (cj >= rowlen) cj -= rowlen;  // the vector crossed into the next row
-            uint32_t acc = 0;
-#pragma unroll
-            for (int k = 0; k < L; ++k) {
-                const int64_t p = cj + (C - k) * CH;
-                const uint32_t t = (uint32_t)__mul24(taps.h[k], w[HLE + j + (C - k) * CH]);
-                acc += (p >= 0 && p < rowlen) ? t : 0u;
-            }
-            q[j] = round32(acc, shl, frac);
-        }
-    }
-
-    if (v < nvec) {
-        if constexpr (STAGE == FIR_OUT_U8_SAT) {
-            uint32_t o[VEC / 4];
-#pragma unroll
-            for (int i = 0; i < VEC / 4; ++i) {
-                o[i] = (uint32_t)stage_out32<STAGE>(q[4 * i]) | ((uint32_t)stage_out32<STAGE>(q[4 * i + 1]) << 8) |
-                       ((uint32_t)stage_out32<STAGE>(q[4 * i + 2]) << 16) |
-                       ((uint32_t)stage_out32<STAGE>(q[4 * i + 3]) << 24);
-            }
-            if constexpr (VEC == 16) {
-                u32x4 val = {o[0], o[1], o[2], o[3]};
-                u32x4* p = reinterpret_cast<u32x4*>(y + g0);
-                if (NT) __builtin_nontemporal_store(val, p); else *p = val;
-            } else {
-                u32x2 val = {o[0], o[1]};
-                u32x2* p = reinterpret_cast<u32x2*>(y + g0);
-                if (NT) __builtin_nontemporal_store(val, p); else *p = val;
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < VEC / 4; ++i) {
-                u32x4 val = {(uint32_t)q[4 * i], (uint32_t)q[4 * i + 1], (uint32_t)q[4 * i + 2], (uint32_t)q[4 * i + 3]};
-                u32x4* p = reinterpret_cast<u32x4*>(y + g0) + i;
-                if (NT) __builtin_nontemporal_store(val, p); else *p = val;
-            }
-        }
-    } else {
-        const int n = (int)min((int64_t)VEC, total - g0);
-#pragma unroll
-        for (int j = 0; j < VEC; ++j)
-            if (j < n) y[g0 + j] = stage_out32<STAGE>(q[j]);
-    }
-}
 
 // ---------------------------------------------------------------------------------------
 // Generic LDS sliding-window kernel.
@@ -246,31 +85,27 @@ __global__ __launch_bounds__(kBlock) void fir1d_generic_kernel(const InT* __rest
 // ---------------------------------------------------------------------------------------
 // Host-side launchers.
 
-static bool g_nt_enabled = [] {
-    const char* e = getenv("FIR_HIP_NT");
-    return e == nullptr || e[0] != '0';
-}();
+// Hot-kernel shape chosen by the A/B microbenchmark (tools/microbench; profiles/r01_micro.txt):
+// one 64-vector chunk per wave, default-policy loads and stores (non-temporal stores cost
+// 25-45 % on this 1:2 read:write stream; more chunks per wave or a persistent grid 3-15 %).
+constexpr int kRegU = 1;
+constexpr int kRegFlags = 0;
+constexpr int kPersistBlocks = 2048;
 
 template <typename InT, int STAGE, int L, int CH>
 static hipError_t launch_reg(const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
                              const int32_t* hq, int frac, int acc_bits, hipStream_t stream) {
     using OutT = typename OutTraits<STAGE>::T;
-    constexpr int VEC = 4 * InTraits<InT>::kPerDword;
     RowGeom g;
     g.total = total;
     g.rowlen32 = (uint32_t)(rows > 1 ? rowlen : 0);
     g.multi_row = rows > 1;
     TapsN<L> t;
     for (int k = 0; k < L; ++k) t.h[k] = hq[k];
-    const int64_t threads = (total + VEC - 1) / VEC;
-    const int64_t blocks = (threads + kBlock - 1) / kBlock;
-    if (g_nt_enabled) {
-        hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, true>), dim3((unsigned)blocks), dim3(kBlock), 0,
-                           stream, (const InT*)x, (OutT*)y, g, t, 32 - acc_bits, frac);
-    } else {
-        hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, false>), dim3((unsigned)blocks), dim3(kBlock), 0,
-                           stream, (const InT*)x, (OutT*)y, g, t, 32 - acc_bits, frac);
-    }
+    int64_t ntiles = 0, blocks = 0;
+    reg_launch_geometry<InT, kRegU, kRegFlags>(total, kPersistBlocks, &ntiles, &blocks);
+    hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, kRegU, kRegFlags>), dim3((unsigned)blocks), dim3(kBlock),
+                       0, stream, (const InT*)x, (OutT*)y, g, t, 32 - acc_bits, frac, ntiles);
     return hipGetLastError();
 }
 
