@@ -43,6 +43,7 @@ for s in $STEPS; do
                      python bench.py --steps 10 --warmup 2 --cpu-seconds 0 --no-parity; fatal $? || exit
              done ;;
         micro) run micro 300 tools/microbench/fir_micro 28 20; fatal $? ;;
+        micro2d) run micro2d 300 tools/microbench/fir2d_micro 15; fatal $? ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done

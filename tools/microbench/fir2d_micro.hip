@@ -1,0 +1,121 @@
+// fir2d_micro.hip — A/B microbenchmark for the 2-D kernel (dev tool, not the product).
+// Variants of fir2d_reg_kernel<5,5,u8> (pixels per lane, strip height) on an 8192x8192 u8
+// frame, batches of back-to-back launches interleaved round-robin; each variant is checked
+// against a CPU evaluation on sampled pixels (all four borders included).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "fir2d_reg.h"
+
+using namespace fir;
+
+#define CK(e)                                                                              \
+    do {                                                                                   \
+        hipError_t _e = (e);                                                               \
+        if (_e != hipSuccess) {                                                            \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #e, hipGetErrorString(_e)); \
+            exit(1);                                                                       \
+        }                                                                                  \
+    } while (0)
+
+static int32_t g_h[5][5];
+
+template <int VEC, int STRIP, bool DOT2>
+static void launch(const uint8_t* x, uint8_t* y, int64_t H, int64_t W, hipStream_t s) {
+    Taps2<5, 5> t;
+    for (int m = 0; m < 5; ++m)
+        for (int n = 0; n < 5; ++n) t.h[m][n] = g_h[m][n];
+    pack_taps2(t);
+    const dim3 grid = fir2d_reg_grid<VEC, STRIP>(H, W);
+    hipLaunchKernelGGL((fir2d_reg_kernel<5, 5, FIR_OUT_U8_SAT, VEC, STRIP, DOT2>), grid, dim3(kBlock), 0, s, x, y, H,
+                       W, t, 0, 12);
+}
+
+struct V {
+    std::string name;
+    void (*fn)(const uint8_t*, uint8_t*, int64_t, int64_t, hipStream_t);
+    std::vector<float> us;
+};
+
+int main(int argc, char** argv) {
+    const int64_t H = 8192, W = 8192;
+    const int rounds = argc > 1 ? atoi(argv[1]) : 15;
+    const int h1[5] = {256, 1024, 1536, 1024, 256};
+    for (int m = 0; m < 5; ++m)
+        for (int n = 0; n < 5; ++n) g_h[m][n] = h1[m] * h1[n] / 4096 + (m == 0 && n == 1 ? 7 : 0) - (m == 3 && n == 4 ? 3 : 0);
+    std::vector<uint8_t> hx(H * W), hy(H * W);
+    uint64_t s = 88172645463325252ull;
+    for (auto& v : hx) {
+        s ^= s << 13;
+        s ^= s >> 7;
+        s ^= s << 17;
+        v = (uint8_t)(s >> 33);
+    }
+    uint8_t *dx, *dy;
+    CK(hipMalloc(&dx, H * W));
+    CK(hipMalloc(&dy, H * W));
+    CK(hipMemcpy(dx, hx.data(), H * W, hipMemcpyHostToDevice));
+    hipStream_t st;
+    CK(hipStreamCreate(&st));
+    std::vector<V> vs = {
+        {"mad vec8 strip16", launch<8, 16, false>, {}},  {"dot2 vec8 strip16", launch<8, 16, true>, {}},
+        {"dot2 vec8 strip32", launch<8, 32, true>, {}},  {"dot2 vec8 strip8", launch<8, 8, true>, {}},
+        {"dot2 vec16 strip16", launch<16, 16, true>, {}}, {"dot2 vec16 strip8", launch<16, 8, true>, {}},
+        {"dot2 vec4 strip16", launch<4, 16, true>, {}},  {"dot2 vec4 strip32", launch<4, 32, true>, {}},
+    };
+    auto ref = [&](int64_t i, int64_t j) {
+        uint32_t a = 0;
+        for (int m = 0; m < 5; ++m)
+            for (int n = 0; n < 5; ++n) {
+                const int64_t ii = i - m + 2, jj = j - n + 2;
+                if (ii >= 0 && ii < H && jj >= 0 && jj < W) a += (uint32_t)(g_h[m][n] * (int32_t)hx[ii * W + jj]);
+            }
+        const int32_t q = ((int32_t)a >> 12) + (((int32_t)a >> 11) & 1);
+        return (uint8_t)std::min(std::max(q, 0), 255);
+    };
+    for (auto& v : vs) {
+        CK(hipMemset(dy, 0xA5, H * W));
+        v.fn(dx, dy, H, W, st);
+        CK(hipGetLastError());
+        CK(hipStreamSynchronize(st));
+        CK(hipMemcpy(hy.data(), dy, H * W, hipMemcpyDeviceToHost));
+        int64_t bad = 0, n = 0;
+        for (int64_t i = 0; i < H; ++i) {
+            const bool edge_row = i < 3 || i >= H - 3 || i % 31 == 0 || i % 32 < 3;
+            for (int64_t j = 0; j < W; j += (edge_row || j < 3 || j >= W - 3) ? 1 : 61) {
+                ++n;
+                if (hy[i * W + j] != ref(i, j) && bad++ < 3)
+                    fprintf(stderr, "%s: (%lld,%lld) %d vs %d\n", v.name.c_str(), (long long)i, (long long)j,
+                            hy[i * W + j], ref(i, j));
+            }
+        }
+        printf("check %-16s %s (%lld px)\n", v.name.c_str(), bad ? "FAIL" : "ok", (long long)n);
+        if (bad) return 1;
+    }
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int r = 0; r < rounds; ++r)
+        for (auto& v : vs) {
+            CK(hipEventRecord(a, st));
+            for (int i = 0; i < 10; ++i) v.fn(dx, dy, H, W, st);
+            CK(hipEventRecord(b, st));
+            CK(hipEventSynchronize(b));
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, b));
+            v.us.push_back(ms * 100.f);
+        }
+    printf("%-16s %10s %10s %10s %9s\n", "variant", "median_us", "min_us", "Gpx/s", "GB/s(alg)");
+    for (auto& v : vs) {
+        std::sort(v.us.begin(), v.us.end());
+        const double med = v.us[v.us.size() / 2];
+        printf("%-16s %10.1f %10.1f %10.1f %9.1f\n", v.name.c_str(), med, v.us[0], H * W / med / 1e3,
+               2.0 * H * W / med / 1e3);
+    }
+    return 0;
+}

@@ -1,0 +1,231 @@
+// fir2d_reg.h — register/DPP 2-D FIR kernel template, shared by the library
+// (fir2d.hip) and the A/B microbenchmark (tools/microbench/fir2d_micro.hip).
+//
+// y[i,j] = stage(round(wrap(sum_m sum_n hq[m][n] * x[i - m + R/2][j - n + C/2]))), zero padded.
+//
+// A lane owns VEC horizontally adjacent pixels (one VEC-byte load per input row); the
+// horizontal (C-1)-pixel halo arrives from the neighbouring lanes by DPP wave shifts (lanes
+// 0 / 63 load one dword of the neighbouring wave's pixels); the vertical (R-1)-row halo is a
+// register ring of R partial output rows: each input row is loaded once per STRIP-row strip
+// and scattered into the R output rows it feeds (input-stationary).  Strips overlap by R-1
+// input rows (served from the Infinity Cache).  The next input row is loaded before the
+// current one is consumed.
+#pragma once
+
+#include "fir_common.h"
+
+namespace fir {
+
+template <int R, int C>
+struct Taps2 {
+    int32_t h[R][C];
+    // DOT2 form: pair p of row m = (h[m][C-1-2p], h[m][C-2-2p]) as two int16 (0 past the row)
+    uint32_t p2[R][(C + 1) / 2];
+};
+
+template <int R, int C>
+inline void pack_taps2(Taps2<R, C>& t) {
+    for (int m = 0; m < R; ++m)
+        for (int p = 0; p < (C + 1) / 2; ++p) {
+            const int lo = t.h[m][C - 1 - 2 * p];
+            const int hi = (C - 2 - 2 * p) >= 0 ? t.h[m][C - 2 - 2 * p] : 0;
+            t.p2[m][p] = ((uint32_t)lo & 0xFFFFu) | ((uint32_t)hi << 16);
+        }
+}
+
+typedef short fir_short2 __attribute__((ext_vector_type(2)));
+
+// v_dot2_i32_i16 (no clamp: wrap-around int32) on raw dwords
+__device__ __forceinline__ uint32_t dot2_acc(uint32_t a, uint32_t b, uint32_t c) {
+    return (uint32_t)__builtin_amdgcn_sdot2(__builtin_bit_cast(fir_short2, a), __builtin_bit_cast(fir_short2, b),
+                                            (int)c, false);
+}
+
+// bytes k and k+1 of a little-endian byte stream held in dwords s[], zero-extended into the
+// two 16-bit halves of one dword (one v_perm_b32).
+template <int K>
+__device__ __forceinline__ uint32_t pair16(const uint32_t* s) {
+    constexpr int d0 = K / 4, b0 = K % 4, d1 = (K + 1) / 4, b1 = (K + 1) % 4;
+    if constexpr (d0 == d1) {
+        constexpr uint32_t sel = (uint32_t)b0 | (0x0Cu << 8) | ((uint32_t)b1 << 16) | (0x0Cu << 24);
+        return __builtin_amdgcn_perm(s[d0], s[d0], sel);
+    } else {
+        // perm(hi_src, lo_src): bytes 0-3 = lo_src, 4-7 = hi_src
+        constexpr uint32_t sel = (uint32_t)b0 | (0x0Cu << 8) | ((uint32_t)(4 + b1) << 16) | (0x0Cu << 24);
+        return __builtin_amdgcn_perm(s[d1], s[d0], sel);
+    }
+}
+
+template <int K0, int N>
+struct PairBuilder {
+    __device__ static __forceinline__ void run(const uint32_t* s, uint32_t* P) {
+        if constexpr (N > 0) {
+            P[K0] = pair16<K0>(s);
+            PairBuilder<K0 + 1, N - 1>::run(s, P);
+        }
+    }
+};
+
+// Branch-free row load: the address is always in bounds (the caller clamps it) and the
+// value is zeroed by a select when the row/column is outside the frame, so the compiler can
+// count outstanding loads exactly (a load inside a branch makes it wait for all of them).
+template <int ND>
+__device__ __forceinline__ void load_row_px(const uint8_t* __restrict__ p, bool ok, uint32_t (&d)[ND]) {
+    typedef uint32_t vN __attribute__((ext_vector_type(ND)));
+    const vN q = *reinterpret_cast<const vN*>(p);
+#pragma unroll
+    for (int i = 0; i < ND; ++i) d[i] = ok ? q[i] : 0u;
+}
+
+template <int R, int C, int STAGE, int VEC, int STRIP, bool DOT2>
+__global__ __launch_bounds__(kBlock) void fir2d_reg_kernel(const uint8_t* __restrict__ x,
+                                                           typename OutTraits<STAGE>::T* __restrict__ y, int64_t H,
+                                                           int64_t W, Taps2<R, C> taps, int shl, int frac) {
+    using OutT = typename OutTraits<STAGE>::T;
+    constexpr int ND = VEC / 4;  // dwords per lane per row
+    constexpr int CC = C / 2;
+    constexpr int HLE = C - 1 - CC, HRE = CC;  // horizontal halo
+    constexpr int TOP = R - 1 - R / 2;         // input rows above an output row
+    static_assert(HLE <= 4 && HRE <= 4, "horizontal halo must fit in one dword");
+    constexpr int T = STRIP + R - 1;  // input rows per strip (the strip loop is fully unrolled)
+
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // vector column index
+    const int64_t col0 = v * VEC;
+    const bool active = col0 < W;
+    const int64_t colc = active ? col0 : W - VEC;  // in-bounds column for idle lanes
+    const int64_t r0 = (int64_t)blockIdx.y * STRIP;
+    // halo dword: lane 0 reads the 4 pixels left of its vector, lane 63 the 4 right of it;
+    // every other lane re-reads its own first dword (same cache line, value unused)
+    const int64_t hraw = lane == 0 ? col0 - 4 : (lane == kWave - 1 ? col0 + VEC : col0);
+    const bool hlane = (lane == 0 && HLE > 0) || (lane == kWave - 1 && HRE > 0);
+    const bool hin = hraw >= 0 && hraw < W;
+    const int64_t hcol = hin ? hraw : colc;
+    const bool hok = hlane && hin;
+
+    uint32_t acc[R][VEC];
+#pragma unroll
+    for (int s = 0; s < R; ++s)
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) acc[s][j] = 0;
+
+    auto row_ptr = [&](int64_t row) { return x + (row < 0 ? 0 : (row >= H ? H - 1 : row)) * W; };
+    uint32_t cur[ND], hcur;
+    {
+        const int64_t row = r0 - TOP;
+        const bool rok = row >= 0 && row < H;
+        const uint8_t* rp = row_ptr(row);
+        load_row_px<ND>(rp + colc, rok && active, cur);
+        const uint32_t hv = *reinterpret_cast<const uint32_t*>(rp + hcol);
+        hcur = (hok && rok) ? hv : 0u;
+    }
+
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        {
+            const int s = t % R;
+            uint32_t nxt[ND] = {}, hnxt = 0;
+            if (t + 1 < T) {  // compile-time after the unroll
+                const int64_t row = r0 - TOP + t + 1;
+                const bool rok = row >= 0 && row < H;
+                const uint8_t* rp = row_ptr(row);
+                load_row_px<ND>(rp + colc, rok && active, nxt);
+                const uint32_t hv = *reinterpret_cast<const uint32_t*>(rp + hcol);
+                hnxt = (hok && rok) ? hv : 0u;
+            }
+            if constexpr (DOT2) {
+                // byte stream: [left-halo dword | own dwords | right-halo dword]; window pixel i
+                // is stream byte i + (4 - HLE).  P[k] = (w[k], w[k+1]) as int16 halves.
+                uint32_t sb[ND + 2];
+                sb[0] = HLE > 0 ? from_prev_lane(hcur, cur[ND - 1]) : 0u;
+#pragma unroll
+                for (int i = 0; i < ND; ++i) sb[1 + i] = cur[i];
+                sb[ND + 1] = HRE > 0 ? from_next_lane(hcur, cur[0]) : 0u;
+                constexpr int NP = VEC + C - 1;  // pairs P[0 .. VEC+C-2]
+                uint32_t Pr[NP + 4 - HLE];
+                PairBuilder<4 - HLE, NP>::run(sb, Pr);
+                const uint32_t* P = Pr + (4 - HLE);
+#pragma unroll
+                for (int m = 0; m < R; ++m) {
+                    const int slot = (s + 1 + m) % R;
+#pragma unroll
+                    for (int j = 0; j < VEC; ++j) {
+                        uint32_t a = acc[slot][j];
+#pragma unroll
+                        for (int p = 0; p < (C + 1) / 2; ++p) a = dot2_acc(P[j + 2 * p], taps.p2[m][p], a);
+                        acc[slot][j] = a;
+                    }
+                }
+            } else {
+            int32_t w[HLE + VEC + HRE];
+            if constexpr (HLE > 0) {
+                const uint32_t p = from_prev_lane(hcur, cur[ND - 1]);
+#pragma unroll
+                for (int i = 0; i < HLE; ++i) w[i] = (int32_t)((p >> (8 * (4 - HLE + i))) & 0xFFu);
+            }
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) w[HLE + j] = (int32_t)((cur[j / 4] >> (8 * (j % 4))) & 0xFFu);
+            if constexpr (HRE > 0) {
+                const uint32_t nx = from_next_lane(hcur, cur[0]);
+#pragma unroll
+                for (int i = 0; i < HRE; ++i) w[HLE + VEC + i] = (int32_t)((nx >> (8 * i)) & 0xFFu);
+            }
+            // input row t feeds output rows o = t - (R-1) + m, ring slot (s + 1 + m) % R
+#pragma unroll
+            for (int m = 0; m < R; ++m) {
+                const int slot = (s + 1 + m) % R;
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) {
+                    uint32_t a = acc[slot][j];
+#pragma unroll
+                    for (int n = 0; n < C; ++n) a += (uint32_t)__mul24(taps.h[m][n], w[HLE + j + CC - n]);
+                    acc[slot][j] = a;
+                }
+            }
+            }
+            {  // output row o = t - (R-1) is complete in slot (s + 1) % R
+                const int slot = (s + 1) % R;
+                const int o = t - (R - 1);
+                const int64_t orow = r0 + o;
+                if (o >= 0 && active && orow < H) {
+                    OutT* dst = y + orow * W + col0;
+                    if constexpr (STAGE == FIR_OUT_U8_SAT) {
+                        typedef uint32_t vN __attribute__((ext_vector_type(ND)));
+                        vN val;
+#pragma unroll
+                        for (int i = 0; i < ND; ++i) {
+                            uint32_t o4 = 0;
+#pragma unroll
+                            for (int b = 0; b < 4; ++b)
+                                o4 |= (uint32_t)stage_out32<STAGE>(round32(acc[slot][4 * i + b], shl, frac)) << (8 * b);
+                            val[i] = o4;
+                        }
+                        *reinterpret_cast<vN*>(dst) = val;
+                    } else {
+                        typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+                        for (int i = 0; i < VEC / 4; ++i) {
+                            v4 val;
+#pragma unroll
+                            for (int b = 0; b < 4; ++b) val[b] = (uint32_t)round32(acc[slot][4 * i + b], shl, frac);
+                            reinterpret_cast<v4*>(dst)[i] = val;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) acc[slot][j] = 0;
+            }
+#pragma unroll
+            for (int i = 0; i < ND; ++i) cur[i] = nxt[i];
+            hcur = hnxt;
+        }
+    }
+}
+
+template <int VEC, int STRIP>
+inline dim3 fir2d_reg_grid(int64_t H, int64_t W) {
+    const int64_t vecs = W / VEC;
+    return dim3((unsigned)((vecs + kBlock - 1) / kBlock), (unsigned)((H + STRIP - 1) / STRIP));
+}
+
+}  // namespace fir
