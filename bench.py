@@ -152,10 +152,18 @@ def main() -> int:
     local_rank = _env_int("LOCAL_RANK", 0)
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # FIR_DIST_BACKEND=gloo rehearses the N>1 flow on a box with fewer GPUs than ranks (ranks
+    # share devices, halos staged through the host); the real multi-GPU run uses nccl (= RCCL).
+    backend = os.environ.get("FIR_DIST_BACKEND", "nccl")
+    dev_index = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
+    red_dev = dev if backend == "nccl" else torch.device("cpu")
 
     stream = torch.cuda.Stream(device=dev)  # a dedicated (non-null) stream for every launch
     torch.cuda.set_stream(stream)
@@ -164,7 +172,10 @@ def main() -> int:
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local_rank])
+            if backend == "nccl":
+                dist.barrier(device_ids=[dev_index])
+            else:
+                dist.barrier()
 
     for _ in range(args.warmup):
         wl.step()
@@ -177,9 +188,20 @@ def main() -> int:
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # parity: full output vs the C oracle (every rank, its own segment with the received halos)
+    parity = "skipped"
+    if not args.no_parity:
+        ref = wl.oracle(_cpu_threads())
+        ok = bool(np.array_equal(wl.y.cpu().numpy(), ref))
+        if world > 1:
+            f = torch.tensor([0 if ok else 1], device=red_dev)
+            dist.all_reduce(f, op=dist.ReduceOp.MAX)
+            ok = int(f.item()) == 0
+        parity = "bit-exact vs C oracle (full output, every rank)" if ok else "MISMATCH"
 
     # Roofline: the dominant (bulk) kernel alone, `steps` back-to-back launches on the stream it
     # runs on, bracketed by two HIP events (events between launches would perturb the stream:
@@ -192,17 +214,6 @@ def main() -> int:
     ev1.record()
     ev1.synchronize()
     kern_avg_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
-
-    # parity: full output vs the C oracle (every rank, its own segment with the received halos)
-    parity = "skipped"
-    if not args.no_parity:
-        ref = wl.oracle(_cpu_threads())
-        ok = bool(np.array_equal(wl.y.cpu().numpy(), ref))
-        if world > 1:
-            f = torch.tensor([0 if ok else 1], device=dev)
-            dist.all_reduce(f, op=dist.ReduceOp.MAX)
-            ok = int(f.item()) == 0
-        parity = "bit-exact vs C oracle (full output, every rank)" if ok else "MISMATCH"
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -223,9 +234,11 @@ def main() -> int:
     pmc = ROOT / "profiles" / f"pmc_{args.workload}.json"
     if pmc.exists():
         try:
-            traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
+            summary = json.loads(pmc.read_text())
         except (ValueError, OSError):
-            traffic = None
+            summary = {}
+        if summary.get("algorithmic_bytes_per_launch") == wl.units * wl.bytes_per_unit:
+            traffic = summary.get("hbm_bytes_per_launch")  # only for the profiled workload size
 
     total_units = wl.units * world * args.steps
     value = total_units / elapsed / 1e9

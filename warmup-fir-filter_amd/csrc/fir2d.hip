@@ -53,20 +53,12 @@ static hipError_t launch2d_reg(const uint8_t* x, void* y, int64_t H, int64_t W, 
                                int acc_bits, hipStream_t s) {
     using OutT = typename OutTraits<STAGE>::T;
     Taps2<R, C> t;
-    bool taps16 = true;
     for (int m = 0; m < R; ++m)
-        for (int n = 0; n < C; ++n) {
-            t.h[m][n] = hq[m * C + n];
-            taps16 &= t.h[m][n] >= -32768 && t.h[m][n] <= 32767;
-        }
-    pack_taps2(t);
+        for (int n = 0; n < C; ++n) t.h[m][n] = hq[m * C + n];
+    pack_taps2(t);  // packed v_dot2_i32_i16 taps: two MACs per instruction (taps are int16 here)
     const dim3 grid = fir2d_reg_grid<kVec2d, kStrip2d>(H, W);
-    if (taps16)  // packed v_dot2_i32_i16: two MACs per instruction
-        hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2d, true>), grid, dim3(kBlock), 0, s, x,
-                           (OutT*)y, H, W, t, 32 - acc_bits, frac);
-    else
-        hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2d, false>), grid, dim3(kBlock), 0, s, x,
-                           (OutT*)y, H, W, t, 32 - acc_bits, frac);
+    hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2d, true>), grid, dim3(kBlock), 0, s, x, (OutT*)y,
+                       H, W, t, 32 - acc_bits, frac);
     return hipGetLastError();
 }
 
@@ -93,10 +85,10 @@ int launch_fir2d(const uint8_t* x, int64_t H, int64_t W, const int32_t* hq, int 
     if (H == 0 || W == 0) return FIR_OK;
     if (!x || !y) return *err = "x and y must not be NULL", FIR_EINVAL;
     if (H > 65535 * (int64_t)kStrip2d) return *err = "height too large", FIR_EINVAL;
-    bool taps24 = true;
-    for (int k = 0; k < R * C; ++k) taps24 &= (hq[k] >= -(1 << 23) && hq[k] < (1 << 23));
+    bool taps16 = true;  // the register kernel multiplies on v_dot2_i32_i16
+    for (int k = 0; k < R * C; ++k) taps16 &= (hq[k] >= -32768 && hq[k] <= 32767);
     const bool fast = reg2d_shape(R, C) && W % kVec2d == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)y % 16 == 0 &&
-                      acc_bits <= 32 && frac <= 31 && taps24 && W >= kVec2d;
+                      acc_bits <= 32 && frac <= 31 && taps16 && W >= kVec2d;
     hipError_t e;
     if (fast) {
         e = stage == FIR_OUT_U8_SAT ? launch2d_reg_shape<FIR_OUT_U8_SAT>(R, C, x, y, H, W, hq, frac, acc_bits, stream)

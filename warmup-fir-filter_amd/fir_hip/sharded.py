@@ -40,20 +40,31 @@ def post_halo_exchange(seg: torch.Tensor, taps: int, channels: int = 1, group=No
     hl, hr = halo_sizes(taps, channels)
     if seg.numel() < max(hl, hr):
         raise ValueError("segment shorter than the filter halo")
+    staged = seg.is_cuda and dist.get_backend(group) == "gloo"
+    # gloo has no device point-to-point: the few halo samples are staged through the host
+    # (only to rehearse the multi-rank flow on a single-GPU box; RCCL sends device buffers)
+    buf_dev = torch.device("cpu") if staged else seg.device
+
+    def _send(t):
+        return t.cpu() if staged else t.contiguous()
+
     ops, left, right = [], None, None
     if rank > 0:
         if hl:
-            left = torch.empty(hl, dtype=seg.dtype, device=seg.device)
+            left = torch.empty(hl, dtype=seg.dtype, device=buf_dev)
             ops.append(dist.P2POp(dist.irecv, left, _peer(group, rank - 1), group))
         if hr:
-            ops.append(dist.P2POp(dist.isend, seg[:hr].contiguous(), _peer(group, rank - 1), group))
+            ops.append(dist.P2POp(dist.isend, _send(seg[:hr]), _peer(group, rank - 1), group))
     if rank < world - 1:
         if hr:
-            right = torch.empty(hr, dtype=seg.dtype, device=seg.device)
+            right = torch.empty(hr, dtype=seg.dtype, device=buf_dev)
             ops.append(dist.P2POp(dist.irecv, right, _peer(group, rank + 1), group))
         if hl:
-            ops.append(dist.P2POp(dist.isend, seg[seg.numel() - hl:].contiguous(), _peer(group, rank + 1), group))
+            ops.append(dist.P2POp(dist.isend, _send(seg[seg.numel() - hl:]), _peer(group, rank + 1), group))
     works = dist.batch_isend_irecv(ops) if ops else []
+    if staged:
+        wait_all(works)
+        return (None if left is None else left.to(seg.device), None if right is None else right.to(seg.device), [])
     return left, right, works
 
 
