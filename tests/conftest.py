@@ -6,6 +6,7 @@ the host-side validation logic, the C-ABI exports and the sharded driver over gl
 """
 from __future__ import annotations
 
+import functools
 import json
 import sys
 from pathlib import Path
@@ -46,9 +47,15 @@ def load_kats(kind: str) -> list[dict]:
     return recs
 
 
+@functools.lru_cache(maxsize=None)
+def _ragged_arrays(name: str) -> dict:
+    with np.load(GOLDEN / f"random_{name}.npz") as d:  # NpzFile re-inflates on every d[key]
+        return {k: d[k] for k in d.files}
+
+
 def iter_ragged(name: str):
     """Yield (x, h, params, y) from random_{fixed,ideal}.npz."""
-    d = np.load(GOLDEN / f"random_{name}.npz")
+    d = _ragged_arrays(name)
     xo, ho, yo = d["x_off"], d["h_off"], d["y_off"]
     for i in range(len(xo) - 1):
         params = tuple(int(v) for v in d["params"][i]) if d["params"].shape[1] else ()
