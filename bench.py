@@ -140,8 +140,8 @@ class Workload:
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=100, help="untimed steps (clocks take ~40 launches to ramp)")
     ap.add_argument("--workload", default="fir1d_i16", choices=("fir1d_i16", "cplx_i16", "fir2d_u8"))
     ap.add_argument("--log2n", type=int, default=28, help="int16 values per GPU (2^28 = BASELINE configs[1])")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0 = skip)")
@@ -192,17 +192,6 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # parity: full output vs the C oracle (every rank, its own segment with the received halos)
-    parity = "skipped"
-    if not args.no_parity:
-        ref = wl.oracle(_cpu_threads())
-        ok = bool(np.array_equal(wl.y.cpu().numpy(), ref))
-        if world > 1:
-            f = torch.tensor([0 if ok else 1], device=red_dev)
-            dist.all_reduce(f, op=dist.ReduceOp.MAX)
-            ok = int(f.item()) == 0
-        parity = "bit-exact vs C oracle (full output, every rank)" if ok else "MISMATCH"
-
     # Roofline: the dominant (bulk) kernel alone, `steps` back-to-back launches on the stream it
     # runs on, bracketed by two HIP events (events between launches would perturb the stream:
     # each record adds a ~11 us gap).  Average duration = event time / launches.
@@ -214,6 +203,20 @@ def main() -> int:
     ev1.record()
     ev1.synchronize()
     kern_avg_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
+
+    wl.step()  # restore the full step's output (the loop above ran the bulk kernel alone)
+    torch.cuda.synchronize()
+
+    # parity: full output vs the C oracle (every rank, its own segment with the received halos)
+    parity = "skipped"
+    if not args.no_parity:
+        ref = wl.oracle(_cpu_threads())
+        ok = bool(np.array_equal(wl.y.cpu().numpy(), ref))
+        if world > 1:
+            f = torch.tensor([0 if ok else 1], device=red_dev)
+            dist.all_reduce(f, op=dist.ReduceOp.MAX)
+            ok = int(f.item()) == 0
+        parity = "bit-exact vs C oracle (full output, every rank)" if ok else "MISMATCH"
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:

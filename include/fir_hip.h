@@ -16,6 +16,9 @@
  *                         one per row.  A single row is the fir_1d_fixed_golden call itself.
  *   fir1d_fixed_rows_dev  same, device buffers, asynchronous on a caller stream (bench,
  *                         sharded driver, graph capture).
+ *   fir1d_fixed_rows_multi[_dev] the same for F coefficient sets over one input: the loop
+ *                         over a bank's filters in gen_fixed_output.py:92-105, one read of x
+ *                         for up to 4 filters.
  *   fir1d_fixed_edges_dev recomputes the first (L-1-L/2) and last (L/2) outputs of a
  *                         segment from neighbour halo samples (multi-GPU sharding, SURVEY
  *                         §8(e)); no reference counterpart (the reference is one process).
@@ -75,6 +78,16 @@ int fir1d_fixed_rows_dev(const void* x_dev, int in_dtype, int64_t rows, int64_t 
                          int channels, const int32_t* hq, int taps, int frac_bits, int acc_bits,
                          int out_stage, void* y_dev, void* stream);
 
+/* F filters of `taps` taps each over the same x: hq is F x taps (row-major), y holds F
+ * consecutive output planes shaped like x (plane f at y + f * rows*width*channels elements).
+ * Results are identical to F calls of fir1d_fixed_rows; u8 input reads x once per 4 filters. */
+int fir1d_fixed_rows_multi(const void* x, int in_dtype, int64_t rows, int64_t width, int channels,
+                           const int32_t* hq, int taps, int filters, int frac_bits, int acc_bits, int out_stage,
+                           void* y, int device);
+int fir1d_fixed_rows_multi_dev(const void* x_dev, int in_dtype, int64_t rows, int64_t width, int channels,
+                               const int32_t* hq, int taps, int filters, int frac_bits, int acc_bits,
+                               int out_stage, void* y_dev, void* stream);
+
 /* Recompute the first (taps-1-taps/2)*channels and last (taps/2)*channels outputs of a
  * single-row segment of n*channels samples, reading out-of-segment samples from
  * halo_left_dev ((taps-1-taps/2)*channels samples preceding the segment) and
@@ -101,6 +114,16 @@ int fir1d_ideal_rows(const uint8_t* x, int64_t rows, int64_t width, const double
                      double* y, int device);
 int fir1d_ideal_rows_dev(const uint8_t* x_dev, int64_t rows, int64_t width, const double* h,
                          int taps, double* y_dev, void* stream);
+
+/* ---- fixed-vs-ideal comparison metrics -----------------------------
+ * One pass over `n` samples of ideal (float64) and fixed (uint8) outputs.  out[9] =
+ * {max|d|, sum|d|, sum d^2, sum d, #(fixed==0), #(fixed==255), #(ideal<0 or >255), n, 0}
+ * with d = fixed - ideal; the report ratios are these over n.  Float64 sums are
+ * compensated and reduced in a fixed order (deterministic); counts and max are exact. */
+int64_t fir_metrics_work_bytes(void);
+int fir_compare_metrics(const double* ideal, const uint8_t* fixed, int64_t n, double* out, int device);
+int fir_compare_metrics_dev(const double* ideal_dev, const uint8_t* fixed_dev, int64_t n, double* out_dev,
+                            void* work_dev, void* stream);
 
 #ifdef __cplusplus
 }

@@ -288,3 +288,44 @@ def test_repeat_launch_deterministic():
     b = torch_ops.fir1d_fixed_rows_dev(x, TAPS["wrap5"])
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+# ---- multi-filter fusion ----------------------------------------------
+def test_multi_filter_banks_equal_reference_outputs(images, image_outputs):
+    """One fused call per (image, bank) reproduces all 56 reference fixed outputs."""
+    by_key = {(o["case_stem"], o["tap"], o["coeff_name"]): o["fixed_u8_sha256"] for o in image_outputs["outputs"]}
+    for stem, x in images.items():
+        for tap, bank in (("3tap", h_coeff_3tap_map), ("5tap", h_coeff_5tap_map)):
+            hq = np.stack([fo.quantize_h(h) for h in bank.values()])
+            ys = fir_hip.fir1d_fixed_rows_multi(x, hq)
+            for name, y in zip(bank, ys):
+                assert _sha(y) == by_key[(stem, tap, name)], (stem, tap, name)
+
+
+@pytest.mark.parametrize("F", [1, 2, 3, 4, 5, 9])
+@pytest.mark.parametrize("dtype,L", [(np.uint8, 3), (np.uint8, 5), (np.uint8, 12), (np.int16, 5)])
+def test_multi_filter_random_vs_oracle(F, dtype, L):
+    rng = np.random.default_rng(F * 100 + L)
+    if dtype == np.uint8:
+        x = rng.integers(0, 256, (61, 1283), dtype=np.uint8)
+    else:
+        x = rng.integers(-32768, 32768, (7, 10_001), dtype=np.int16)
+    hq = rng.integers(-5000, 5000, (F, L))
+    for stage in (fir_hip.OUT_U8_SAT, fir_hip.OUT_I32):
+        ys = fir_hip.fir1d_fixed_rows_multi(x, hq, 12, 32, stage)
+        assert ys.shape == (F,) + x.shape
+        for f in range(F):
+            assert np.array_equal(ys[f], fo.fir1d_rows(x, hq[f], 12, 32, stage)), (f, stage)
+
+
+def test_generator_over_golden_images_uses_fused_path(tmp_path, images, image_outputs):
+    inp = tmp_path / "input"
+    inp.mkdir()
+    for stem, x in images.items():
+        np.save(inp / f"{stem}_x_u8.npy", x)
+    out = tmp_path / "output"
+    assert generate_fixed_3tap_output_vector(input_dir=inp, output_dir=out) == 28
+    assert generate_fixed_5tap_output_vector(input_dir=inp, output_dir=out) == 28
+    for o in image_outputs["outputs"]:
+        p = out / f"fixed_{o['tap']}" / f"{o['case_stem']}__{o['coeff_name']}_fixed_{o['tap']}_y_u8.npy"
+        assert _sha(np.load(p)) == o["fixed_u8_sha256"], p.name

@@ -1,0 +1,104 @@
+"""GPU end-to-end: the pipeline driver (BASELINE configs[0]) and the report metrics kernel.
+
+Runs warmup-fir-filter_amd/pipeline_fir_1d.py's run_pipeline on the 7 committed golden
+images in a temp dir and checks every artefact against the reference: all 56 fixed and 56
+ideal output files bit-exact (SHA-256), every per-case report metric against the
+reference's _compute_metrics values (counts / max exact, float sums to 1e-12 relative),
+and the report averages against the published accuracy numbers
+(fir_1d/docs/fir_1d_{3,5}tap_compare_analysis_v1.md:40-49).
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+
+import numpy as np
+import pytest
+
+import fir_hip
+from conftest import GOLDEN
+from oracle import c_oracle, fir_oracle as fo
+from pipeline_fir_1d import run_pipeline
+
+EXACT = ("num_samples", "max_abs_err", "sat_low_ratio", "sat_high_ratio", "sat_ratio", "clip_needed_ratio")
+CLOSE = ("mae", "rmse", "mean_err")
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def _check_metrics(got: dict, want: dict, what: str):
+    for k in EXACT:
+        assert got[k] == want[k], (what, k, got[k], want[k])
+    for k in CLOSE:
+        assert got[k] == pytest.approx(want[k], rel=1e-12, abs=1e-15), (what, k)
+
+
+def test_metrics_kernel_matches_reference_metrics(images, image_outputs):
+    co = c_oracle()
+    for o in image_outputs["outputs"]:
+        x = images[o["case_stem"]]
+        h = image_outputs["banks"][o["tap"]][o["coeff_name"]]
+        yi = co.fir1d_ideal_rows(x, h)
+        yf = co.fir1d_rows(x, fo.quantize_h(h), 12, 32, 0)
+        _check_metrics(fir_hip.compare_metrics(yi, yf), o["metrics"], o["case_stem"])
+
+
+def test_metrics_edge_cases():
+    assert fir_hip.compare_metrics(np.zeros(0), np.zeros(0, np.uint8))["num_samples"] == 0
+    rng = np.random.default_rng(1)
+    for n in (1, 255, 256, 257, 1000, 262_144 + 7):
+        yi = rng.uniform(-300, 600, n)
+        yf = rng.integers(0, 256, n, dtype=np.uint8)
+        _check_metrics(fir_hip.compare_metrics(yi, yf), fo.compute_metrics(yi, yf), str(n))
+    with pytest.raises(ValueError, match="Shape mismatch"):
+        fir_hip.compare_metrics(np.zeros(3), np.zeros(4, np.uint8))
+
+
+def test_pipeline_end_to_end_on_golden_images(tmp_path, image_outputs):
+    res = run_pipeline(tap="all", overwrite_vectors=False, skip_input=False, skip_ideal=False, skip_fixed=False,
+                       skip_report=False, skip_restore=True, restore_kind="all", ideal_policy="clip",
+                       overwrite_images=False, strict_report=True, strict_restore=False, top_k=5,
+                       image_dir=GOLDEN / "images_u8.npz", vector_dir=tmp_path / "vector",
+                       image_out_dir=tmp_path / "img")
+    assert res["ideal_counts"] == {"ideal_3tap": 28, "ideal_5tap": 28}
+    assert res["fixed_counts"] == {"fixed_3tap": 28, "fixed_5tap": 28}
+    out = tmp_path / "vector" / "output"
+    for o in image_outputs["outputs"]:
+        t, stem, c = o["tap"], o["case_stem"], o["coeff_name"]
+        assert _sha(np.load(out / f"fixed_{t}" / f"{stem}__{c}_fixed_{t}_y_u8.npy")) == o["fixed_u8_sha256"]
+        assert _sha(np.load(out / f"ideal_{t}" / f"{stem}__{c}_ideal_{t}_y_f64.npy")) == o["ideal_f64_sha256"]
+    published = {"3tap": (2.4078, 5.8063, 255.0, 0.2440), "5tap": (1.1302, 2.9380, 118.0625, 0.2579)}
+    for t in ("3tap", "5tap"):
+        summary = json.loads((out / f"report_{t}" / f"compare_{t}_summary.json").read_text())
+        assert not any(summary["validation"][k] for k in summary["validation"])
+        want = {(o["case_stem"], o["coeff_name"]): o["metrics"] for o in image_outputs["outputs"] if o["tap"] == t}
+        assert len(summary["cases"]) == 28
+        for row in summary["cases"]:
+            _check_metrics(row, want[(row["case_stem"], row["coeff_name"])], row["key"])
+        ov = summary["overall"]
+        mae, rmse, mx, sat = published[t]
+        assert (round(ov["avg_mae"], 4), round(ov["avg_rmse"], 4), ov["max_max_abs_err"],
+                round(ov["avg_sat_ratio"], 4)) == (mae, rmse, mx, sat)
+        assert (out / f"report_{t}" / f"compare_{t}_cases.csv").exists()
+    # second run: everything exists, nothing regenerated
+    res2 = run_pipeline(tap="3", overwrite_vectors=False, skip_input=False, skip_ideal=False, skip_fixed=False,
+                        skip_report=True, skip_restore=True, restore_kind="all", ideal_policy="clip",
+                        overwrite_images=False, strict_report=False, strict_restore=False, top_k=5,
+                        image_dir=GOLDEN / "images_u8.npz", vector_dir=tmp_path / "vector",
+                        image_out_dir=tmp_path / "img")
+    assert res2["ideal_counts"] == {"ideal_3tap": 0} and res2["fixed_counts"] == {"fixed_3tap": 0}
+    assert res2["input_manifest"]["skipped_cases"] == 7
+
+
+def test_pipeline_restore_small_images(tmp_path, images):
+    small = {k: v for k, v in images.items() if v.size <= 64 * 64}
+    np.savez(tmp_path / "small.npz", **small)
+    res = run_pipeline(tap="5", overwrite_vectors=True, skip_input=False, skip_ideal=False, skip_fixed=False,
+                       skip_report=False, skip_restore=False, restore_kind="all", ideal_policy="normalize",
+                       overwrite_images=True, strict_report=True, strict_restore=False, top_k=3,
+                       image_dir=tmp_path / "small.npz", vector_dir=tmp_path / "vector", image_out_dir=tmp_path / "img")
+    assert res["restore_summary"]["num_converted"] == 16
+    assert len(list((tmp_path / "img" / "ideal_5tap_normalize").glob("*.png"))) == 8
+    assert len(list((tmp_path / "img" / "fixed_5tap").glob("*.png"))) == 8

@@ -37,7 +37,7 @@ for s in $STEPS; do
         benchcplx) run bench_cplx 300 python bench.py --workload cplx_i16 --cpu-seconds 5; fatal $? ;;
         bench2d) run bench_2d 300 python bench.py --workload fir2d_u8 --cpu-seconds 5; fatal $? ;;
         prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-                  python bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-parity; fatal $? ;;
+                  python bench.py --steps 200 --warmup 100 --cpu-seconds 0 --no-parity; fatal $? ;;
         pmc) for c in FETCH_SIZE WRITE_SIZE; do
                  run "pmc_$c" 300 rocprofv3 --pmc "$c" --kernel-trace -d "$OUT/pmc_$c" -o run --output-format csv -- \
                      python bench.py --steps 10 --warmup 2 --cpu-seconds 0 --no-parity; fatal $? || exit

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "fir1d_reg.h"
+#include "old_fir1d_reg.h"  // r01f version (before the multi-filter template), A/B only
 
 using namespace fir;
 
@@ -134,10 +135,22 @@ template <int U, int FLAGS>
 static void launch_fir(const int16_t* x, int32_t* y, int64_t n, hipStream_t s, int pblocks) {
     RowGeom g{n, 0, 0};
     TapsN<5> t;
-    for (int k = 0; k < 5; ++k) t.h[k] = kTaps[k];
+    for (int k = 0; k < 5; ++k) t.h[0][k] = kTaps[k];
+    pack_taps(t);
     int64_t ntiles, blocks;
     reg_launch_geometry<int16_t, U, FLAGS>(n, pblocks, &ntiles, &blocks);
     hipLaunchKernelGGL((fir1d_reg_kernel<int16_t, FIR_OUT_I32, 5, 1, U, FLAGS>), dim3((unsigned)blocks),
+                       dim3(kBlock), 0, s, x, y, g, t, 0, 12, ntiles);
+}
+
+template <int U, int FLAGS>
+static void launch_fir_old(const int16_t* x, int32_t* y, int64_t n, hipStream_t s, int pblocks) {
+    fir_old::RowGeom g{n, 0, 0};
+    fir_old::TapsN<5> t;
+    for (int k = 0; k < 5; ++k) t.h[k] = kTaps[k];
+    int64_t ntiles, blocks;
+    fir_old::reg_launch_geometry<int16_t, U, FLAGS>(n, pblocks, &ntiles, &blocks);
+    hipLaunchKernelGGL((fir_old::fir1d_reg_kernel<int16_t, FIR_OUT_I32, 5, 1, U, FLAGS>), dim3((unsigned)blocks),
                        dim3(kBlock), 0, s, x, y, g, t, 0, 12, ntiles);
 }
 
@@ -181,18 +194,14 @@ int main(int argc, char** argv) {
     CK(hipStreamCreate(&st));
 
     std::vector<Variant> vs = {
-        {"fir U1 plain", true, launch_fir<1, 0>, 0, {}},
-        {"fir U2 plain", true, launch_fir<2, 0>, 0, {}},
-        {"fir U4 plain", true, launch_fir<4, 0>, 0, {}},
-        {"fir U1 nt-st", true, launch_fir<1, kNtStore>, 0, {}},
-        {"fir U1 nt-ld", true, launch_fir<1, kNtLoad>, 0, {}},
-        {"fir U1 nt-ld+st", true, launch_fir<1, kNtLoad | kNtStore>, 0, {}},
-        {"fir U2 nt-ld+st", true, launch_fir<2, kNtLoad | kNtStore>, 0, {}},
-        {"fir U2 persist2048", true, launch_fir<2, kPersist>, 2048, {}},
-        {"fir U1 persist4096", true, launch_fir<1, kPersist>, 4096, {}},
+        {"fir U1 mad (r01f)", true, launch_fir_old<1, 0>, 0, {}},
+        {"fir U1 mad", true, launch_fir<1, 0>, 0, {}},
+        {"fir U1 mad acc32", true, launch_fir<1, kAcc32>, 0, {}},
+        {"fir U1 dot2 acc32", true, launch_fir<1, kDot2 | kAcc32>, 0, {}},
+        {"fir U1 dot2", true, launch_fir<1, kDot2>, 0, {}},
+        {"fir U2 dot2 acc32", true, launch_fir<2, kDot2 | kAcc32>, 0, {}},
+        {"fir U1 dot2 acc32 nt-ld", true, launch_fir<1, kDot2 | kAcc32 | kNtLoad>, 0, {}},
         {"copy U1 plain", false, launch_copy<1, 0>, 0, {}},
-        {"copy U1 nt-st", false, launch_copy<1, kNtStore>, 0, {}},
-        {"copy-pol ld0 st-sc0", false, launch_copy_policy<0, 1>, 0, {}},
     };
 
     // correctness (FIR variants): sampled positions + both ends

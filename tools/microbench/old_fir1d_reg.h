@@ -15,18 +15,16 @@
 
 #include "fir_common.h"
 
-namespace fir {
+namespace fir_old {
+using namespace fir;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-typedef short fir_short2v __attribute__((ext_vector_type(2)));
 
 enum RegFlags : int {
     kNtLoad = 1,   // non-temporal 16-byte loads (streamed once)
     kNtStore = 2,  // non-temporal stores
     kPersist = 4,  // grid-stride over tiles with the next tile's loads issued early
-    kDot2 = 8,     // int16 samples, 1 channel, int16 taps: packed v_dot2_i32_i16 MACs
-    kAcc32 = 16,   // acc_bits == 32: the wrap is the hardware's, skip the shl/ashr pair
 };
 
 constexpr int kDppWaveRol1 = 0x134;  // lane i <- lane i+1, lane 63 <- lane 0
@@ -39,24 +37,10 @@ __device__ __forceinline__ uint32_t dpp_ror1(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppWaveRor1, 0xF, 0xF, false);
 }
 
-// F filters of L taps each (F > 1: several filters share one read of x).
-// pk[f][p] packs the taps of window samples 2p and 2p+1 (h[L-1-2p], h[L-2-2p]) as two
-// int16 halves for v_dot2 (0 past the end); filled by pack_taps() on the host.
-template <int L, int F = 1>
+template <int L>
 struct TapsN {
-    int32_t h[F][L];
-    uint32_t pk[F][(L + 1) / 2];
+    int32_t h[L];
 };
-
-template <int L, int F>
-inline void pack_taps(TapsN<L, F>& t) {
-    for (int f = 0; f < F; ++f)
-        for (int p = 0; p < (L + 1) / 2; ++p) {
-            const int lo = t.h[f][L - 1 - 2 * p];
-            const int hi = L - 2 - 2 * p >= 0 ? t.h[f][L - 2 - 2 * p] : 0;
-            t.pk[f][p] = ((uint32_t)lo & 0xFFFFu) | ((uint32_t)hi << 16);
-        }
-}
 
 struct RowGeom {
     int64_t total;      // samples in the buffer (rows * width * channels)
@@ -128,99 +112,44 @@ __device__ __forceinline__ void store_vec(typename OutTraits<STAGE>::T* __restri
     }
 }
 
-// (wrap(acc) + 2^(f-1)) >> f, with the wrap skipped when acc_bits == 32 (ACC32).
-template <bool ACC32>
-__device__ __forceinline__ int32_t round_acc(uint32_t acc, int shl, int frac) {
-    const int32_t a = ACC32 ? (int32_t)acc : (int32_t)(acc << shl) >> shl;
-    return (a >> frac) + ((a >> (frac - 1)) & 1);
-}
-
-// Sample pair (s, s+1) of the window as two int16 halves; window dword i holds samples
-// 2i - 2*NDL and 2i - 2*NDL + 1.  LAST_ZERO: the caller multiplies the high half by 0, so it
-// may come from outside the window.
-template <int NDL, int NW, int S, bool LAST_ZERO>
-__device__ __forceinline__ uint32_t sample_pair(const uint32_t* Wd) {
-    constexpr int e = S + 2 * NDL;  // sample index from the window start
-    if constexpr (e % 2 == 0) {
-        return Wd[e / 2];
-    } else if constexpr ((e + 1) / 2 < NW) {
-        return __builtin_amdgcn_alignbit(Wd[(e + 1) / 2], Wd[(e - 1) / 2], 16);  // v_alignbit_b32
+// Compute the VEC outputs of one vector from its window (left halo | own | right halo).
+template <typename InT, int L, int CH>
+__device__ __forceinline__ void fir_vector(const int32_t* w, int64_t col0, int64_t rowlen, const TapsN<L>& taps,
+                                           int shl, int frac, int32_t* q) {
+    constexpr int VEC = 4 * InTraits<InT>::kPerDword;
+    constexpr int C = L / 2;
+    constexpr int HLE = (L - 1 - C) * CH;
+    constexpr int HRE = C * CH;
+    const bool interior = col0 >= HLE && col0 + VEC + HRE <= rowlen;
+    if (interior) {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int k = 0; k < L; ++k) acc += (uint32_t)__mul24(taps.h[k], w[HLE + j + (C - k) * CH]);
+            q[j] = round32(acc, shl, frac);
+        }
     } else {
-        static_assert(LAST_ZERO, "pair leaves the window");
-        return Wd[(e - 1) / 2] >> 16;
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            int64_t cj = col0 + j;
+            if (cj >= rowlen) cj -= rowlen;  // the vector crossed into the next row
+            uint32_t acc = 0;
+#pragma unroll
+            for (int k = 0; k < L; ++k) {
+                const int64_t p = cj + (C - k) * CH;
+                const uint32_t t = (uint32_t)__mul24(taps.h[k], w[HLE + j + (C - k) * CH]);
+                acc += (p >= 0 && p < rowlen) ? t : 0u;
+            }
+            q[j] = round32(acc, shl, frac);
+        }
     }
 }
 
-template <int NDL, int NW, int L, int J, int P>
-struct Dot2Row {  // sum over tap pairs p >= P for output J (int16 samples, one channel)
-    __device__ static __forceinline__ uint32_t run(const uint32_t* Wd, const uint32_t* pk, uint32_t acc) {
-        if constexpr (P < (L + 1) / 2) {
-            constexpr int HL = L - 1 - L / 2;
-            constexpr int S = J - HL + 2 * P;
-            const uint32_t pr = sample_pair<NDL, NW, S, (L % 2 == 1) && (P == (L + 1) / 2 - 1)>(Wd);
-            acc = (uint32_t)__builtin_amdgcn_sdot2(__builtin_bit_cast(fir_short2v, pr),
-                                                   __builtin_bit_cast(fir_short2v, pk[P]), (int)acc, false);
-            return Dot2Row<NDL, NW, L, J, P + 1>::run(Wd, pk, acc);
-        } else {
-            return acc;
-        }
-    }
-};
-
-template <int NDL, int NW, int L, int J, int VEC, bool ACC32>
-struct Dot2Vec {
-    __device__ static __forceinline__ void run(const uint32_t* Wd, const uint32_t* pk, int shl, int frac,
-                                               int32_t* q) {
-        if constexpr (J < VEC) {
-            q[J] = round_acc<ACC32>(Dot2Row<NDL, NW, L, J, 0>::run(Wd, pk, 0u), shl, frac);
-            Dot2Vec<NDL, NW, L, J + 1, VEC, ACC32>::run(Wd, pk, shl, frac, q);
-        }
-    }
-};
-
-// Interior vector (the whole window inside one row): no masks.
-template <typename InT, int L, int CH, bool ACC32>
-__device__ __forceinline__ void fir_vector_interior(const int32_t* w, const int32_t* taps, int shl, int frac,
-                                                    int32_t* q) {
-    constexpr int VEC = 4 * InTraits<InT>::kPerDword;
-    constexpr int C = L / 2;
-    constexpr int HLE = (L - 1 - C) * CH;
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) {
-        uint32_t acc = 0;
-#pragma unroll
-        for (int k = 0; k < L; ++k) acc += (uint32_t)__mul24(taps[k], w[HLE + j + (C - k) * CH]);
-        q[j] = round_acc<ACC32>(acc, shl, frac);
-    }
-}
-
-// Vector whose window crosses a row edge (or the buffer ends): per-sample column masks.
-template <typename InT, int L, int CH, bool ACC32>
-__device__ __forceinline__ void fir_vector_masked(const int32_t* w, int64_t col0, int64_t rowlen, const int32_t* taps,
-                                               int shl, int frac, int32_t* q) {
-    constexpr int VEC = 4 * InTraits<InT>::kPerDword;
-    constexpr int C = L / 2;
-    constexpr int HLE = (L - 1 - C) * CH;
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) {
-        int64_t cj = col0 + j;
-        if (cj >= rowlen) cj -= rowlen;  // the vector crossed into the next row
-        uint32_t acc = 0;
-#pragma unroll
-        for (int k = 0; k < L; ++k) {
-            const int64_t p = cj + (C - k) * CH;
-            const uint32_t t = (uint32_t)__mul24(taps[k], w[HLE + j + (C - k) * CH]);
-            acc += (p >= 0 && p < rowlen) ? t : 0u;
-        }
-        q[j] = round_acc<ACC32>(acc, shl, frac);
-    }
-}
-
-// y holds F output planes of g.total samples each (plane f at y + f * g.total).
-template <typename InT, int STAGE, int L, int CH, int U, int FLAGS, int F = 1>
+template <typename InT, int STAGE, int L, int CH, int U, int FLAGS>
 __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict__ x,
                                                            typename OutTraits<STAGE>::T* __restrict__ y,
-                                                           RowGeom g, TapsN<L, F> taps, int shl, int frac,
+                                                           RowGeom g, TapsN<L> taps, int shl, int frac,
                                                            int64_t ntiles) {
     using IT = InTraits<InT>;
     constexpr int EPD = IT::kPerDword;
@@ -232,8 +161,6 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
     constexpr int NDL = (HLE + EPD - 1) / EPD;  // dwords shifted in from lane-1
     constexpr int NDR = (HRE + EPD - 1) / EPD;  // dwords shifted in from lane+1
     constexpr bool NTL = FLAGS & kNtLoad, NTS = FLAGS & kNtStore, PERSIST = FLAGS & kPersist;
-    constexpr bool DOT2 = (FLAGS & kDot2) && sizeof(InT) == 2 && CH == 1;
-    constexpr bool ACC32 = FLAGS & kAcc32;
     constexpr int WPB = kBlock / kWave;
 
     const int lane = threadIdx.x & (kWave - 1);
@@ -267,21 +194,31 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
         for (int u = 0; u < U; ++u) {
             const int64_t v = vb + u * kWave + lane;
             const int64_t g0 = v * VEC;
-            // window dwords: NDL from lane-1 | 4 own | NDR from lane+1
-            constexpr int NW = NDL + 4 + NDR;
-            uint32_t Wd[NW];
+            int32_t w[HLE + VEC + HRE];
+            if constexpr (NDL > 0) {
+                uint32_t prev[4];
 #pragma unroll
-            for (int qd = 0; qd < NDL; ++qd) {
-                const int src = 4 - NDL + qd;
-                const uint32_t seam = u == 0 ? hv[src] : dpp_ror1(own[u - 1][src]);
-                Wd[qd] = from_prev_lane(seam, own[u][src]);
+                for (int qd = 4 - NDL; qd < 4; ++qd) {
+                    const uint32_t seam = u == 0 ? hv[qd] : dpp_ror1(own[u - 1][qd]);
+                    prev[qd] = from_prev_lane(seam, own[u][qd]);
+                }
+#pragma unroll
+                for (int i = 0; i < HLE; ++i) {
+                    constexpr int base = VEC - HLE;
+                    w[i] = IT::get(prev[(base + i) / EPD], (base + i) % EPD);
+                }
             }
 #pragma unroll
-            for (int qd = 0; qd < 4; ++qd) Wd[NDL + qd] = own[u][qd];
+            for (int j = 0; j < VEC; ++j) w[HLE + j] = IT::get(own[u][j / EPD], j % EPD);
+            if constexpr (NDR > 0) {
+                uint32_t next[4];
 #pragma unroll
-            for (int qd = 0; qd < NDR; ++qd) {
-                const uint32_t seam = u == U - 1 ? hv[qd] : dpp_rol1(own[u + 1][qd]);
-                Wd[NDL + 4 + qd] = from_next_lane(seam, own[u][qd]);
+                for (int qd = 0; qd < NDR; ++qd) {
+                    const uint32_t seam = u == U - 1 ? hv[qd] : dpp_rol1(own[u + 1][qd]);
+                    next[qd] = from_next_lane(seam, own[u][qd]);
+                }
+#pragma unroll
+                for (int i = 0; i < HRE; ++i) w[HLE + VEC + i] = IT::get(next[i / EPD], i % EPD);
             }
             if (g0 < total) {
                 int64_t col0, rowlen;
@@ -292,28 +229,9 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
                     rowlen = total;
                     col0 = g0;
                 }
-                const bool interior = col0 >= HLE && col0 + VEC + HRE <= rowlen;
-                // samples of the window as int32 (first window sample = -HLE)
-                int32_t w[HLE + VEC + HRE];
-#pragma unroll
-                for (int i = 0; i < HLE + VEC + HRE; ++i) {
-                    constexpr int off = NDL * EPD - HLE;
-                    w[i] = IT::get(Wd[(off + i) / EPD], (off + i) % EPD);
-                }
-#pragma unroll
-                for (int f = 0; f < F; ++f) {
-                    int32_t q[VEC];
-                    if (__builtin_expect(interior, 1)) {
-                        if constexpr (DOT2) {
-                            Dot2Vec<NDL, NW, L, 0, VEC, ACC32>::run(Wd, taps.pk[f], shl, frac, q);
-                        } else {
-                            fir_vector_interior<InT, L, CH, ACC32>(w, taps.h[f], shl, frac, q);
-                        }
-                    } else {
-                        fir_vector_masked<InT, L, CH, ACC32>(w, col0, rowlen, taps.h[f], shl, frac, q);
-                    }
-                    store_vec<STAGE, VEC, NTS>(y + f * total, g0, total, v < nvec, q);
-                }
+                int32_t q[VEC];
+                fir_vector<InT, L, CH>(w, col0, rowlen, taps, shl, frac, q);
+                store_vec<STAGE, VEC, NTS>(y, g0, total, v < nvec, q);
             }
         }
         if constexpr (PERSIST) {

@@ -183,6 +183,44 @@ int fir1d_fixed_rows_dev(const void* x_dev, int in_dtype, int64_t rows, int64_t 
     }
 }
 
+int fir1d_fixed_rows_multi(const void* x, int in_dtype, int64_t rows, int64_t width, int channels,
+                           const int32_t* hq, int taps, int filters, int frac_bits, int acc_bits, int out_stage,
+                           void* y, int device) {
+    try {
+        int64_t n = 0, rw = 0, nf = 0;
+        if (channels < 1 || filters < 1 || !mul_ok(rows, width, &rw) || !mul_ok(rw, channels, &n) ||
+            !mul_ok(n, filters, &nf))
+            return fail(FIR_EINVAL, "invalid rows/width/channels/filters");
+        if (n == 0) {
+            std::string err;
+            int rc = fir::launch_fir1d_rows_multi(nullptr, in_dtype, 0, 0, channels, hq, taps, filters, frac_bits,
+                                                  acc_bits, out_stage, nullptr, nullptr, &err);
+            return rc ? fail(rc, err) : FIR_OK;
+        }
+        if (!x || !y) return fail(FIR_EINVAL, "x and y must not be NULL");
+        return run_host(device, x, (size_t)n * in_size(in_dtype), y, (size_t)nf * out_size(out_stage),
+                        [&](void* dx, void* dy, hipStream_t s, std::string* err) {
+                            return fir::launch_fir1d_rows_multi(dx, in_dtype, rows, width, channels, hq, taps, filters,
+                                                                frac_bits, acc_bits, out_stage, dy, s, err);
+                        });
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int fir1d_fixed_rows_multi_dev(const void* x_dev, int in_dtype, int64_t rows, int64_t width, int channels,
+                               const int32_t* hq, int taps, int filters, int frac_bits, int acc_bits, int out_stage,
+                               void* y_dev, void* stream) {
+    try {
+        std::string err;
+        int rc = fir::launch_fir1d_rows_multi(x_dev, in_dtype, rows, width, channels, hq, taps, filters, frac_bits,
+                                              acc_bits, out_stage, y_dev, (hipStream_t)stream, &err);
+        return rc ? fail(rc, err) : FIR_OK;
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
 int fir1d_fixed_edges_dev(const void* x_dev, int in_dtype, int64_t n, int channels, const int32_t* hq, int taps,
                           int frac_bits, int acc_bits, int out_stage, const void* halo_left_dev,
                           const void* halo_right_dev, void* y_dev, void* stream) {
@@ -254,6 +292,51 @@ int fir1d_ideal_rows_dev(const uint8_t* x_dev, int64_t rows, int64_t width, cons
     try {
         std::string err;
         int rc = fir::launch_fir1d_ideal(x_dev, rows, width, h, taps, y_dev, (hipStream_t)stream, &err);
+        return rc ? fail(rc, err) : FIR_OK;
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int64_t fir_metrics_work_bytes(void) { return (int64_t)fir::metrics_work_bytes(); }
+
+int fir_compare_metrics(const double* ideal, const uint8_t* fixed, int64_t n, double* out, int device) {
+    try {
+        if (n < 0 || !out || (n > 0 && (!ideal || !fixed))) return fail(FIR_EINVAL, "invalid arguments");
+        DeviceState* st = nullptr;
+        int rc = device_state(device, &st);
+        if (rc) return rc;
+        std::lock_guard<std::mutex> lk(st->mu);
+        if ((rc = init_locked(st, device))) return rc;
+        const size_t ib = (size_t)n * 8, fb = (size_t)n;
+        const size_t fo = (ib + 255) / 256 * 256;
+        if ((rc = ensure(st->in, fo + fb + 1)) || (rc = ensure(st->out, fir::metrics_work_bytes() + 256))) return rc;
+        char* din = (char*)st->in.ptr;
+        if (n > 0) {
+            HIP_TRY(hipMemcpyAsync(din, ideal, ib, hipMemcpyHostToDevice, st->stream));
+            HIP_TRY(hipMemcpyAsync(din + fo, fixed, fb, hipMemcpyHostToDevice, st->stream));
+        }
+        double* dout = (double*)st->out.ptr;
+        std::string err;
+        rc = fir::launch_metrics((const double*)din, (const uint8_t*)(din + fo), n, dout, (char*)st->out.ptr + 256,
+                                 st->stream, &err);
+        if (rc) {
+            (void)hipStreamSynchronize(st->stream);
+            return fail(rc, err);
+        }
+        HIP_TRY(hipMemcpyAsync(out, dout, 9 * sizeof(double), hipMemcpyDeviceToHost, st->stream));
+        HIP_TRY(hipStreamSynchronize(st->stream));
+        return FIR_OK;
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int fir_compare_metrics_dev(const double* ideal_dev, const uint8_t* fixed_dev, int64_t n, double* out_dev,
+                            void* work_dev, void* stream) {
+    try {
+        std::string err;
+        int rc = fir::launch_metrics(ideal_dev, fixed_dev, n, out_dev, work_dev, (hipStream_t)stream, &err);
         return rc ? fail(rc, err) : FIR_OK;
     } catch (...) {
         return fail(FIR_EHIP, "internal error");

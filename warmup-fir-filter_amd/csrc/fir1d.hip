@@ -92,36 +92,55 @@ constexpr int kRegU = 1;
 constexpr int kRegFlags = 0;
 constexpr int kPersistBlocks = 2048;
 
-template <typename InT, int STAGE, int L, int CH>
-static hipError_t launch_reg(const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
-                             const int32_t* hq, int frac, int acc_bits, hipStream_t stream) {
+template <typename InT, int STAGE, int L, int CH, int F, int FL>
+static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
+                                   const int32_t* hq, int frac, int acc_bits, hipStream_t stream) {
     using OutT = typename OutTraits<STAGE>::T;
     RowGeom g;
     g.total = total;
     g.rowlen32 = (uint32_t)(rows > 1 ? rowlen : 0);
     g.multi_row = rows > 1;
-    TapsN<L> t;
-    for (int k = 0; k < L; ++k) t.h[k] = hq[k];
+    TapsN<L, F> t;
+    for (int f = 0; f < F; ++f)
+        for (int k = 0; k < L; ++k) t.h[f][k] = hq[f * L + k];
+    pack_taps(t);
     int64_t ntiles = 0, blocks = 0;
-    reg_launch_geometry<InT, kRegU, kRegFlags>(total, kPersistBlocks, &ntiles, &blocks);
-    hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, kRegU, kRegFlags>), dim3((unsigned)blocks), dim3(kBlock),
-                       0, stream, (const InT*)x, (OutT*)y, g, t, 32 - acc_bits, frac, ntiles);
+    reg_launch_geometry<InT, kRegU, FL>(total, kPersistBlocks, &ntiles, &blocks);
+    hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, kRegU, FL, F>), dim3((unsigned)blocks), dim3(kBlock), 0,
+                       stream, (const InT*)x, (OutT*)y, g, t, 32 - acc_bits, frac, ntiles);
     return hipGetLastError();
 }
 
-template <typename InT, int STAGE, int CH>
+// Picks the kernel variant: acc_bits == 32 drops the wrap shifts; int16 samples with int16
+// taps (one channel) multiply on packed v_dot2_i32_i16.
+template <typename InT, int STAGE, int L, int CH, int F>
+static hipError_t launch_reg(const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
+                             const int32_t* hq, int frac, int acc_bits, hipStream_t stream) {
+    bool taps16 = true;
+    for (int k = 0; k < F * L; ++k) taps16 &= hq[k] >= -32768 && hq[k] <= 32767;
+    const bool acc32 = acc_bits == 32;
+    if constexpr (sizeof(InT) == 2 && CH == 1) {
+        if (taps16)
+            return acc32 ? launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kDot2 | kAcc32>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream)
+                         : launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kDot2>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
+    }
+    return acc32 ? launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kAcc32>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream)
+                 : launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
+}
+
+template <typename InT, int STAGE, int CH, int F>
 static hipError_t launch_reg_taps(int L, const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
                                   const int32_t* hq, int frac, int acc_bits, hipStream_t s) {
     switch (L) {
-        case 1: return launch_reg<InT, STAGE, 1, CH>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 2: return launch_reg<InT, STAGE, 2, CH>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 3: return launch_reg<InT, STAGE, 3, CH>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 4: return launch_reg<InT, STAGE, 4, CH>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 5: return launch_reg<InT, STAGE, 5, CH>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 6: return launch_reg<InT, STAGE, 6, CH>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 7: return launch_reg<InT, STAGE, 7, CH>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 8: return launch_reg<InT, STAGE, 8, CH>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 9: return launch_reg<InT, STAGE, 9, CH>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 1: return launch_reg<InT, STAGE, 1, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 2: return launch_reg<InT, STAGE, 2, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 3: return launch_reg<InT, STAGE, 3, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 4: return launch_reg<InT, STAGE, 4, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 5: return launch_reg<InT, STAGE, 5, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 6: return launch_reg<InT, STAGE, 6, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 7: return launch_reg<InT, STAGE, 7, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 8: return launch_reg<InT, STAGE, 8, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 9: return launch_reg<InT, STAGE, 9, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -173,6 +192,17 @@ static int check_common(int in_dtype, int64_t rows, int64_t width, int ch, const
     return FIR_OK;
 }
 
+// Conditions for the register/DPP kernel (otherwise the generic LDS kernel runs).
+static bool reg_path_ok(const void* x, const void* y, int in_dtype, int64_t rows, int64_t rowlen, int64_t total,
+                        int ch, const int32_t* hq, int nh, int L, int frac, int acc_bits) {
+    const int vec = in_dtype == FIR_IN_U8 ? 16 : 8;
+    bool taps24 = true;
+    for (int k = 0; k < nh; ++k) taps24 &= (hq[k] >= -(1 << 23) && hq[k] < (1 << 23));
+    return L <= 9 && (ch == 1 || (ch == 2 && in_dtype == FIR_IN_I16)) && acc_bits <= 32 && frac <= 31 && taps24 &&
+           ((uintptr_t)x % 16 == 0) && ((uintptr_t)y % 16 == 0) &&
+           (rows == 1 || (rowlen >= vec + (L - 1) * ch && total < ((int64_t)1 << 32)));
+}
+
 int launch_fir1d_rows(const void* x, int in_dtype, int64_t rows, int64_t width, int ch, const int32_t* hq, int L,
                       int frac, int acc_bits, int stage, void* y, hipStream_t stream, std::string* err) {
     int rc = check_common(in_dtype, rows, width, ch, hq, L, frac, acc_bits, stage, err);
@@ -181,35 +211,71 @@ int launch_fir1d_rows(const void* x, int in_dtype, int64_t rows, int64_t width, 
     const int64_t total = rows * rowlen;
     if (total == 0) return FIR_OK;
     if (!x || !y) return *err = "x and y must not be NULL", FIR_EINVAL;
-
-    const int vec = in_dtype == FIR_IN_U8 ? 16 : 8;
-    const int c = L / 2;
-    bool taps24 = true;
-    for (int k = 0; k < L; ++k) taps24 &= (hq[k] >= -(1 << 23) && hq[k] < (1 << 23));
-    const bool fast = L <= 9 && (ch == 1 || (ch == 2 && in_dtype == FIR_IN_I16)) && acc_bits <= 32 && frac <= 31 &&
-                      taps24 && ((uintptr_t)x % 16 == 0) && ((uintptr_t)y % 16 == 0) &&
-                      (rows == 1 || (rowlen >= vec + (L - 1) * ch && total < ((int64_t)1 << 32)));
-    (void)c;
     hipError_t e;
-    if (fast) {
+    if (reg_path_ok(x, y, in_dtype, rows, rowlen, total, ch, hq, L, L, frac, acc_bits)) {
         if (in_dtype == FIR_IN_U8) {
             e = stage == FIR_OUT_U8_SAT
-                    ? launch_reg_taps<uint8_t, FIR_OUT_U8_SAT, 1>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream)
-                    : launch_reg_taps<uint8_t, FIR_OUT_I32, 1>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
+                    ? launch_reg_taps<uint8_t, FIR_OUT_U8_SAT, 1, 1>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream)
+                    : launch_reg_taps<uint8_t, FIR_OUT_I32, 1, 1>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
         } else if (ch == 1) {
             e = stage == FIR_OUT_U8_SAT
-                    ? launch_reg_taps<int16_t, FIR_OUT_U8_SAT, 1>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream)
-                    : launch_reg_taps<int16_t, FIR_OUT_I32, 1>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
+                    ? launch_reg_taps<int16_t, FIR_OUT_U8_SAT, 1, 1>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream)
+                    : launch_reg_taps<int16_t, FIR_OUT_I32, 1, 1>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
         } else {
             e = stage == FIR_OUT_U8_SAT
-                    ? launch_reg_taps<int16_t, FIR_OUT_U8_SAT, 2>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream)
-                    : launch_reg_taps<int16_t, FIR_OUT_I32, 2>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
+                    ? launch_reg_taps<int16_t, FIR_OUT_U8_SAT, 2, 1>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream)
+                    : launch_reg_taps<int16_t, FIR_OUT_I32, 2, 1>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
         }
     } else {
         e = dispatch_generic(in_dtype, stage, x, y, 0, total, total, rowlen, rows > 1, ch, nullptr, nullptr, hq, L,
                              frac, acc_bits, stream);
     }
     if (e != hipSuccess) return *err = std::string("fir1d launch failed: ") + hipGetErrorString(e), FIR_EHIP;
+    return FIR_OK;
+}
+
+// u8 images: up to 4 filters per launch share one read of x.
+template <int STAGE>
+static hipError_t launch_multi_u8(int F, int L, const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
+                                  const int32_t* hq, int frac, int acc_bits, hipStream_t s) {
+    switch (F) {
+        case 1: return launch_reg_taps<uint8_t, STAGE, 1, 1>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 2: return launch_reg_taps<uint8_t, STAGE, 1, 2>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 3: return launch_reg_taps<uint8_t, STAGE, 1, 3>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 4: return launch_reg_taps<uint8_t, STAGE, 1, 4>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+int launch_fir1d_rows_multi(const void* x, int in_dtype, int64_t rows, int64_t width, int ch, const int32_t* hq,
+                            int L, int F, int frac, int acc_bits, int stage, void* y, hipStream_t stream,
+                            std::string* err) {
+    if (F < 1) return *err = "filters must be >= 1", FIR_EINVAL;
+    int rc = check_common(in_dtype, rows, width, ch, hq, L, frac, acc_bits, stage, err);
+    if (rc) return rc;
+    const int64_t rowlen = width * ch;
+    const int64_t total = rows * rowlen;
+    if (total == 0) return FIR_OK;
+    if (!x || !y) return *err = "x and y must not be NULL", FIR_EINVAL;
+    const size_t osz = stage == FIR_OUT_I32 ? 4 : 1;
+    const bool fused = in_dtype == FIR_IN_U8 && ch == 1 && (total * (int64_t)osz) % 16 == 0 &&
+                       reg_path_ok(x, y, in_dtype, rows, rowlen, total, ch, hq, F * L, L, frac, acc_bits);
+    for (int f0 = 0; f0 < F;) {
+        const int nf = fused ? (F - f0 < 4 ? F - f0 : 4) : 1;
+        void* yf = (char*)y + (size_t)f0 * (size_t)total * osz;
+        const int32_t* hf = hq + (size_t)f0 * L;
+        if (fused) {
+            const hipError_t e =
+                stage == FIR_OUT_U8_SAT
+                    ? launch_multi_u8<FIR_OUT_U8_SAT>(nf, L, x, yf, rows, total, rowlen, hf, frac, acc_bits, stream)
+                    : launch_multi_u8<FIR_OUT_I32>(nf, L, x, yf, rows, total, rowlen, hf, frac, acc_bits, stream);
+            if (e != hipSuccess) return *err = std::string("fir1d multi launch failed: ") + hipGetErrorString(e), FIR_EHIP;
+        } else {
+            rc = launch_fir1d_rows(x, in_dtype, rows, width, ch, hf, L, frac, acc_bits, stage, yf, stream, err);
+            if (rc) return rc;
+        }
+        f0 += nf;
+    }
     return FIR_OK;
 }
 

@@ -12,6 +12,11 @@ namespace fir {
 int launch_fir1d_rows(const void* x, int in_dtype, int64_t rows, int64_t width, int ch, const int32_t* hq, int L,
                       int frac, int acc_bits, int stage, void* y, hipStream_t stream, std::string* err);
 
+// F filters of L taps (hq row-major F x L) over the same x; y = F consecutive output planes.
+int launch_fir1d_rows_multi(const void* x, int in_dtype, int64_t rows, int64_t width, int ch, const int32_t* hq,
+                            int L, int F, int frac, int acc_bits, int stage, void* y, hipStream_t stream,
+                            std::string* err);
+
 // Recompute the halo-dependent edge outputs of a single-row segment.
 int launch_fir1d_edges(const void* x, int in_dtype, int64_t n, int ch, const int32_t* hq, int L, int frac,
                        int acc_bits, int stage, const void* halo_left, const void* halo_right, void* y,
@@ -24,5 +29,10 @@ int launch_fir2d(const uint8_t* x, int64_t height, int64_t width, const int32_t*
 // float64 ideal model over uint8 rows.
 int launch_fir1d_ideal(const uint8_t* x, int64_t rows, int64_t width, const double* h, int L, double* y,
                        hipStream_t stream, std::string* err);
+
+// Fixed-vs-ideal comparison metrics (one pass); `work` >= metrics_work_bytes().
+size_t metrics_work_bytes();
+int launch_metrics(const double* ideal, const uint8_t* fixed, int64_t n, double* out, void* work,
+                   hipStream_t stream, std::string* err);
 
 }  // namespace fir

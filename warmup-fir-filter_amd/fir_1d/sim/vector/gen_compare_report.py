@@ -1,0 +1,164 @@
+"""Ideal-vs-fixed comparison report, shared by the 3-tap and 5-tap stages.
+
+Mirrors the reference's twin modules ``fir_1d/sim/vector/gen_{3,5}tap_compare_report.py``
+(identical except the tap literal): the same file pairing (``{case}__{coeff}_ideal_Ntap_y_f64.npy``
+with ``..._fixed_Ntap_y_u8.npy``), validation lists and strict-mode error, CSV columns,
+summary-JSON sections (config / validation / overall / by_coeff / worst_cases_by_rmse /
+cases), console summary and return value.  The per-case metrics (:67-112 there) are one
+fused GPU reduction (``fir_hip.compare_metrics``) instead of seven NumPy passes; counts and
+max|d| are exact, the float64 sums agree with NumPy's to ~1e-15 relative.
+"""
+from __future__ import annotations
+
+import csv
+import json
+import re
+from datetime import datetime, timezone
+from pathlib import Path
+from typing import Any
+
+import numpy as np
+
+import fir_hip
+
+THIS_FILE = Path(__file__).resolve()
+DEFAULT_OUTPUT_DIR = THIS_FILE.parent / "output"
+
+CSV_FIELDS = ["key", "case_stem", "coeff_name", "height", "width", "num_samples", "max_abs_err", "mae", "rmse",
+              "mean_err", "sat_low_ratio", "sat_high_ratio", "sat_ratio", "clip_needed_ratio", "ideal_file",
+              "fixed_file"]
+_AVG_COLS = ["max_abs_err", "mae", "rmse", "mean_err", "sat_low_ratio", "sat_high_ratio", "sat_ratio",
+             "clip_needed_ratio"]
+_MAX_COLS = ["max_abs_err", "mae", "rmse", "sat_ratio"]
+_VALIDATION_KEYS = ["invalid_ideal_filenames", "invalid_fixed_filenames", "duplicate_ideal_keys",
+                    "duplicate_fixed_keys", "missing_ideal_keys", "missing_fixed_keys", "shape_mismatch_cases"]
+
+
+def name_patterns(tap: str) -> tuple[re.Pattern, re.Pattern]:
+    return (re.compile(rf"^(?P<case_stem>.+?)__(?P<coeff_name>.+)_ideal_{tap}_y_f64\.npy$"),
+            re.compile(rf"^(?P<case_stem>.+?)__(?P<coeff_name>.+)_fixed_{tap}_y_u8\.npy$"))
+
+
+def _collect(directory: Path, pattern: re.Pattern):
+    found, invalid, dups = {}, [], []
+    for path in sorted((p for p in directory.glob("*.npy") if p.is_file()), key=lambda p: p.name.lower()):
+        m = pattern.match(path.name)
+        if m is None:
+            invalid.append(path.name)
+            continue
+        key = (m.group("case_stem"), m.group("coeff_name"))
+        if key in found:
+            dups.append(f"{key[0]}__{key[1]}")
+        else:
+            found[key] = path
+    return found, invalid, sorted(dups)
+
+
+def compute_metrics(y_ideal: np.ndarray, y_fixed: np.ndarray) -> dict[str, float | int]:
+    """Per-case metrics (reference :67-112) on the GPU."""
+    if y_ideal.shape != y_fixed.shape:
+        raise ValueError(f"Shape mismatch: ideal={y_ideal.shape}, fixed={y_fixed.shape}")
+    if y_fixed.dtype != np.uint8:
+        y_fixed = y_fixed.astype(np.uint8)
+    return fir_hip.compare_metrics(y_ideal, y_fixed)
+
+
+def summarize_rows(rows: list[dict[str, Any]]) -> dict[str, Any]:
+    out: dict[str, Any] = {"num_cases": len(rows),
+                           "num_samples_total": int(sum(int(r["num_samples"]) for r in rows))}
+    for c in _AVG_COLS:
+        out[f"avg_{c}"] = float(np.mean([float(r[c]) for r in rows])) if rows else 0.0
+    for c in _MAX_COLS:
+        out[f"max_{c}"] = float(np.max([float(r[c]) for r in rows])) if rows else 0.0
+    return out
+
+
+def generate_compare_report(tap: str, *, ideal_dir: Path, fixed_dir: Path, report_dir: Path, top_k: int = 5,
+                            strict: bool = False, verbose: bool = True) -> dict[str, Any]:
+    ideal_dir, fixed_dir, report_dir = Path(ideal_dir).resolve(), Path(fixed_dir).resolve(), Path(report_dir).resolve()
+    if not ideal_dir.exists():
+        raise FileNotFoundError(f"Ideal output directory not found: {ideal_dir}")
+    if not fixed_dir.exists():
+        raise FileNotFoundError(f"Fixed output directory not found: {fixed_dir}")
+    ideal_re, fixed_re = name_patterns(tap)
+    ideal_map, bad_ideal, dup_ideal = _collect(ideal_dir, ideal_re)
+    fixed_map, bad_fixed, dup_fixed = _collect(fixed_dir, fixed_re)
+    shared = sorted(set(ideal_map) & set(fixed_map))
+    if not shared:
+        raise ValueError(f"No matched {tap} ideal/fixed pairs found. ideal_dir={ideal_dir}, fixed_dir={fixed_dir}")
+
+    rows, mismatched = [], []
+    for key in shared:
+        ip, fp = ideal_map[key], fixed_map[key]
+        yi, yf = np.load(ip), np.load(fp)
+        name = f"{key[0]}__{key[1]}"
+        if yi.shape != yf.shape:
+            mismatched.append({"key": name, "ideal_shape": list(yi.shape), "fixed_shape": list(yf.shape),
+                               "ideal_file": ip.name, "fixed_file": fp.name})
+            continue
+        m = compute_metrics(yi, yf)
+        h, w = (int(yi.shape[0]), int(yi.shape[1])) if yi.ndim >= 2 else (1, int(yi.shape[0]))
+        rows.append({"key": name, "case_stem": key[0], "coeff_name": key[1], "height": h, "width": w, **m,
+                     "ideal_file": ip.name, "fixed_file": fp.name})
+    rows.sort(key=lambda r: (str(r["case_stem"]), str(r["coeff_name"])))
+
+    validation = {
+        "invalid_ideal_filenames": sorted(bad_ideal), "invalid_fixed_filenames": sorted(bad_fixed),
+        "duplicate_ideal_keys": dup_ideal, "duplicate_fixed_keys": dup_fixed,
+        "missing_ideal_keys": [f"{a}__{b}" for a, b in sorted(set(fixed_map) - set(ideal_map))],
+        "missing_fixed_keys": [f"{a}__{b}" for a, b in sorted(set(ideal_map) - set(fixed_map))],
+        "shape_mismatch_cases": mismatched,
+    }
+    has_issue = any(len(validation[k]) > 0 for k in _VALIDATION_KEYS)
+    if strict and has_issue:
+        raise ValueError(
+            "Validation failed in strict mode. "
+            f"missing_ideal={len(validation['missing_ideal_keys'])}, "
+            f"missing_fixed={len(validation['missing_fixed_keys'])}, "
+            f"shape_mismatch={len(validation['shape_mismatch_cases'])}, "
+            f"invalid_ideal_names={len(validation['invalid_ideal_filenames'])}, "
+            f"invalid_fixed_names={len(validation['invalid_fixed_filenames'])}, "
+            f"duplicate_ideal_keys={len(validation['duplicate_ideal_keys'])}, "
+            f"duplicate_fixed_keys={len(validation['duplicate_fixed_keys'])}")
+
+    overall = summarize_rows(rows)
+    groups: dict[str, list] = {}
+    for r in rows:
+        groups.setdefault(str(r["coeff_name"]), []).append(r)
+    by_coeff = {c: summarize_rows(rs) for c, rs in sorted(groups.items())}
+    worst = sorted(rows, key=lambda r: (-float(r["rmse"]), str(r["key"])))[:max(top_k, 0)]
+
+    report_dir.mkdir(parents=True, exist_ok=True)
+    csv_path = report_dir / f"compare_{tap}_cases.csv"
+    json_path = report_dir / f"compare_{tap}_summary.json"
+    with csv_path.open("w", encoding="utf-8", newline="") as f:
+        wr = csv.DictWriter(f, fieldnames=CSV_FIELDS)
+        wr.writeheader()
+        for r in rows:
+            wr.writerow({k: r.get(k, "") for k in CSV_FIELDS})
+    payload = {
+        "generated_at_utc": datetime.now(timezone.utc).isoformat(),
+        "config": {"ideal_dir": str(ideal_dir), "fixed_dir": str(fixed_dir), "report_dir": str(report_dir),
+                   "top_k": int(top_k), "strict": bool(strict),
+                   "comparison_note": "Metrics are computed on fixed(uint8 clipped) - ideal(float64 raw)."},
+        "validation": validation, "overall": overall, "by_coeff": by_coeff, "worst_cases_by_rmse": worst,
+        "cases": rows,
+    }
+    json_path.write_text(json.dumps(payload, indent=2, ensure_ascii=False) + "\n", encoding="utf-8")
+    if verbose:
+        print(f"[{tap} compare summary]")
+        for k in ("num_cases", "num_samples_total"):
+            print(f"- {k}: {overall[k]}")
+        for k in ("avg_mae", "avg_rmse", "max_max_abs_err", "avg_sat_ratio"):
+            print(f"- {k}: {overall[k]:.6f}")
+        print("[validation]")
+        for k in _VALIDATION_KEYS:
+            print(f"- {k}: {len(validation[k])}")
+        if worst:
+            print("[worst cases by rmse]")
+            for i, r in enumerate(worst, start=1):
+                print(f"{i}. key={r['key']}, rmse={r['rmse']:.6f}, mae={r['mae']:.6f}, "
+                      f"max_abs_err={r['max_abs_err']:.6f}")
+        print(f"[reports]\n- csv: {csv_path}\n- json: {json_path}")
+    return {"csv_path": str(csv_path), "json_path": str(json_path), "num_cases": overall["num_cases"],
+            "num_samples_total": overall["num_samples_total"], "validation_has_issue": has_issue}

@@ -67,14 +67,49 @@ def _generate_fixed_outputs_for_tap_map(*, input_dir: Path, out_dir: Path, coeff
     for in_path in inputs:
         x_u8 = _load_input_image_u8(in_path)
         stem = _case_stem_from_input(in_path)
+        pending = []
         for coeff_name, h in coeff_map.items():
             out_path = out_dir / f"{stem}__{coeff_name}_fixed_{tap_label}_y_u8.npy"
-            if out_path.exists() and not overwrite:
-                continue
-            np.save(out_path, _run_fixed_rowwise(x_u8, h, frac_bits=frac_bits, acc_bits=acc_bits,
-                                                 coeff_bits=coeff_bits))
-            generated += 1
+            if not out_path.exists() or overwrite:
+                pending.append((out_path, h))
+        generated += _run_bank(x_u8, pending, frac_bits=frac_bits, acc_bits=acc_bits, coeff_bits=coeff_bits)
     return generated
+
+
+def _run_bank(x_u8: np.ndarray, pending: list, *, frac_bits: int, acc_bits: int, coeff_bits: int) -> int:
+    """All pending filters of a bank over one image: one fused launch per group of equal tap
+    counts (the image is read once per 4 filters).  Taps are validated in bank order, and if
+    one fails the filters before it are still written before the error propagates, as the
+    reference's one-file-at-a-time loop (gen_fixed_output.py:92-105) would."""
+    if not pending:
+        return 0
+    height, width = x_u8.shape
+    taps, error = [], None
+    for out_path, h in pending:
+        try:
+            taps.append((out_path, quantize_fixed_taps(h, frac_bits, acc_bits, coeff_bits)))
+        except ValueError as exc:
+            error = exc
+            break
+    written, i = 0, 0
+    while i < len(taps):
+        j = i
+        while j < len(taps) and len(taps[j][1]) == len(taps[i][1]):
+            j += 1
+        group = taps[i:j]
+        if height == 0 or width == 0:
+            ys = np.zeros((len(group), height, width), dtype=np.uint8)
+        else:
+            f, a = device_bits(frac_bits, acc_bits)
+            ys = fir_hip.fir1d_fixed_rows_multi(np.ascontiguousarray(x_u8, dtype=np.uint8),
+                                                np.stack([t for _, t in group]), f, a, fir_hip.OUT_U8_SAT)
+        for (out_path, _), y in zip(group, ys):
+            np.save(out_path, y)
+            written += 1
+        i = j
+    if error is not None:
+        raise error
+    return written
 
 
 def generate_fixed_3tap_output_vector(input_dir: Path = DEFAULT_INPUT_DIR, output_dir: Path = DEFAULT_OUTPUT_DIR,

@@ -1,0 +1,108 @@
+"""Restore PNG images from ideal/fixed output vectors.
+
+Mirror of the reference stage ``fir_1d/sim/vector/restore_images.py`` (same arguments,
+file-name pattern, output sub-directories ``{kind}_{tap}tap[_{policy}]``, skip / strict
+behaviour and summary dict).  PNG encoding is host I/O (Pillow), outside the GPU path;
+the u8 conversions are the reference's: ``clip`` = rint + clip to [0,255] (:51-54),
+``normalize`` = min/max rescale (:57-64); fixed outputs are already uint8.
+"""
+from __future__ import annotations
+
+import re
+from datetime import datetime, timezone
+from pathlib import Path
+from typing import Any
+
+import numpy as np
+
+THIS_FILE = Path(__file__).resolve()
+DEFAULT_VECTOR_OUTPUT_DIR = THIS_FILE.parent / "output"
+DEFAULT_OUTPUT_IMG_DIR = THIS_FILE.parent.parent / "output_img"
+VALID_KINDS = ("ideal", "fixed")
+VALID_TAPS = ("3", "5")
+IDEAL_POLICIES = ("clip", "normalize")
+FILENAME_RE = re.compile(
+    r"^(?P<case_stem>.+?)__(?P<coeff_name>.+)_(?P<kind>ideal|fixed)_(?P<tap>[35])tap_y_(?P<dtype_tag>f64|u8)\.npy$")
+
+
+def _to_u8_clip(a: np.ndarray) -> np.ndarray:
+    return np.clip(np.rint(a), 0, 255).astype(np.uint8)
+
+
+def _to_u8_normalized(a: np.ndarray) -> np.ndarray:
+    a = a.astype(np.float64, copy=False)
+    lo, hi = float(a.min()), float(a.max())
+    if hi <= lo:
+        return np.zeros(a.shape, dtype=np.uint8)
+    return np.rint(np.clip((a - lo) * (255.0 / (hi - lo)), 0, 255)).astype(np.uint8)
+
+
+def _to_image_u8(a: np.ndarray, kind: str, ideal_policy: str) -> np.ndarray:
+    if a.ndim != 2:
+        raise ValueError(f"Expected 2D array for image restore, got shape={a.shape}")
+    if kind == "fixed":
+        return a if a.dtype == np.uint8 else _to_u8_clip(a.astype(np.float64, copy=False))
+    if kind != "ideal":
+        raise ValueError(f"Unsupported kind={kind}")
+    if ideal_policy == "clip":
+        return _to_u8_clip(a.astype(np.float64, copy=False))
+    if ideal_policy == "normalize":
+        return _to_u8_normalized(a)
+    raise ValueError(f"Unsupported ideal_policy={ideal_policy}")
+
+
+def _selected(value: str, valid: tuple[str, ...]) -> list[str]:
+    return list(valid) if value == "all" else [value]
+
+
+def restore_images(*, vector_output_dir: Path = DEFAULT_VECTOR_OUTPUT_DIR, output_img_dir: Path = DEFAULT_OUTPUT_IMG_DIR,
+                   kind: str = "all", tap: str = "all", ideal_policy: str = "clip", overwrite: bool = False,
+                   strict: bool = False) -> dict[str, Any]:
+    vector_output_dir, output_img_dir = Path(vector_output_dir).resolve(), Path(output_img_dir).resolve()
+    if not vector_output_dir.exists():
+        raise FileNotFoundError(f"Vector output directory not found: {vector_output_dir}")
+    kinds, taps = _selected(kind, VALID_KINDS), _selected(tap, VALID_TAPS)
+    try:
+        from PIL import Image
+    except ModuleNotFoundError as exc:
+        raise RuntimeError("Pillow is required to write PNG images.") from exc
+    converted, skipped = [], []
+    for k in kinds:
+        for t in taps:
+            src = vector_output_dir / f"{k}_{t}tap"
+            if not src.exists():
+                skipped.append({"reason": "missing_input_subdir", "kind": k, "tap": f"{t}tap", "path": str(src)})
+                if strict:
+                    raise FileNotFoundError(f"Expected input subdir not found: {src}")
+                continue
+            dst = output_img_dir / (f"{k}_{t}tap_{ideal_policy}" if k == "ideal" and ideal_policy != "clip"
+                                    else f"{k}_{t}tap")
+            dst.mkdir(parents=True, exist_ok=True)
+            for p in sorted((q for q in src.glob("*.npy") if q.is_file()), key=lambda q: q.name.lower()):
+                m = FILENAME_RE.match(p.name)
+                if m is None:
+                    skipped.append({"reason": "invalid_filename", "path": str(p)})
+                    if strict:
+                        raise ValueError(f"Invalid vector filename: {p.name}")
+                    continue
+                if m.group("kind") != k or m.group("tap") != t:
+                    skipped.append({"reason": "kind_tap_mismatch", "path": str(p), "expected_kind": k,
+                                    "expected_tap": t, "file_kind": m.group("kind"), "file_tap": m.group("tap")})
+                    if strict:
+                        raise ValueError(f"Kind/tap mismatch in filename={p.name}, expected {k}_{t}tap")
+                    continue
+                out = dst / f"{p.stem}.png"
+                if out.exists() and not overwrite:
+                    skipped.append({"reason": "exists", "path": str(out)})
+                    continue
+                img = _to_image_u8(np.load(p), k, ideal_policy)
+                Image.fromarray(img, mode="L").save(out)
+                converted.append({"input_npy": str(p), "output_img": str(out), "kind": k, "tap": f"{t}tap",
+                                  "ideal_policy": ideal_policy if k == "ideal" else "n/a",
+                                  "height": int(img.shape[0]), "width": int(img.shape[1]), "dtype": str(img.dtype),
+                                  "pixel_min": int(img.min()), "pixel_max": int(img.max())})
+    return {"generated_at_utc": datetime.now(timezone.utc).isoformat(),
+            "config": {"vector_output_dir": str(vector_output_dir), "output_img_dir": str(output_img_dir),
+                       "kind": kind, "tap": tap, "ideal_policy": ideal_policy, "overwrite": bool(overwrite),
+                       "strict": bool(strict)},
+            "num_converted": len(converted), "num_skipped": len(skipped), "converted": converted, "skipped": skipped}

@@ -20,8 +20,8 @@ from pathlib import Path
 import numpy as np
 
 __all__ = [
-    "FirHipError", "lib", "lib_path", "device_count", "fir1d_fixed_rows", "fir2d_fixed",
-    "fir1d_ideal_rows", "IN_U8", "IN_I16", "OUT_U8_SAT", "OUT_I32", "MAX_TAPS", "EXPORTS",
+    "FirHipError", "lib", "lib_path", "device_count", "fir1d_fixed_rows", "fir1d_fixed_rows_multi", "fir2d_fixed",
+    "fir1d_ideal_rows", "compare_metrics", "IN_U8", "IN_I16", "OUT_U8_SAT", "OUT_I32", "MAX_TAPS", "EXPORTS",
 ]
 
 IN_U8, IN_I16 = 0, 1
@@ -49,11 +49,16 @@ EXPORTS = {
     "fir_device_count": (_i32, [ctypes.POINTER(_i32)]),
     "fir1d_fixed_rows": (_i32, [_vp, _i32, _i64, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _i32]),
     "fir1d_fixed_rows_dev": (_i32, [_vp, _i32, _i64, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp]),
+    "fir1d_fixed_rows_multi": (_i32, [_vp, _i32, _i64, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32]),
+    "fir1d_fixed_rows_multi_dev": (_i32, [_vp, _i32, _i64, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
     "fir1d_fixed_edges_dev": (_i32, [_vp, _i32, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "fir2d_fixed": (_i32, [_vp, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32]),
     "fir2d_fixed_dev": (_i32, [_vp, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
     "fir1d_ideal_rows": (_i32, [_vp, _i64, _i64, _vp, _i32, _vp, _i32]),
     "fir1d_ideal_rows_dev": (_i32, [_vp, _i64, _i64, _vp, _i32, _vp, _vp]),
+    "fir_metrics_work_bytes": (_i64, []),
+    "fir_compare_metrics": (_i32, [_vp, _vp, _i64, _vp, _i32]),
+    "fir_compare_metrics_dev": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp]),
 }
 
 _lib = None
@@ -140,6 +145,37 @@ def fir1d_fixed_rows(x: np.ndarray, hq, frac_bits: int = 12, acc_bits: int = 32,
     return y
 
 
+def fir1d_fixed_rows_multi(x: np.ndarray, hq2, frac_bits: int = 12, acc_bits: int = 32,
+                           out_stage: int = OUT_U8_SAT, channels: int = 1, device: int = 0) -> np.ndarray:
+    """F filters (rows of the F x L array hq2) over the same x in one call; returns an
+    array of shape (F, *x.shape).  u8 input is read once per 4 filters on the GPU."""
+    x = np.ascontiguousarray(x)
+    if x.dtype == np.uint8:
+        in_dtype = IN_U8
+    elif x.dtype == np.int16:
+        in_dtype = IN_I16
+    else:
+        raise FirHipError(f"x dtype must be uint8 or int16, got {x.dtype}")
+    h2 = np.asarray(hq2, dtype=np.int64)
+    if h2.ndim != 2 or h2.shape[0] < 1:
+        raise FirHipError("hq2 must be a non-empty (filters, taps) array")
+    nf, L = h2.shape
+    h = _taps_i32(h2.reshape(-1)) if nf * L <= MAX_TAPS else np.ascontiguousarray(h2, dtype=np.int32).reshape(-1)
+    if L > MAX_TAPS:
+        raise FirHipError(f"{L} taps exceed the library limit of {MAX_TAPS}")
+    if x.ndim == 0:
+        x = x.reshape(1)
+    rowlen = x.shape[-1]
+    rows = x.size // rowlen if rowlen else 0
+    if rowlen % channels:
+        raise FirHipError("row length must be a multiple of channels")
+    y = np.empty((nf,) + x.shape, dtype=np.uint8 if out_stage == OUT_U8_SAT else np.int32)
+    _check(lib().fir1d_fixed_rows_multi(_ptr(x), in_dtype, rows, rowlen // channels, channels, _ptr(h), L, nf,
+                                        int(frac_bits), int(acc_bits), int(out_stage), _ptr(y), int(device)),
+           "fir1d_fixed_rows_multi")
+    return y
+
+
 def fir2d_fixed(x: np.ndarray, hq2, frac_bits: int = 12, acc_bits: int = 32, out_stage: int = OUT_U8_SAT,
                 device: int = 0) -> np.ndarray:
     """2-D same-mode fixed FIR of a uint8 frame with a (R, C) quantized kernel."""
@@ -171,3 +207,25 @@ def fir1d_ideal_rows(x_u8: np.ndarray, h, device: int = 0) -> np.ndarray:
     _check(lib().fir1d_ideal_rows(_ptr(x), rows, width, _ptr(hh), hh.size, _ptr(y), int(device)),
            "fir1d_ideal_rows")
     return y
+
+
+def metrics_from_sums(s, n: int) -> dict:
+    """The report's metric dict (gen_3tap_compare_report.py:102-112) from the 9 sums."""
+    if n == 0:
+        return {"num_samples": 0, "max_abs_err": 0.0, "mae": 0.0, "rmse": 0.0, "mean_err": 0.0,
+                "sat_low_ratio": 0.0, "sat_high_ratio": 0.0, "sat_ratio": 0.0, "clip_needed_ratio": 0.0}
+    lo, hi = float(s[4]) / n, float(s[5]) / n
+    return {"num_samples": int(n), "max_abs_err": float(s[0]), "mae": float(s[1]) / n,
+            "rmse": float(np.sqrt(float(s[2]) / n)), "mean_err": float(s[3]) / n, "sat_low_ratio": lo,
+            "sat_high_ratio": hi, "sat_ratio": lo + hi, "clip_needed_ratio": float(s[6]) / n}
+
+
+def compare_metrics(y_ideal: np.ndarray, y_fixed: np.ndarray, device: int = 0) -> dict:
+    """_compute_metrics (gen_3tap_compare_report.py:67-112) in one GPU pass."""
+    if y_ideal.shape != y_fixed.shape:
+        raise ValueError(f"Shape mismatch: ideal={y_ideal.shape}, fixed={y_fixed.shape}")
+    yi = np.ascontiguousarray(y_ideal, dtype=np.float64).reshape(-1)
+    yf = np.ascontiguousarray(y_fixed, dtype=np.uint8).reshape(-1)
+    out = np.zeros(9, dtype=np.float64)
+    _check(lib().fir_compare_metrics(_ptr(yi), _ptr(yf), yi.size, _ptr(out), int(device)), "fir_compare_metrics")
+    return metrics_from_sums(out, yi.size)

@@ -67,6 +67,30 @@ def fir1d_fixed_rows_dev(x: torch.Tensor, hq, frac_bits: int = 12, acc_bits: int
     return out
 
 
+def fir1d_fixed_rows_multi_dev(x: torch.Tensor, hq2, frac_bits: int = 12, acc_bits: int = 32,
+                               out_stage: int = OUT_U8_SAT, channels: int = 1, out: torch.Tensor | None = None,
+                               stream=None) -> torch.Tensor:
+    """F filters (rows of hq2) over the same device tensor; returns (F, *x.shape)."""
+    _check_dev(x, "x")
+    if x.dtype not in _IN:
+        raise FirHipError(f"x dtype must be uint8 or int16, got {x.dtype}")
+    h2 = np.asarray(hq2, dtype=np.int64)
+    if h2.ndim != 2:
+        raise FirHipError("hq2 must be a (filters, taps) array")
+    nf, L = h2.shape
+    h = np.ascontiguousarray(h2, dtype=np.int32).reshape(-1)
+    if out is None:
+        out = torch.empty((nf,) + tuple(x.shape), dtype=_OUT_DTYPE[out_stage], device=x.device)
+    _check_dev(out, "out")
+    rowlen = x.shape[-1] if x.dim() else 1
+    rows = x.numel() // rowlen if rowlen else 0
+    _check(lib().fir1d_fixed_rows_multi_dev(ctypes.c_void_p(x.data_ptr()), _IN[x.dtype], rows, rowlen // channels,
+                                            channels, h.ctypes.data_as(ctypes.c_void_p), L, nf, int(frac_bits),
+                                            int(acc_bits), int(out_stage), ctypes.c_void_p(out.data_ptr()),
+                                            _stream_ptr(x, stream)), "fir1d_fixed_rows_multi_dev")
+    return out
+
+
 def fir1d_fixed_edges_dev(x: torch.Tensor, hq, out: torch.Tensor, halo_left: torch.Tensor | None,
                           halo_right: torch.Tensor | None, frac_bits: int = 12, acc_bits: int = 32,
                           out_stage: int = OUT_I32, channels: int = 1, stream=None) -> torch.Tensor:
