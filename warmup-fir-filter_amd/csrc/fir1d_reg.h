@@ -128,13 +128,6 @@ __device__ __forceinline__ void store_vec(typename OutTraits<STAGE>::T* __restri
     }
 }
 
-// (wrap(acc) + 2^(f-1)) >> f, with the wrap skipped when acc_bits == 32 (ACC32).
-template <bool ACC32>
-__device__ __forceinline__ int32_t round_acc(uint32_t acc, int shl, int frac) {
-    const int32_t a = ACC32 ? (int32_t)acc : (int32_t)(acc << shl) >> shl;
-    return (a >> frac) + ((a >> (frac - 1)) & 1);
-}
-
 // Sample pair (s, s+1) of the window as two int16 halves; window dword i holds samples
 // 2i - 2*NDL and 2i - 2*NDL + 1.  LAST_ZERO: the caller multiplies the high half by 0, so it
 // may come from outside the window.

@@ -21,7 +21,17 @@ struct Taps2 {
     int32_t h[R][C];
     // DOT2 form: pair p of row m = (h[m][C-1-2p], h[m][C-2-2p]) as two int16 (0 past the row)
     uint32_t p2[R][(C + 1) / 2];
+    // SEP form (h[m][n] == col[m] * row[n] exactly): packed row taps, column taps
+    uint32_t rowp[(C + 1) / 2];
+    int32_t col[R];
 };
+
+// 2-D kernel arithmetic: general 5x5 on v_mad_i32_i24 / packed v_dot2, or rank-1 separable
+// (a horizontal dot2 pass per input row, then R column MACs on the row sums).
+// MODE = arithmetic (low 2 bits) | kMode2dNoWrap: the host proved |acc| + 2^(f-1) can never
+// reach the wrap limit, so every accumulator starts at the rounding bias 2^(f-1) and the
+// epilogue is one arithmetic shift (exactly fir_1d_fixed_ref.py:110-120 when no wrap occurs).
+enum Fir2dMode : int { kMode2dMad = 0, kMode2dDot2 = 1, kMode2dSep = 2, kMode2dNoWrap = 4 };
 
 template <int R, int C>
 inline void pack_taps2(Taps2<R, C>& t) {
@@ -39,6 +49,28 @@ typedef short fir_short2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t dot2_acc(uint32_t a, uint32_t b, uint32_t c) {
     return (uint32_t)__builtin_amdgcn_sdot2(__builtin_bit_cast(fir_short2, a), __builtin_bit_cast(fir_short2, b),
                                             (int)c, false);
+}
+
+// First MAC of a chain without a zero-initialised destination: VOP3P v_dot2_i32_i16 with an
+// inline-constant or VGPR addend (hipcc otherwise emits v_dot2c plus a v_mov of the addend).
+// Pure VALU, no memory, no hazards: safe as inline asm.
+__device__ __forceinline__ uint32_t dot2_from0(uint32_t pair, uint32_t taps) {
+    uint32_t d;
+    asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(d) : "v"(pair), "s"(taps));
+    return d;
+}
+__device__ __forceinline__ uint32_t dot2_from(uint32_t pair, uint32_t taps, uint32_t c) {
+    uint32_t d;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(pair), "s"(taps), "v"(c));
+    return d;
+}
+
+// v_mad_i32_i24 d = a[23:0] * b[23:0] + c (|a|, |b| < 2^23 host-checked); as asm because hipcc
+// sign-extends a value it cannot range-check (v_bfe_i32) before every __mul24.
+__device__ __forceinline__ uint32_t mad_i24(uint32_t a, int32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "s"(b), "v"(c));
+    return d;
 }
 
 // bytes k and k+1 of a little-endian byte stream held in dwords s[], zero-extended into the
@@ -69,6 +101,21 @@ struct PairBuilder {
 // Branch-free row load: the address is always in bounds (the caller clamps it) and the
 // value is zeroed by a select when the row/column is outside the frame, so the compiler can
 // count outstanding loads exactly (a load inside a branch makes it wait for all of them).
+// One saturated u8 output.  NOWRAP (bias already in acc): clamp to [0, 256*2^f - 1] first,
+// then shift -- the same value as sat(acc >> f), in an order hipcc (ROCm 7.2) does not fuse
+// into v_ashr_pk_u8_i32: that fusion left bits set above the packed byte pair, which the
+// following v_lshl_or merged into the next pixel (measured: wrong byte 2 of every dword).
+template <bool NOWRAP>
+__device__ __forceinline__ uint32_t sat_u8_pixel(uint32_t acc, int shl, int frac, int32_t sat_hi) {
+    if constexpr (NOWRAP) {
+        uint32_t c;  // v_med3_i32(acc, 0, hi) == clamp(acc, 0, hi) since hi > 0 (hipcc emits max + min)
+        asm("v_med3_i32 %0, %1, 0, %2" : "=v"(c) : "v"(acc), "s"(sat_hi));
+        return c >> frac;
+    } else {
+        return (uint32_t)min(max(round32(acc, shl, frac), 0), 255);
+    }
+}
+
 template <int ND>
 __device__ __forceinline__ void load_row_px(const uint8_t* __restrict__ p, bool ok, uint32_t (&d)[ND]) {
     typedef uint32_t vN __attribute__((ext_vector_type(ND)));
@@ -77,7 +124,7 @@ __device__ __forceinline__ void load_row_px(const uint8_t* __restrict__ p, bool 
     for (int i = 0; i < ND; ++i) d[i] = ok ? q[i] : 0u;
 }
 
-template <int R, int C, int STAGE, int VEC, int STRIP, bool DOT2>
+template <int R, int C, int STAGE, int VEC, int STRIP, int MODE>
 __global__ __launch_bounds__(kBlock) void fir2d_reg_kernel(const uint8_t* __restrict__ x,
                                                            typename OutTraits<STAGE>::T* __restrict__ y, int64_t H,
                                                            int64_t W, Taps2<R, C> taps, int shl, int frac) {
@@ -103,11 +150,16 @@ __global__ __launch_bounds__(kBlock) void fir2d_reg_kernel(const uint8_t* __rest
     const int64_t hcol = hin ? hraw : colc;
     const bool hok = hlane && hin;
 
+    constexpr bool NOWRAP = (MODE & kMode2dNoWrap) != 0;
+    const int32_t sat_hi = (256 << frac) - 1;  // NOWRAP u8: clamp before the shift (frac <= 22)
+    const uint32_t acc0 = NOWRAP ? (1u << (frac - 1)) : 0u;  // rounding bias folded into the init
+    uint32_t acc0v;  // the same in a VGPR, for dot2_from
+    asm("v_mov_b32 %0, %1" : "=v"(acc0v) : "s"(acc0));
     uint32_t acc[R][VEC];
 #pragma unroll
     for (int s = 0; s < R; ++s)
 #pragma unroll
-        for (int j = 0; j < VEC; ++j) acc[s][j] = 0;
+        for (int j = 0; j < VEC; ++j) acc[s][j] = acc0;
 
     auto row_ptr = [&](int64_t row) { return x + (row < 0 ? 0 : (row >= H ? H - 1 : row)) * W; };
     uint32_t cur[ND], hcur;
@@ -133,7 +185,7 @@ __global__ __launch_bounds__(kBlock) void fir2d_reg_kernel(const uint8_t* __rest
                 const uint32_t hv = *reinterpret_cast<const uint32_t*>(rp + hcol);
                 hnxt = (hok && rok) ? hv : 0u;
             }
-            if constexpr (DOT2) {
+            if constexpr ((MODE & 3) != kMode2dMad) {
                 // byte stream: [left-halo dword | own dwords | right-halo dword]; window pixel i
                 // is stream byte i + (4 - HLE).  P[k] = (w[k], w[k+1]) as int16 halves.
                 uint32_t sb[ND + 2];
@@ -145,15 +197,31 @@ __global__ __launch_bounds__(kBlock) void fir2d_reg_kernel(const uint8_t* __rest
                 uint32_t Pr[NP + 4 - HLE];
                 PairBuilder<4 - HLE, NP>::run(sb, Pr);
                 const uint32_t* P = Pr + (4 - HLE);
+                if constexpr ((MODE & 3) == kMode2dDot2) {
 #pragma unroll
-                for (int m = 0; m < R; ++m) {
-                    const int slot = (s + 1 + m) % R;
+                    for (int m = 0; m < R; ++m) {
+                        const int slot = (s + 1 + m) % R;
+#pragma unroll
+                        for (int j = 0; j < VEC; ++j) {
+                            // m = R-1 opens the row: its first MAC starts from the bias (acc0)
+                            uint32_t a = m == R - 1 ? dot2_from(P[j], taps.p2[m][0], acc0v)
+                                                    : dot2_acc(P[j], taps.p2[m][0], acc[slot][j]);
+#pragma unroll
+                            for (int p = 1; p < (C + 1) / 2; ++p) a = dot2_acc(P[j + 2 * p], taps.p2[m][p], a);
+                            acc[slot][j] = a;
+                        }
+                    }
+                } else {  // separable: exact row sums (|r| < 2^23, host-checked), then the column taps
 #pragma unroll
                     for (int j = 0; j < VEC; ++j) {
-                        uint32_t a = acc[slot][j];
+                        uint32_t r = dot2_from0(P[j], taps.rowp[0]);
 #pragma unroll
-                        for (int p = 0; p < (C + 1) / 2; ++p) a = dot2_acc(P[j + 2 * p], taps.p2[m][p], a);
-                        acc[slot][j] = a;
+                        for (int p = 1; p < (C + 1) / 2; ++p) r = dot2_acc(P[j + 2 * p], taps.rowp[p], r);
+#pragma unroll
+                        for (int m = 0; m < R; ++m) {
+                            const int slot = (s + 1 + m) % R;
+                            acc[slot][j] = mad_i24(r, taps.col[m], m == R - 1 ? acc0v : acc[slot][j]);
+                        }
                     }
                 }
             } else {
@@ -176,7 +244,7 @@ __global__ __launch_bounds__(kBlock) void fir2d_reg_kernel(const uint8_t* __rest
                 const int slot = (s + 1 + m) % R;
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) {
-                    uint32_t a = acc[slot][j];
+                    uint32_t a = m == R - 1 ? acc0 : acc[slot][j];
 #pragma unroll
                     for (int n = 0; n < C; ++n) a += (uint32_t)__mul24(taps.h[m][n], w[HLE + j + CC - n]);
                     acc[slot][j] = a;
@@ -197,7 +265,7 @@ __global__ __launch_bounds__(kBlock) void fir2d_reg_kernel(const uint8_t* __rest
                             uint32_t o4 = 0;
 #pragma unroll
                             for (int b = 0; b < 4; ++b)
-                                o4 |= (uint32_t)stage_out32<STAGE>(round32(acc[slot][4 * i + b], shl, frac)) << (8 * b);
+                                o4 |= sat_u8_pixel<NOWRAP>(acc[slot][4 * i + b], shl, frac, sat_hi) << (8 * b);
                             val[i] = o4;
                         }
                         *reinterpret_cast<vN*>(dst) = val;
@@ -207,13 +275,11 @@ __global__ __launch_bounds__(kBlock) void fir2d_reg_kernel(const uint8_t* __rest
                         for (int i = 0; i < VEC / 4; ++i) {
                             v4 val;
 #pragma unroll
-                            for (int b = 0; b < 4; ++b) val[b] = (uint32_t)round32(acc[slot][4 * i + b], shl, frac);
+                            for (int b = 0; b < 4; ++b) val[b] = (uint32_t)(NOWRAP ? (int32_t)acc[slot][4 * i + b] >> frac : round32(acc[slot][4 * i + b], shl, frac));
                             reinterpret_cast<v4*>(dst)[i] = val;
                         }
                     }
                 }
-#pragma unroll
-                for (int j = 0; j < VEC; ++j) acc[slot][j] = 0;
             }
 #pragma unroll
             for (int i = 0; i < ND; ++i) cur[i] = nxt[i];

@@ -57,6 +57,13 @@ __device__ __forceinline__ int32_t round32(uint32_t acc, int shl, int frac) {
     return (a >> frac) + ((a >> (frac - 1)) & 1);
 }
 
+// (wrap(acc) + 2^(f-1)) >> f, with the wrap skipped when acc_bits == 32 (ACC32).
+template <bool ACC32>
+__device__ __forceinline__ int32_t round_acc(uint32_t acc, int shl, int frac) {
+    const int32_t a = ACC32 ? (int32_t)acc : (int32_t)(acc << shl) >> shl;
+    return (a >> frac) + ((a >> (frac - 1)) & 1);
+}
+
 // 64-bit generic form (any acc_bits >= 1, any frac_bits >= 1); |acc| < 2^52.
 __device__ __forceinline__ int64_t round64(int64_t acc, int frac, int acc_bits) {
     if (acc_bits < 64) {
