@@ -14,7 +14,12 @@ prints ONE JSON line.  Extra keys:
                 launch from the committed rocprofv3 summary in profiles/ (null if absent)
   cpu_baseline  the C oracle (oracle/fir_oracle.c, OpenMP) on this host's cores, same input
   parity        every rank's full output compared bit-exactly with the C oracle
-Other workloads (`--workload cplx_i16 | fir2d_u8`) measure configs[2] / configs[4].
+  cpu_baseline_numpy  the vectorised NumPy restatement (oracle/fir_oracle.py, one core) on a
+                bounded leading slice of the same input (BASELINE.md's "NumPy CPU path")
+Other workloads: `cplx_i16` / `fir2d_u8` measure configs[2] / configs[4]; `fir1d_u8` the
+reference's own u8 -> sat-u8 golden path (a1/a4) at scale; `ideal_u8` (the f64
+ideal model) and `bank_u8` (the fused 4-filter 3-tap bank, §8(f) 3) measure
+the next rows on 2^28 u8 samples in 4096-sample rows (the reference's image-row layout).
 """
 from __future__ import annotations
 
@@ -43,6 +48,11 @@ SEED = 20260227
 SHARPEN5 = [-256, -1024, 6656, -1024, -256]  # h_coeff_5tap_map["sharpen"] in Q4.12
 SIMPLE_LP3 = [1024, 2048, 1024]              # h_coeff_3tap_map["simple_lp"] in Q4.12
 SIMPLE_LP5 = [256, 1024, 1536, 1024, 256]    # h_coeff_5tap_map["simple_lp"] in Q4.12
+SHARPEN5_F64 = [-1 / 16, -4 / 16, 26 / 16, -4 / 16, -1 / 16]  # h_coeff_5tap_map["sharpen"]
+BANK3 = [[1365] * 3, [1024, 2048, 1024], [-4096, 0, 4096], [-512, 5120, -512]]  # h_coeff_3tap_map, Q4.12
+ROW_W = 4096
+KERNELS = {"fir1d_i16": "fir1d_reg_kernel", "cplx_i16": "fir1d_reg_kernel", "fir2d_u8": "fir2d_reg_kernel",
+           "fir1d_u8": "fir1d_reg_kernel", "ideal_u8": "fir1d_ideal_kernel", "bank_u8": "fir1d_reg_kernel"}
 
 
 def _env_int(name: str, default: int) -> int:
@@ -96,22 +106,59 @@ class Workload:
             self.dtype = "int32 (u8 in, int32 wrap-around acc, u8 saturated out)"
             self.config = {"workload": "fir2d_u8_5x5_simple_lp_outer_q4.12", "frame": [self.h, self.w],
                            "parallelism": "single GPU (replicas when N > 1)"}
+        elif name in ("ideal_u8", "bank_u8", "fir1d_u8"):
+            self.n = 1 << log2n
+            self.x_host = rng.integers(0, 256, (self.n // ROW_W, ROW_W), dtype=np.uint8)
+            self.units = self.n
+            self.unit = "Gsamples/s"
+            par = "single GPU (replicas when N > 1)"
+            if name == "fir1d_u8":
+                self.taps = torch_ops.Taps(SHARPEN5)
+                self.bytes_per_unit = 1 + 1
+                self.dtype = "int32 (u8 in, int32 wrap-around acc, u8 saturated out)"
+                self.config = {"workload": "fir1d_u8_5tap_sharpen_q4.12_rows4096", "samples_per_gpu": self.n,
+                               "row_width": ROW_W, "taps": 5, "parallelism": par}
+            elif name == "ideal_u8":
+                self.bytes_per_unit = 1 + 8
+                self.dtype = "f64 (u8 in, f64 taps, per-op rounded k-order sums, f64 out)"
+                self.config = {"workload": "fir1d_ideal_f64_5tap_sharpen_rows4096", "samples_per_gpu": self.n,
+                               "row_width": ROW_W, "taps": 5, "parallelism": par}
+            else:
+                self.bytes_per_unit = 1 + len(BANK3)
+                self.dtype = "int32 (u8 in, int32 wrap-around acc, u8 saturated out x 4 filters)"
+                self.config = {"workload": "fir1d_u8_bank4_3tap_q4.12_rows4096", "samples_per_gpu": self.n,
+                               "row_width": ROW_W, "filters": len(BANK3), "taps": 3, "parallelism": par}
         else:
             raise SystemExit(f"unknown workload {name}")
         self.x = torch.from_numpy(self.x_host).to(dev)
-        out_dtype = torch.uint8 if name == "fir2d_u8" else torch.int32
-        self.y = torch.empty(self.x.shape, dtype=out_dtype, device=dev)
+        if name == "ideal_u8":
+            self.y = torch.empty(self.x.shape, dtype=torch.float64, device=dev)
+        elif name == "bank_u8":
+            self.y = torch.empty((len(BANK3),) + tuple(self.x.shape), dtype=torch.uint8, device=dev)
+        else:
+            u8 = name in ("fir2d_u8", "fir1d_u8")
+            self.y = torch.empty(self.x.shape, dtype=torch.uint8 if u8 else torch.int32, device=dev)
         self.left = self.right = None
+
+    @property
+    def sharded_1d(self) -> bool:
+        return self.world > 1 and self.name in ("fir1d_i16", "cplx_i16")
 
     def bulk(self):
         if self.name == "fir2d_u8":
             torch_ops.fir2d_fixed_dev(self.x, self.hq2, 12, 32, fir_hip.OUT_U8_SAT, out=self.y)
+        elif self.name == "ideal_u8":
+            torch_ops.fir1d_ideal_rows_dev(self.x, SHARPEN5_F64, out=self.y)
+        elif self.name == "bank_u8":
+            torch_ops.fir1d_fixed_rows_multi_dev(self.x, BANK3, 12, 32, fir_hip.OUT_U8_SAT, out=self.y)
+        elif self.name == "fir1d_u8":
+            torch_ops.fir1d_fixed_rows_dev(self.x, self.taps, 12, 32, fir_hip.OUT_U8_SAT, out=self.y)
         else:
             torch_ops.fir1d_fixed_rows_dev(self.x, self.taps, 12, 32, fir_hip.OUT_I32, self.channels, out=self.y)
 
     def step(self):
         """One pass of the hot path (for N > 1: halo exchange || bulk kernel, then edges)."""
-        sharded_1d = self.world > 1 and self.name != "fir2d_u8"
+        sharded_1d = self.sharded_1d
         works = []
         if sharded_1d:
             self.left, self.right, works = sharded.post_halo_exchange(self.x, self.taps.n, self.channels)
@@ -129,6 +176,13 @@ class Workload:
         for _ in range(reps):
             if self.name == "fir2d_u8":
                 out = co.fir2d(self.x_host, self.hq2, 12, 32, co.OUT_U8_SAT, nthreads=nthreads)
+            elif self.name == "ideal_u8":
+                out = co.fir1d_ideal_rows(self.x_host, SHARPEN5_F64, nthreads=nthreads)
+            elif self.name == "bank_u8":
+                out = np.stack([co.fir1d_rows(self.x_host, h, 12, 32, co.OUT_U8_SAT, nthreads=nthreads)
+                                for h in BANK3])
+            elif self.name == "fir1d_u8":
+                out = co.fir1d_rows(self.x_host, self.taps.h, 12, 32, co.OUT_U8_SAT, nthreads=nthreads)
             else:
                 hl = None if self.left is None else self.left.cpu().numpy()
                 hr = None if self.right is None else self.right.cpu().numpy()
@@ -136,13 +190,35 @@ class Workload:
                                     halo_left=hl, halo_right=hr, nthreads=nthreads)
         return out
 
+    def numpy_oracle(self, max_units: int):
+        """The NumPy restatement on the leading ``max_units`` units; returns the units done."""
+        from oracle import fir_oracle as fo
+
+        if self.name == "fir2d_u8":
+            rows = max(1, min(self.h, max_units // self.w))
+            fo.fir2d_fixed(self.x_host[:rows], self.hq2, 12, 32, fo.OUT_U8_SAT)
+            return rows * self.w
+        if self.name in ("ideal_u8", "bank_u8", "fir1d_u8"):
+            rows = max(1, min(self.x_host.shape[0], max_units // ROW_W))
+            if self.name == "fir1d_u8":
+                fo.fir1d_rows(self.x_host[:rows], self.taps.h, 12, 32, fo.OUT_U8_SAT)
+            elif self.name == "ideal_u8":
+                fo.fir1d_ideal_rows(self.x_host[:rows], SHARPEN5_F64)
+            else:
+                for h in BANK3:
+                    fo.fir1d_rows(self.x_host[:rows], h, 12, 32, fo.OUT_U8_SAT)
+            return rows * ROW_W
+        n = min(self.units, max_units)
+        fo.fir1d_i16_i32(self.x_host[:n * self.channels], self.taps.h, 12, 32, channels=self.channels)
+        return n
+
 
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=100, help="untimed steps (clocks take ~40 launches to ramp)")
-    ap.add_argument("--workload", default="fir1d_i16", choices=("fir1d_i16", "cplx_i16", "fir2d_u8"))
+    ap.add_argument("--workload", default="fir1d_i16", choices=tuple(KERNELS))
     ap.add_argument("--log2n", type=int, default=28, help="int16 values per GPU (2^28 = BASELINE configs[1])")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0 = skip)")
     ap.add_argument("--no-parity", action="store_true", help="skip the full-size oracle comparison")
@@ -218,7 +294,7 @@ def main() -> int:
             ok = int(f.item()) == 0
         parity = "bit-exact vs C oracle (full output, every rank)" if ok else "MISMATCH"
 
-    cpu = None
+    cpu = cpu_np = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         nthr = _cpu_threads()
         wl.oracle(nthr)  # warm (page-in, thread pool)
@@ -232,6 +308,12 @@ def main() -> int:
         cpu = {"value": round(wl.units * reps / tc / 1e9, 4), "unit": wl.unit, "cores": nthr, "kind": "port",
                "sample": f"C oracle (oracle/fir_oracle.c, OpenMP {nthr} threads) on the full per-GPU workload "
                          f"({wl.units} units) x {reps} repetitions, {tc:.1f} s"}
+        tn0 = time.perf_counter()
+        done = wl.numpy_oracle(1 << 24)
+        tn = time.perf_counter() - tn0
+        cpu_np = {"value": round(done / tn / 1e9, 5), "unit": wl.unit, "cores": 1, "kind": "port",
+                  "sample": f"NumPy restatement (oracle/fir_oracle.py, int64 accumulation) on the first {done} "
+                            f"units of the same input, {tn:.1f} s"}
 
     traffic = None
     pmc = ROOT / "profiles" / f"pmc_{args.workload}.json"
@@ -263,10 +345,11 @@ def main() -> int:
         "config": wl.config,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "fir1d_reg_kernel" if args.workload != "fir2d_u8" else "fir2d_reg_kernel",
+                     "kernel": KERNELS[args.workload],
                      "kernel_avg_us": round(kern_avg_s * 1e6, 2), "algorithmic_bytes_per_launch": alg_bytes,
                      "timing": f"HIP events around {args.steps} back-to-back launches of the kernel"},
         "cpu_baseline": cpu,
+        "cpu_baseline_numpy": cpu_np,
         "parity": parity,
     }
     if rank == 0:

@@ -42,6 +42,17 @@ for s in $STEPS; do
                  run "pmc_$c" 300 rocprofv3 --pmc "$c" --kernel-trace -d "$OUT/pmc_$c" -o run --output-format csv -- \
                      python bench.py --steps 10 --warmup 2 --cpu-seconds 0 --no-parity; fatal $? || exit
              done ;;
+        bench_*) wl=${s#bench_}
+             run "bench_$wl" 300 python bench.py --workload "$wl" --cpu-seconds 5; fatal $? ;;
+        prof_*) wl=${s#prof_}
+             run "prof_$wl" 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$wl" -o run --output-format csv -- \
+                 python bench.py --workload "$wl" --steps 200 --warmup 100 --cpu-seconds 0 --no-parity; fatal $? ;;
+        pmc_*) wl=${s#pmc_}
+             for c in FETCH_SIZE WRITE_SIZE; do
+                 run "pmc_${wl}_$c" 300 rocprofv3 --pmc "$c" --kernel-trace -d "$OUT/pmc_${wl}_$c" -o run \
+                     --output-format csv -- python bench.py --workload "$wl" --steps 10 --warmup 2 --cpu-seconds 0 \
+                     --no-parity; fatal $? || exit
+             done ;;
         micro) run micro 300 tools/microbench/fir_micro 28 20; fatal $? ;;
         micro2d) run micro2d 300 tools/microbench/fir2d_micro 15; fatal $? ;;
         dist2|dist4) n=${s#dist}

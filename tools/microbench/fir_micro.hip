@@ -133,7 +133,7 @@ static const int32_t kTaps[5] = {-256, -1024, 6656, -1024, -256};
 
 template <int U, int FLAGS>
 static void launch_fir(const int16_t* x, int32_t* y, int64_t n, hipStream_t s, int pblocks) {
-    RowGeom g{n, 0, 0};
+    RowGeom g{n, 0, 0, 1};
     TapsN<5> t;
     for (int k = 0; k < 5; ++k) t.h[0][k] = kTaps[k];
     pack_taps(t);

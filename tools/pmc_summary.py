@@ -8,7 +8,7 @@ on gfx950 FETCH_SIZE reports exactly half of the bytes of a wide (16 B/lane) coa
 streaming read, so it is doubled; WRITE_SIZE is exact for 16-B/lane streaming stores.
 
 Usage: tools/pmc_summary.py <dir with pmc_FETCH_SIZE/ and pmc_WRITE_SIZE/> <kernel substring>
-                            <algorithmic bytes per launch> <out.json>
+                            <algorithmic bytes per launch> <out.json> [dir prefix, default pmc_]
 """
 from __future__ import annotations
 
@@ -32,8 +32,9 @@ def per_launch(path: Path, counter: str, kernel: str) -> list[float]:
 
 def main() -> None:
     root, kernel, alg, out = Path(sys.argv[1]), sys.argv[2], int(sys.argv[3]), Path(sys.argv[4])
-    fetch = per_launch(root / "pmc_FETCH_SIZE" / "run_counter_collection.csv", "FETCH_SIZE", kernel)
-    write = per_launch(root / "pmc_WRITE_SIZE" / "run_counter_collection.csv", "WRITE_SIZE", kernel)
+    pre = sys.argv[5] if len(sys.argv) > 5 else "pmc_"
+    fetch = per_launch(root / f"{pre}FETCH_SIZE" / "run_counter_collection.csv", "FETCH_SIZE", kernel)
+    write = per_launch(root / f"{pre}WRITE_SIZE" / "run_counter_collection.csv", "WRITE_SIZE", kernel)
     fetch_b = statistics.median(fetch) * 1024 * 2  # KiB -> B, x2 gfx950 correction
     write_b = statistics.median(write) * 1024
     summary = {

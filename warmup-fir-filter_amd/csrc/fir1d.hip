@@ -100,6 +100,7 @@ static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t
     g.total = total;
     g.rowlen32 = (uint32_t)(rows > 1 ? rowlen : 0);
     g.multi_row = rows > 1;
+    g.aligned = rows == 1 || rowlen % (4 * InTraits<InT>::kPerDword) == 0;
     TapsN<L, F> t;
     for (int f = 0; f < F; ++f)
         for (int k = 0; k < L; ++k) t.h[f][k] = hq[f * L + k];
@@ -112,13 +113,24 @@ static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t
 }
 
 // Picks the kernel variant: acc_bits == 32 drops the wrap shifts; int16 samples with int16
-// taps (one channel) multiply on packed v_dot2_i32_i16.
+// taps (one channel) multiply on packed v_dot2_i32_i16; so do u8 samples (byte pairs) when
+// no accumulator can wrap: 255 * sum|h| + 2^(f-1) < 2^(acc_bits-1) for every filter.
 template <typename InT, int STAGE, int L, int CH, int F>
 static hipError_t launch_reg(const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
                              const int32_t* hq, int frac, int acc_bits, hipStream_t stream) {
     bool taps16 = true;
     for (int k = 0; k < F * L; ++k) taps16 &= hq[k] >= -32768 && hq[k] <= 32767;
     const bool acc32 = acc_bits == 32;
+    if constexpr (sizeof(InT) == 1 && CH == 1) {
+        bool nowrap = frac <= 22;
+        for (int f = 0; f < F; ++f) {
+            int64_t habs = 0;
+            for (int k = 0; k < L; ++k) habs += hq[f * L + k] < 0 ? -(int64_t)hq[f * L + k] : hq[f * L + k];
+            nowrap &= 255 * habs + ((int64_t)1 << (frac - 1)) < ((int64_t)1 << (acc_bits - 1));
+        }
+        if (taps16 && nowrap)
+            return launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kU8Dot2>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
+    }
     if constexpr (sizeof(InT) == 2 && CH == 1) {
         if (taps16)
             return acc32 ? launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kDot2 | kAcc32>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream)

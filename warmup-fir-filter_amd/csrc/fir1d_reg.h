@@ -27,6 +27,7 @@ enum RegFlags : int {
     kPersist = 4,  // grid-stride over tiles with the next tile's loads issued early
     kDot2 = 8,     // int16 samples, 1 channel, int16 taps: packed v_dot2_i32_i16 MACs
     kAcc32 = 16,   // acc_bits == 32: the wrap is the hardware's, skip the shl/ashr pair
+    kU8Dot2 = 32,  // u8 samples, 1 channel, int16 taps, no wrap possible: byte-pair v_dot2 MACs
 };
 
 constexpr int kDppWaveRol1 = 0x134;  // lane i <- lane i+1, lane 63 <- lane 0
@@ -62,6 +63,7 @@ struct RowGeom {
     int64_t total;      // samples in the buffer (rows * width * channels)
     uint32_t rowlen32;  // width * channels, valid when multi_row
     int multi_row;      // rows > 1 (then total < 2^32 is guaranteed by the host)
+    int aligned;        // one row, or rows a whole number of vectors: no vector straddles a row
 };
 
 // Load vector `v` (VEC samples) into 4 dwords: one 16-byte load when wholly in range,
@@ -91,17 +93,24 @@ __device__ __forceinline__ void load_vec(const InT* __restrict__ x, int64_t v, i
     }
 }
 
-template <int STAGE, int VEC, bool NT>
+// PRESAT: q already holds the saturated bytes (u8 stage), no clamp needed.
+template <int STAGE, int VEC, bool NT, bool PRESAT = false>
 __device__ __forceinline__ void store_vec(typename OutTraits<STAGE>::T* __restrict__ y, int64_t g0, int64_t total,
                                           bool full, const int32_t (&q)[VEC]) {
     if (full) {
         if constexpr (STAGE == FIR_OUT_U8_SAT) {
             uint32_t o[VEC / 4];
 #pragma unroll
-            for (int i = 0; i < VEC / 4; ++i)
-                o[i] = (uint32_t)stage_out32<STAGE>(q[4 * i]) | ((uint32_t)stage_out32<STAGE>(q[4 * i + 1]) << 8) |
-                       ((uint32_t)stage_out32<STAGE>(q[4 * i + 2]) << 16) |
-                       ((uint32_t)stage_out32<STAGE>(q[4 * i + 3]) << 24);
+            for (int i = 0; i < VEC / 4; ++i) {
+                if constexpr (PRESAT)
+                    o[i] = (uint32_t)q[4 * i] | ((uint32_t)q[4 * i + 1] << 8) | ((uint32_t)q[4 * i + 2] << 16) |
+                           ((uint32_t)q[4 * i + 3] << 24);
+                else
+                    o[i] = (uint32_t)stage_out32<STAGE>(q[4 * i]) |
+                           ((uint32_t)stage_out32<STAGE>(q[4 * i + 1]) << 8) |
+                           ((uint32_t)stage_out32<STAGE>(q[4 * i + 2]) << 16) |
+                           ((uint32_t)stage_out32<STAGE>(q[4 * i + 3]) << 24);
+            }
             if constexpr (VEC == 16) {
                 const u32x4 val = {o[0], o[1], o[2], o[3]};
                 u32x4* p = reinterpret_cast<u32x4*>(y + g0);
@@ -124,7 +133,7 @@ __device__ __forceinline__ void store_vec(typename OutTraits<STAGE>::T* __restri
         const int n = (int)min((int64_t)VEC, total - g0);
 #pragma unroll
         for (int j = 0; j < VEC; ++j)
-            if (j < n) y[g0 + j] = stage_out32<STAGE>(q[j]);
+            if (j < n) y[g0 + j] = PRESAT ? (typename OutTraits<STAGE>::T)q[j] : stage_out32<STAGE>(q[j]);
     }
 }
 
@@ -171,6 +180,45 @@ struct Dot2Vec {
     }
 };
 
+// u8 window bytes K and K+1 zero-extended into two int16 halves (one v_perm_b32, shared by
+// every output and filter that uses the pair); past the window the high half is a zero tap's.
+template <int NW, int K>
+__device__ __forceinline__ uint32_t byte_pair(const uint32_t* Wd) {
+    if constexpr (K + 1 < 4 * NW) {
+        return pair16<K>(Wd);
+    } else {
+        return __builtin_amdgcn_perm(0u, Wd[K / 4], (uint32_t)(K % 4) | 0x0C0C0C00u);
+    }
+}
+
+template <int NDL, int NW, int L, int J, int P>
+struct U8Dot2Row {  // sum over tap pairs p >= P for output J, continuing from acc
+    __device__ static __forceinline__ uint32_t run(const uint32_t* Wd, const uint32_t* pk, uint32_t acc) {
+        if constexpr (P < (L + 1) / 2) {
+            constexpr int HL = L - 1 - L / 2;
+            const uint32_t pr = byte_pair<NW, J - HL + 2 * P + 4 * NDL>(Wd);
+            acc = P == 0 ? dot2_from(pr, pk[0], acc) : dot2_acc(pr, pk[P], acc);
+            return U8Dot2Row<NDL, NW, L, J, P + 1>::run(Wd, pk, acc);
+        } else {
+            return acc;
+        }
+    }
+};
+
+// No-wrap u8 form: every chain starts at the rounding bias (a VGPR), the u8 stage is
+// v_med3 clamp then shift (sat_u8_pixel), the int32 stage one arithmetic shift.
+template <int NDL, int NW, int L, int J, int VEC, int STAGE>
+struct U8Dot2Vec {
+    __device__ static __forceinline__ void run(const uint32_t* Wd, const uint32_t* pk, uint32_t bias, int frac,
+                                               int32_t sat_hi, int32_t* q) {
+        if constexpr (J < VEC) {
+            const uint32_t acc = U8Dot2Row<NDL, NW, L, J, 0>::run(Wd, pk, bias);
+            q[J] = STAGE == FIR_OUT_U8_SAT ? (int32_t)sat_u8_pixel<true>(acc, 0, frac, sat_hi) : (int32_t)acc >> frac;
+            U8Dot2Vec<NDL, NW, L, J + 1, VEC, STAGE>::run(Wd, pk, bias, frac, sat_hi, q);
+        }
+    }
+};
+
 // Interior vector (the whole window inside one row): no masks.
 template <typename InT, int L, int CH, bool ACC32>
 __device__ __forceinline__ void fir_vector_interior(const int32_t* w, const int32_t* taps, int shl, int frac,
@@ -187,26 +235,28 @@ __device__ __forceinline__ void fir_vector_interior(const int32_t* w, const int3
     }
 }
 
-// Vector whose window crosses a row edge (or the buffer ends): per-sample column masks.
+// Vector whose window crosses a row edge (or a buffer end).  In window-relative sample
+// offsets o (vector start = 0) the vector's row spans [-a, b) and the next row [b, b + r);
+// outputs j < b see window w1 (samples outside [-a, b) zeroed), outputs j >= b window w2.
+// Both are plain interior sums; all tests are 32-bit (a, b, r clamped far beyond the window).
 template <typename InT, int L, int CH, bool ACC32>
-__device__ __forceinline__ void fir_vector_masked(const int32_t* w, int64_t col0, int64_t rowlen, const int32_t* taps,
-                                               int shl, int frac, int32_t* q) {
+__device__ __forceinline__ void fir_vector_masked(const int32_t* w, int a, int b, int r, const int32_t* taps,
+                                                  int shl, int frac, int32_t* q) {
     constexpr int VEC = 4 * InTraits<InT>::kPerDword;
     constexpr int C = L / 2;
     constexpr int HLE = (L - 1 - C) * CH;
+    constexpr int NS = HLE + VEC + C * CH;
+    int32_t w1[NS], w2[NS], q1[VEC], q2[VEC];
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) {
-        int64_t cj = col0 + j;
-        if (cj >= rowlen) cj -= rowlen;  // the vector crossed into the next row
-        uint32_t acc = 0;
-#pragma unroll
-        for (int k = 0; k < L; ++k) {
-            const int64_t p = cj + (C - k) * CH;
-            const uint32_t t = (uint32_t)__mul24(taps[k], w[HLE + j + (C - k) * CH]);
-            acc += (p >= 0 && p < rowlen) ? t : 0u;
-        }
-        q[j] = round_acc<ACC32>(acc, shl, frac);
+    for (int i = 0; i < NS; ++i) {
+        const int o = i - HLE;
+        w1[i] = (o >= -a && o < b) ? w[i] : 0;
+        w2[i] = (o >= b && o < b + r) ? w[i] : 0;
     }
+    fir_vector_interior<InT, L, CH, ACC32>(w1, taps, shl, frac, q1);
+    fir_vector_interior<InT, L, CH, ACC32>(w2, taps, shl, frac, q2);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) q[j] = j < b ? q1[j] : q2[j];
 }
 
 // y holds F output planes of g.total samples each (plane f at y + f * g.total).
@@ -227,7 +277,14 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
     constexpr bool NTL = FLAGS & kNtLoad, NTS = FLAGS & kNtStore, PERSIST = FLAGS & kPersist;
     constexpr bool DOT2 = (FLAGS & kDot2) && sizeof(InT) == 2 && CH == 1;
     constexpr bool ACC32 = FLAGS & kAcc32;
+    constexpr bool U8DOT2 = (FLAGS & kU8Dot2) && sizeof(InT) == 1 && CH == 1;
     constexpr int WPB = kBlock / kWave;
+    uint32_t bias = 0;
+    int32_t sat_hi = 0;
+    if constexpr (U8DOT2) {
+        asm("v_mov_b32 %0, %1" : "=v"(bias) : "s"(1u << (frac - 1)));  // once, for dot2_from's addend
+        sat_hi = (256 << frac) - 1;
+    }
 
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t total = g.total;
@@ -285,7 +342,22 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
                     rowlen = total;
                     col0 = g0;
                 }
-                const bool interior = col0 >= HLE && col0 + VEC + HRE <= rowlen;
+                bool interior = col0 >= HLE && col0 + VEC + HRE <= rowlen;
+                if (g.aligned) {
+                    // Every vector lies inside one row, so only its halo can leave the row: zero
+                    // the halo dwords (all of their samples are in the neighbouring row) and take
+                    // the unmasked path.  One row: the loads already zero-fill beyond both ends.
+                    if (g.multi_row) {
+                        const bool zl = col0 == 0, zr = col0 + VEC == rowlen;
+#pragma unroll
+                        for (int qd = 0; qd < NDL; ++qd) Wd[qd] = zl ? 0u : Wd[qd];
+#pragma unroll
+                        for (int qd = 0; qd < NDR; ++qd) Wd[NDL + 4 + qd] = zr ? 0u : Wd[NDL + 4 + qd];
+                    }
+                    interior = true;
+                }
+                constexpr int64_t kFar = 1 << 24;  // beyond any window offset
+                const int ma = (int)min(col0, kFar), mb = (int)min(rowlen - col0, kFar), mr = (int)min(rowlen, kFar);
                 // samples of the window as int32 (first window sample = -HLE)
                 int32_t w[HLE + VEC + HRE];
 #pragma unroll
@@ -299,13 +371,19 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
                     if (__builtin_expect(interior, 1)) {
                         if constexpr (DOT2) {
                             Dot2Vec<NDL, NW, L, 0, VEC, ACC32>::run(Wd, taps.pk[f], shl, frac, q);
+                        } else if constexpr (U8DOT2) {
+                            U8Dot2Vec<NDL, NW, L, 0, VEC, STAGE>::run(Wd, taps.pk[f], bias, frac, sat_hi, q);
                         } else {
                             fir_vector_interior<InT, L, CH, ACC32>(w, taps.h[f], shl, frac, q);
                         }
                     } else {
-                        fir_vector_masked<InT, L, CH, ACC32>(w, col0, rowlen, taps.h[f], shl, frac, q);
+                        fir_vector_masked<InT, L, CH, ACC32>(w, ma, mb, mr, taps.h[f], shl, frac, q);
+                        if constexpr (U8DOT2) {
+#pragma unroll
+                            for (int j = 0; j < VEC; ++j) q[j] = stage_out32<STAGE>(q[j]);
+                        }
                     }
-                    store_vec<STAGE, VEC, NTS>(y + f * total, g0, total, v < nvec, q);
+                    store_vec<STAGE, VEC, NTS, U8DOT2>(y + f * total, g0, total, v < nvec, q);
                 }
             }
         }

@@ -43,79 +43,9 @@ inline void pack_taps2(Taps2<R, C>& t) {
         }
 }
 
-typedef short fir_short2 __attribute__((ext_vector_type(2)));
-
-// v_dot2_i32_i16 (no clamp: wrap-around int32) on raw dwords
-__device__ __forceinline__ uint32_t dot2_acc(uint32_t a, uint32_t b, uint32_t c) {
-    return (uint32_t)__builtin_amdgcn_sdot2(__builtin_bit_cast(fir_short2, a), __builtin_bit_cast(fir_short2, b),
-                                            (int)c, false);
-}
-
-// First MAC of a chain without a zero-initialised destination: VOP3P v_dot2_i32_i16 with an
-// inline-constant or VGPR addend (hipcc otherwise emits v_dot2c plus a v_mov of the addend).
-// Pure VALU, no memory, no hazards: safe as inline asm.
-__device__ __forceinline__ uint32_t dot2_from0(uint32_t pair, uint32_t taps) {
-    uint32_t d;
-    asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(d) : "v"(pair), "s"(taps));
-    return d;
-}
-__device__ __forceinline__ uint32_t dot2_from(uint32_t pair, uint32_t taps, uint32_t c) {
-    uint32_t d;
-    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(pair), "s"(taps), "v"(c));
-    return d;
-}
-
-// v_mad_i32_i24 d = a[23:0] * b[23:0] + c (|a|, |b| < 2^23 host-checked); as asm because hipcc
-// sign-extends a value it cannot range-check (v_bfe_i32) before every __mul24.
-__device__ __forceinline__ uint32_t mad_i24(uint32_t a, int32_t b, uint32_t c) {
-    uint32_t d;
-    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "s"(b), "v"(c));
-    return d;
-}
-
-// bytes k and k+1 of a little-endian byte stream held in dwords s[], zero-extended into the
-// two 16-bit halves of one dword (one v_perm_b32).
-template <int K>
-__device__ __forceinline__ uint32_t pair16(const uint32_t* s) {
-    constexpr int d0 = K / 4, b0 = K % 4, d1 = (K + 1) / 4, b1 = (K + 1) % 4;
-    if constexpr (d0 == d1) {
-        constexpr uint32_t sel = (uint32_t)b0 | (0x0Cu << 8) | ((uint32_t)b1 << 16) | (0x0Cu << 24);
-        return __builtin_amdgcn_perm(s[d0], s[d0], sel);
-    } else {
-        // perm(hi_src, lo_src): bytes 0-3 = lo_src, 4-7 = hi_src
-        constexpr uint32_t sel = (uint32_t)b0 | (0x0Cu << 8) | ((uint32_t)(4 + b1) << 16) | (0x0Cu << 24);
-        return __builtin_amdgcn_perm(s[d1], s[d0], sel);
-    }
-}
-
-template <int K0, int N>
-struct PairBuilder {
-    __device__ static __forceinline__ void run(const uint32_t* s, uint32_t* P) {
-        if constexpr (N > 0) {
-            P[K0] = pair16<K0>(s);
-            PairBuilder<K0 + 1, N - 1>::run(s, P);
-        }
-    }
-};
-
 // Branch-free row load: the address is always in bounds (the caller clamps it) and the
 // value is zeroed by a select when the row/column is outside the frame, so the compiler can
 // count outstanding loads exactly (a load inside a branch makes it wait for all of them).
-// One saturated u8 output.  NOWRAP (bias already in acc): clamp to [0, 256*2^f - 1] first,
-// then shift -- the same value as sat(acc >> f), in an order hipcc (ROCm 7.2) does not fuse
-// into v_ashr_pk_u8_i32: that fusion left bits set above the packed byte pair, which the
-// following v_lshl_or merged into the next pixel (measured: wrong byte 2 of every dword).
-template <bool NOWRAP>
-__device__ __forceinline__ uint32_t sat_u8_pixel(uint32_t acc, int shl, int frac, int32_t sat_hi) {
-    if constexpr (NOWRAP) {
-        uint32_t c;  // v_med3_i32(acc, 0, hi) == clamp(acc, 0, hi) since hi > 0 (hipcc emits max + min)
-        asm("v_med3_i32 %0, %1, 0, %2" : "=v"(c) : "v"(acc), "s"(sat_hi));
-        return c >> frac;
-    } else {
-        return (uint32_t)min(max(round32(acc, shl, frac), 0), 255);
-    }
-}
-
 template <int ND>
 __device__ __forceinline__ void load_row_px(const uint8_t* __restrict__ p, bool ok, uint32_t (&d)[ND]) {
     typedef uint32_t vN __attribute__((ext_vector_type(ND)));
