@@ -198,6 +198,8 @@ int main(int argc, char** argv) {
         {"fir U1 mad", true, launch_fir<1, 0>, 0, {}},
         {"fir U1 mad acc32", true, launch_fir<1, kAcc32>, 0, {}},
         {"fir U1 dot2 acc32", true, launch_fir<1, kDot2 | kAcc32>, 0, {}},
+        {"fir U1 dot2 acc32 coal", true, launch_fir<1, kDot2 | kAcc32 | kCoal>, 0, {}},
+        {"fir U2 dot2 acc32 coal", true, launch_fir<2, kDot2 | kAcc32 | kCoal>, 0, {}},
         {"fir U1 dot2", true, launch_fir<1, kDot2>, 0, {}},
         {"fir U2 dot2 acc32", true, launch_fir<2, kDot2 | kAcc32>, 0, {}},
         {"fir U1 dot2 acc32 nt-ld", true, launch_fir<1, kDot2 | kAcc32 | kNtLoad>, 0, {}},

@@ -85,11 +85,12 @@ __global__ __launch_bounds__(kBlock) void fir1d_generic_kernel(const InT* __rest
 // ---------------------------------------------------------------------------------------
 // Host-side launchers.
 
-// Hot-kernel shape chosen by the A/B microbenchmark (tools/microbench; profiles/r01_micro.txt):
+// Hot-kernel shape chosen by the A/B microbenchmark (tools/microbench; profiles/r01/micro_*.txt):
 // one 64-vector chunk per wave, default-policy loads and stores (non-temporal stores cost
-// 25-45 % on this 1:2 read:write stream; more chunks per wave or a persistent grid 3-15 %).
+// 25-45 % on this 1:2 read:write stream; more chunks per wave or a persistent grid 3-15 %),
+// int32 outputs staged through LDS into whole 1 KiB store instructions (272 -> 257 us).
 constexpr int kRegU = 1;
-constexpr int kRegFlags = 0;
+constexpr int kRegFlags = kCoal;
 constexpr int kPersistBlocks = 2048;
 
 template <typename InT, int STAGE, int L, int CH, int F, int FL>

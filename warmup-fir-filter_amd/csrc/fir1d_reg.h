@@ -28,6 +28,8 @@ enum RegFlags : int {
     kDot2 = 8,     // int16 samples, 1 channel, int16 taps: packed v_dot2_i32_i16 MACs
     kAcc32 = 16,   // acc_bits == 32: the wrap is the hardware's, skip the shl/ashr pair
     kU8Dot2 = 32,  // u8 samples, 1 channel, int16 taps, no wrap possible: byte-pair v_dot2 MACs
+    kCoal = 64,    // int32 outputs of a full 64-vector chunk go out through LDS as contiguous
+                   // 1 KiB store instructions (instead of 16 B per lane at a 16*VEC/4-byte stride)
 };
 
 constexpr int kDppWaveRol1 = 0x134;  // lane i <- lane i+1, lane 63 <- lane 0
@@ -278,6 +280,7 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
     constexpr bool DOT2 = (FLAGS & kDot2) && sizeof(InT) == 2 && CH == 1;
     constexpr bool ACC32 = FLAGS & kAcc32;
     constexpr bool U8DOT2 = (FLAGS & kU8Dot2) && sizeof(InT) == 1 && CH == 1;
+    constexpr bool COAL = (FLAGS & kCoal) && STAGE == FIR_OUT_I32;
     constexpr int WPB = kBlock / kWave;
     uint32_t bias = 0;
     int32_t sat_hi = 0;
@@ -381,6 +384,23 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
                         if constexpr (U8DOT2) {
 #pragma unroll
                             for (int j = 0; j < VEC; ++j) q[j] = stage_out32<STAGE>(q[j]);
+                        }
+                    }
+                    if constexpr (COAL) {
+                        if (vb + (u + 1) * kWave <= nvec) {  // wave-uniform: the whole chunk is full
+                            __shared__ u32x4 sbuf[kBlock * VEC / 4];
+                            u32x4* wb = sbuf + (threadIdx.x - lane) * (VEC / 4);
+#pragma unroll
+                            for (int i = 0; i < VEC / 4; ++i)
+                                wb[lane * (VEC / 4) + i] = u32x4{(uint32_t)q[4 * i], (uint32_t)q[4 * i + 1],
+                                                                 (uint32_t)q[4 * i + 2], (uint32_t)q[4 * i + 3]};
+                            __builtin_amdgcn_wave_barrier();  // one wave's LDS ops complete in order
+                            asm volatile("" ::: "memory");
+                            u32x4* yw = reinterpret_cast<u32x4*>(y + f * total + (vb + u * kWave) * VEC);
+#pragma unroll
+                            for (int i = 0; i < VEC / 4; ++i) yw[i * kWave + lane] = wb[i * kWave + lane];
+                            asm volatile("" ::: "memory");
+                            continue;
                         }
                     }
                     store_vec<STAGE, VEC, NTS, U8DOT2>(y + f * total, g0, total, v < nvec, q);
