@@ -18,8 +18,10 @@ prints ONE JSON line.  Extra keys:
                 bounded leading slice of the same input (BASELINE.md's "NumPy CPU path")
 Other workloads: `cplx_i16` / `fir2d_u8` measure configs[2] / configs[4]; `fir1d_u8` the
 reference's own u8 -> sat-u8 golden path (a1/a4) at scale; `ideal_u8` (the f64
-ideal model) and `bank_u8` (the fused 4-filter 3-tap bank, §8(f) 3) measure
-the next rows on 2^28 u8 samples in 4096-sample rows (the reference's image-row layout).
+ideal model), `bank_u8` (the fused 4-filter 3-tap bank, §8(f) 3) and
+`restore_u8` (the f64 -> u8 clip conversion, §8(f) 4) measure the next rows on 2^28 samples in
+4096-sample rows (the reference's image-row layout).  For workloads without a C oracle leg
+(restore_u8) cpu_baseline times the NumPy restatement.
 """
 from __future__ import annotations
 
@@ -52,7 +54,8 @@ SHARPEN5_F64 = [-1 / 16, -4 / 16, 26 / 16, -4 / 16, -1 / 16]  # h_coeff_5tap_map
 BANK3 = [[1365] * 3, [1024, 2048, 1024], [-4096, 0, 4096], [-512, 5120, -512]]  # h_coeff_3tap_map, Q4.12
 ROW_W = 4096
 KERNELS = {"fir1d_i16": "fir1d_reg_kernel", "cplx_i16": "fir1d_reg_kernel", "fir2d_u8": "fir2d_reg_kernel",
-           "fir1d_u8": "fir1d_reg_kernel", "ideal_u8": "fir1d_ideal_kernel", "bank_u8": "fir1d_reg_kernel"}
+           "fir1d_u8": "fir1d_reg_kernel", "ideal_u8": "fir1d_ideal_kernel", "bank_u8": "fir1d_reg_kernel",
+           "restore_u8": "restore_map_kernel"}
 
 
 def _env_int(name: str, default: int) -> int:
@@ -128,6 +131,15 @@ class Workload:
                 self.dtype = "int32 (u8 in, int32 wrap-around acc, u8 saturated out x 4 filters)"
                 self.config = {"workload": "fir1d_u8_bank4_3tap_q4.12_rows4096", "samples_per_gpu": self.n,
                                "row_width": ROW_W, "filters": len(BANK3), "taps": 3, "parallelism": par}
+        elif name == "restore_u8":
+            self.n = 1 << log2n
+            self.x_host = rng.uniform(-64.0, 320.0, (self.n // ROW_W, ROW_W))  # ideal-output-like f64 rows
+            self.units = self.n
+            self.unit = "Gsamples/s"
+            self.bytes_per_unit = 8 + 1
+            self.dtype = "f64 in, u8 out (rint, clip)"
+            self.config = {"workload": "restore_f64_to_u8_clip_rows4096", "samples_per_gpu": self.n,
+                           "parallelism": "single GPU (replicas when N > 1)"}
         else:
             raise SystemExit(f"unknown workload {name}")
         self.x = torch.from_numpy(self.x_host).to(dev)
@@ -135,6 +147,8 @@ class Workload:
             self.y = torch.empty(self.x.shape, dtype=torch.float64, device=dev)
         elif name == "bank_u8":
             self.y = torch.empty((len(BANK3),) + tuple(self.x.shape), dtype=torch.uint8, device=dev)
+        elif name == "restore_u8":
+            self.y = torch.empty(self.x.shape, dtype=torch.uint8, device=dev)
         else:
             u8 = name in ("fir2d_u8", "fir1d_u8")
             self.y = torch.empty(self.x.shape, dtype=torch.uint8 if u8 else torch.int32, device=dev)
@@ -153,6 +167,8 @@ class Workload:
             torch_ops.fir1d_fixed_rows_multi_dev(self.x, BANK3, 12, 32, fir_hip.OUT_U8_SAT, out=self.y)
         elif self.name == "fir1d_u8":
             torch_ops.fir1d_fixed_rows_dev(self.x, self.taps, 12, 32, fir_hip.OUT_U8_SAT, out=self.y)
+        elif self.name == "restore_u8":
+            torch_ops.restore_u8_dev(self.x, fir_hip.RESTORE_CLIP, out=self.y)
         else:
             torch_ops.fir1d_fixed_rows_dev(self.x, self.taps, 12, 32, fir_hip.OUT_I32, self.channels, out=self.y)
 
@@ -183,6 +199,10 @@ class Workload:
                                 for h in BANK3])
             elif self.name == "fir1d_u8":
                 out = co.fir1d_rows(self.x_host, self.taps.h, 12, 32, co.OUT_U8_SAT, nthreads=nthreads)
+            elif self.name == "restore_u8":
+                from oracle import fir_oracle as fo
+
+                out = fo.to_u8_clip(self.x_host)
             else:
                 hl = None if self.left is None else self.left.cpu().numpy()
                 hr = None if self.right is None else self.right.cpu().numpy()
@@ -198,9 +218,11 @@ class Workload:
             rows = max(1, min(self.h, max_units // self.w))
             fo.fir2d_fixed(self.x_host[:rows], self.hq2, 12, 32, fo.OUT_U8_SAT)
             return rows * self.w
-        if self.name in ("ideal_u8", "bank_u8", "fir1d_u8"):
+        if self.name in ("ideal_u8", "bank_u8", "fir1d_u8", "restore_u8"):
             rows = max(1, min(self.x_host.shape[0], max_units // ROW_W))
-            if self.name == "fir1d_u8":
+            if self.name == "restore_u8":
+                fo.to_u8_clip(self.x_host[:rows])
+            elif self.name == "fir1d_u8":
                 fo.fir1d_rows(self.x_host[:rows], self.taps.h, 12, 32, fo.OUT_U8_SAT)
             elif self.name == "ideal_u8":
                 fo.fir1d_ideal_rows(self.x_host[:rows], SHARPEN5_F64)
@@ -305,9 +327,12 @@ def main() -> int:
             if time.perf_counter() - tc0 >= args.cpu_seconds:
                 break
         tc = time.perf_counter() - tc0
-        cpu = {"value": round(wl.units * reps / tc / 1e9, 4), "unit": wl.unit, "cores": nthr, "kind": "port",
-               "sample": f"C oracle (oracle/fir_oracle.c, OpenMP {nthr} threads) on the full per-GPU workload "
-                         f"({wl.units} units) x {reps} repetitions, {tc:.1f} s"}
+        np_only = args.workload == "restore_u8"  # no C leg: the NumPy restatement, one thread
+        what = "NumPy restatement (oracle/fir_oracle.py)" if np_only else \
+            f"C oracle (oracle/fir_oracle.c, OpenMP {nthr} threads)"
+        cpu = {"value": round(wl.units * reps / tc / 1e9, 4), "unit": wl.unit, "cores": 1 if np_only else nthr,
+               "kind": "port", "sample": f"{what} on the full per-GPU workload ({wl.units} units) x {reps} "
+                                         f"repetitions, {tc:.1f} s"}
         tn0 = time.perf_counter()
         done = wl.numpy_oracle(1 << 24)
         tn = time.perf_counter() - tn0

@@ -27,6 +27,12 @@
  *   fir1d_ideal_rows[_dev] fir_1d/model/python/fir_1d_ref.py:43-65 (fir_1d_ideal) per row as
  *                         in fir_1d/sim/vector/gen_ideal_output.py:37-50.
  *   fir_compare_metrics   fir_1d/sim/vector/gen_3tap_compare_report.py:67-112 (_compute_metrics).
+ *   fir1d_fixed_rows_sharded  the `fir1d_sharded(..., ndev)` entry of SURVEY §8(b): one call
+ *                         spread over several devices of this process (rows split, or a long
+ *                         row split into segments with their halos); the reference has no
+ *                         multi-device form.
+ *   fir_restore_u8[_dev]  fir_1d/sim/vector/restore_images.py:51-64 (_to_u8_clip,
+ *                         _to_u8_normalized), the array half of the restore stage.
  *
  * Arithmetic (all fixed entries): y[n] = stage(round(wrap_acc(sum_k hq[k] * x[n - k + L/2])))
  *   wrap_acc: two's-complement wrap to acc_bits (fir_1d_fixed_ref.py:110-115)
@@ -98,6 +104,17 @@ int fir1d_fixed_edges_dev(const void* x_dev, int in_dtype, int64_t n, int channe
                           const void* halo_left_dev, const void* halo_right_dev, void* y_dev,
                           void* stream);
 
+/* One-process multi-device form of fir1d_fixed_rows.  `devices`
+ * lists ndev device ids (repeats allowed: a device then runs its shards in turn).
+ * rows > 1: contiguous blocks of rows, no exchange (rows are independent).
+ * rows == 1: contiguous segments; each device receives its segment plus the
+ * (taps-1-taps/2)*channels / (taps/2)*channels neighbour samples around it from the host
+ * buffer, so no device-to-device exchange is needed.  One host thread per distinct
+ * device; synchronous; results identical to fir1d_fixed_rows. */
+int fir1d_fixed_rows_sharded(const void* x, int in_dtype, int64_t rows, int64_t width, int channels,
+                             const int32_t* hq, int taps, int frac_bits, int acc_bits, int out_stage,
+                             void* y, const int* devices, int ndev);
+
 /* ---- 2-D fixed-point FIR (a8) ------------------------------------------------------
  * y[i,j] = stage(round(wrap(sum_m sum_n hq[m*tap_cols+n] * x[i-m+tap_rows/2][j-n+tap_cols/2])))
  * x: height x width uint8, zero padded at every frame edge. */
@@ -124,6 +141,19 @@ int64_t fir_metrics_work_bytes(void);
 int fir_compare_metrics(const double* ideal, const uint8_t* fixed, int64_t n, double* out, int device);
 int fir_compare_metrics_dev(const double* ideal_dev, const uint8_t* fixed_dev, int64_t n, double* out_dev,
                             void* work_dev, void* stream);
+
+/* ---- restore-stage u8 conversion -----------------------------------
+ * out[i] = u8 of a[i] (float64), n samples:
+ *   FIR_RESTORE_CLIP       clip(rint(a), 0, 255)                         (restore_images.py:51-54)
+ *   FIR_RESTORE_NORMALIZE  0 if max <= min, else rint(clip((a - min) * (255 / (max - min)),
+ *                          0, 255))                                        (:57-64)
+ * rint rounds half to even; NaN maps to 0.  The _dev form needs fir_restore_work_bytes() of
+ * device scratch (normalize only; may be NULL for clip); a and out 16-byte aligned. */
+typedef enum { FIR_RESTORE_CLIP = 0, FIR_RESTORE_NORMALIZE = 1 } fir_restore_policy;
+int64_t fir_restore_work_bytes(void);
+int fir_restore_u8(const double* a, int64_t n, int policy, uint8_t* out, int device);
+int fir_restore_u8_dev(const double* a_dev, int64_t n, int policy, uint8_t* out_dev, void* work_dev,
+                       void* stream);
 
 #ifdef __cplusplus
 }

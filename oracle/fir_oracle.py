@@ -21,6 +21,8 @@ Reference lines restated (paths relative to the reference root):
   fir1d_ideal_rows fir_1d/model/python/fir_1d_ref.py:43-65 (float64, k-order sum, no clamp)
                   per row as in fir_1d/sim/vector/gen_ideal_output.py:37-50
   compute_metrics fir_1d/sim/vector/gen_3tap_compare_report.py:67-112
+  to_u8_clip      fir_1d/sim/vector/restore_images.py:51-54 (rint, clip, cast)
+  to_u8_normalized fir_1d/sim/vector/restore_images.py:57-64 (min/max rescale)
 
 Variants the reference does not have are defined here by
 the same arithmetic:
@@ -210,3 +212,17 @@ def compute_metrics(y_ideal, y_fixed) -> dict:
         "sat_ratio": lo + hi,
         "clip_needed_ratio": float(np.mean((ideal < 0.0) | (ideal > 255.0))) if n else 0.0,
     }
+
+
+def to_u8_clip(a) -> np.ndarray:
+    """restore_images.py:51-54."""
+    return np.clip(np.rint(np.asarray(a, np.float64)), 0, 255).astype(np.uint8)
+
+
+def to_u8_normalized(a) -> np.ndarray:
+    """restore_images.py:57-64."""
+    a = np.asarray(a, np.float64)
+    lo, hi = float(a.min()), float(a.max())
+    if hi <= lo:
+        return np.zeros(a.shape, dtype=np.uint8)
+    return np.rint(np.clip((a - lo) * (255.0 / (hi - lo)), 0, 255)).astype(np.uint8)

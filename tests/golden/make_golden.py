@@ -14,6 +14,7 @@ Reference entry points exercised (paths relative to the reference root):
   fir_1d/sim/vector/gen_ideal_output.py:37     _run_ideal_rowwise
   fir_1d/sim/vector/gen_3tap_compare_report.py:67  _compute_metrics
   fir_1d/sim/vector/h_coeff.py:3-16            coefficient banks
+  fir_1d/sim/vector/restore_images.py:51,57    _to_u8_clip, _to_u8_normalized
 
 Files written:
   kat_fixed.json, kat_ideal.json     known-answer + error cases (reference tests' vectors)
@@ -21,6 +22,8 @@ Files written:
   images_u8.npz                      the 7 decoded golden input images (u8, H x W)
   image_outputs.json                 sha256 of all 56 fixed + 56 ideal outputs + report metrics
   small_image_outputs.npz            full fixed/ideal outputs of the two 64x64 cases
+  restore_u8.npz                     restore conversions (clip / normalize) of the 16 small
+                                     ideal outputs and of edge-case arrays (ties, +-0, range ends)
   meta.json                          generator environment
 
 Usage:  python tests/golden/make_golden.py [--jobs 8]
@@ -296,11 +299,39 @@ def gen_images(jobs):
     return len(outputs)
 
 
+def gen_restore():
+    if str(REF) not in sys.path:
+        sys.path.insert(0, str(REF))
+    from fir_1d.sim.vector import restore_images as ri
+
+    small = np.load(OUT / "small_image_outputs.npz")
+    arrays = {k: small[k] for k in sorted(small.files) if "_ideal_" in k}
+    rng = np.random.default_rng(515)
+    ties = np.arange(-4.0, 260.0, 0.5).reshape(8, -1)  # every x.5 tie across the u8 range and beyond
+    arrays["edge_ties"] = ties
+    arrays["edge_signed_zero"] = np.array([[-0.0, 0.0, -0.4, 0.4, -0.5, 0.5], [254.5, 255.5, 255.49, -1e300, 1e300, 7.0]])
+    arrays["edge_constant"] = np.full((3, 5), 42.25)
+    arrays["edge_uniform"] = rng.uniform(-300.0, 600.0, (37, 53))
+    arrays["edge_narrow"] = 100.0 + rng.uniform(0.0, 1e-9, (16, 16))
+    arrays["edge_single"] = np.array([[3.5]])
+    out = {}
+    for k, a in arrays.items():
+        out[f"{k}__in"] = a
+        out[f"{k}__clip"] = ri._to_u8_clip(a)
+        out[f"{k}__normalize"] = ri._to_u8_normalized(a)
+    np.savez_compressed(OUT / "restore_u8.npz", **out)
+    return len(arrays)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("--skip-images", action="store_true")
+    ap.add_argument("--only-restore", action="store_true")
     args = ap.parse_args()
+    if args.only_restore:
+        print("restore", gen_restore())
+        return
     fixed_ref, ideal_ref, *_ = _ref_imports()
     import PIL
     meta = {"reference": str(REF), "numpy": np.__version__, "pillow": PIL.__version__,
@@ -310,6 +341,7 @@ def main():
     print("random_ideal", gen_random_ideal(ideal_ref))
     if not args.skip_images:
         print("images", gen_images(args.jobs))
+    print("restore", gen_restore())
     (OUT / "meta.json").write_text(json.dumps(meta, indent=1) + "\n")
 
 

@@ -61,3 +61,18 @@ def test_errors_surface_as_firhiperror():
         fir_hip._taps_i32([])
     with pytest.raises(fir_hip.FirHipError):
         fir_hip._taps_i32(list(range(fir_hip.MAX_TAPS + 1)))
+
+
+def test_sharded_and_restore_argument_checks_without_device(lib):
+    h = (ctypes.c_int32 * 3)(1, 2, 1)
+    devs = (ctypes.c_int32 * 1)(0)
+    assert lib.fir1d_fixed_rows_sharded(None, 0, 1, 16, 1, h, 3, 12, 32, 0, None, devs, 0) == 1
+    assert b"ndev" in lib.fir_last_error()
+    assert lib.fir1d_fixed_rows_sharded(None, 5, 1, 16, 1, h, 3, 12, 32, 0, None, devs, 1) == 1
+    assert b"in_dtype" in lib.fir_last_error()
+    assert lib.fir1d_fixed_rows_sharded(None, 0, 0, 16, 1, h, 3, 12, 32, 0, None, devs, 1) == 0  # empty no-op
+    assert lib.fir_restore_u8_dev(None, 8, 7, None, None, None) == 1
+    assert b"policy" in lib.fir_last_error()
+    assert lib.fir_restore_u8_dev(None, 0, 1, None, None, None) == 0
+    assert lib.fir_restore_u8_dev(None, 8, 1, None, None, None) == 1
+    assert lib.fir_restore_work_bytes() >= 256

@@ -102,3 +102,14 @@ def test_pipeline_restore_small_images(tmp_path, images):
     assert res["restore_summary"]["num_converted"] == 16
     assert len(list((tmp_path / "img" / "ideal_5tap_normalize").glob("*.png"))) == 8
     assert len(list((tmp_path / "img" / "fixed_5tap").glob("*.png"))) == 8
+    # every restored pixel: ideal -> the reference's _to_u8_normalized output, fixed -> as is
+    from PIL import Image
+
+    want = np.load(GOLDEN / "restore_u8.npz")
+    small_out = np.load(GOLDEN / "small_image_outputs.npz")
+    for png in (tmp_path / "img" / "ideal_5tap_normalize").glob("*.png"):
+        key = png.name.replace("_y_f64.png", "")
+        assert np.array_equal(np.asarray(Image.open(png)), want[key + "__normalize"]), png.name
+    for png in (tmp_path / "img" / "fixed_5tap").glob("*.png"):
+        key = png.name.replace("_y_u8.png", "")
+        assert np.array_equal(np.asarray(Image.open(png)), small_out[key]), png.name

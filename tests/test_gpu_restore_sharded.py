@@ -1,0 +1,102 @@
+"""GPU: the restore-stage u8 conversions and the one-process multi-device
+entry fir1d_fixed_rows_sharded, both through the C ABI.
+
+Restore: bit-exact against the reference's own _to_u8_clip / _to_u8_normalized outputs
+(tests/golden/restore_u8.npz, made by tests/golden/make_golden.py) and against the oracle
+on large random arrays (ties at every x.5, both signs of zero, values far out of range).
+Sharded: the box has one GPU, so shards go to repeated ids of device 0 (each shard is its
+own H2D / kernel / D2H with the halo taken from the host buffer); results must equal the
+unsharded call and the oracle for rows split and single-row segments, every tap count the
+register kernel covers, complex channels, and more shards than rows or samples.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+import fir_hip
+from conftest import GOLDEN
+from fir_hip import torch_ops
+from oracle import c_oracle, fir_oracle as fo
+
+
+def test_restore_reference_outputs_bit_exact():
+    d = np.load(GOLDEN / "restore_u8.npz")
+    names = [k[:-4] for k in d.files if k.endswith("__in")]
+    assert len(names) == 22
+    for name in names:
+        a = d[name + "__in"]
+        assert np.array_equal(fir_hip.restore_u8(a, fir_hip.RESTORE_CLIP), d[name + "__clip"]), name
+        assert np.array_equal(fir_hip.restore_u8(a, fir_hip.RESTORE_NORMALIZE), d[name + "__normalize"]), name
+
+
+@pytest.mark.parametrize("n", [1, 7, 1023, 1024, 1025, 4096 * 3 + 5, (1 << 22) + 333])
+def test_restore_random_vs_oracle(n):
+    rng = np.random.default_rng(n)
+    a = rng.uniform(-400.0, 700.0, n)
+    a[rng.integers(0, n, max(1, n // 10))] = rng.integers(-5, 262, max(1, n // 10)) + 0.5  # ties
+    a[: min(n, 2)] = [-0.0, 0.0][: min(n, 2)]
+    assert np.array_equal(fir_hip.restore_u8(a, fir_hip.RESTORE_CLIP), fo.to_u8_clip(a))
+    assert np.array_equal(fir_hip.restore_u8(a, fir_hip.RESTORE_NORMALIZE), fo.to_u8_normalized(a))
+
+
+def test_restore_shapes_constant_and_empty():
+    a = np.full((33, 65), -7.0)
+    assert np.array_equal(fir_hip.restore_u8(a, fir_hip.RESTORE_NORMALIZE), np.zeros((33, 65), np.uint8))
+    assert fir_hip.restore_u8(a).shape == (33, 65)
+    assert fir_hip.restore_u8(np.zeros((0, 4))).shape == (0, 4)
+    with pytest.raises(ValueError, match="zero-size"):
+        fir_hip.restore_u8(np.zeros(0), fir_hip.RESTORE_NORMALIZE)
+
+
+def test_restore_dev_on_ideal_outputs(images):
+    co = c_oracle()
+    x = images["case_000_img_001_1280x853_gray"]
+    yi = co.fir1d_ideal_rows(x, [-1 / 16, -4 / 16, 26 / 16, -4 / 16, -1 / 16])
+    t = torch.from_numpy(yi).cuda()
+    for pol, ref in ((fir_hip.RESTORE_CLIP, fo.to_u8_clip), (fir_hip.RESTORE_NORMALIZE, fo.to_u8_normalized)):
+        got = torch_ops.restore_u8_dev(t, pol)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy(), ref(yi))
+
+
+SHARD_DEVS = [[0], [0, 0], [0, 0, 0], [0] * 7]
+
+
+@pytest.mark.parametrize("devs", SHARD_DEVS)
+@pytest.mark.parametrize("L", [1, 2, 3, 5, 9, 12])
+def test_sharded_single_row_i16(devs, L):
+    rng = np.random.default_rng(100 + L * 10 + len(devs))
+    n = 100_003
+    x = rng.integers(-32768, 32768, n, dtype=np.int16)
+    hq = rng.integers(-20000, 20000, L)
+    got = fir_hip.fir1d_fixed_rows_sharded(x, hq, 12, 32, fir_hip.OUT_I32, devices=devs)
+    assert np.array_equal(got, fo.fir1d_i16_i32(x, hq, 12, 32))
+
+
+@pytest.mark.parametrize("devs", SHARD_DEVS)
+def test_sharded_complex_and_u8_rows(devs, images):
+    rng = np.random.default_rng(7)
+    xc = rng.integers(-32768, 32768, 2 * 50_001, dtype=np.int16)
+    got = fir_hip.fir1d_fixed_rows_sharded(xc, [1024, 2048, 1024], 12, 32, fir_hip.OUT_I32, channels=2,
+                                           devices=devs)
+    assert np.array_equal(got, fo.fir1d_i16_i32(xc, [1024, 2048, 1024], 12, 32, channels=2))
+    x = images["case_005_img_006_4499x2999_gray"]
+    hq = fo.quantize_h([-1 / 16, -4 / 16, 26 / 16, -4 / 16, -1 / 16])
+    got = fir_hip.fir1d_fixed_rows_sharded(x, hq, 12, 32, fir_hip.OUT_U8_SAT, devices=devs)
+    assert np.array_equal(got, fir_hip.fir1d_fixed_rows(x, hq, 12, 32, fir_hip.OUT_U8_SAT))
+
+
+def test_sharded_more_shards_than_work():
+    x = np.arange(3 * 40, dtype=np.uint8).reshape(3, 40)
+    got = fir_hip.fir1d_fixed_rows_sharded(x, [256, 1024, 1536, 1024, 256], devices=[0] * 5)
+    assert np.array_equal(got, fo.fir1d_rows(x, [256, 1024, 1536, 1024, 256], 12, 32, fo.OUT_U8_SAT))
+    x1 = np.arange(3, dtype=np.int16)
+    got = fir_hip.fir1d_fixed_rows_sharded(x1, [3, -7, 11], 4, 32, fir_hip.OUT_I32, devices=[0] * 5)
+    assert np.array_equal(got, fo.fir1d_i16_i32(x1, [3, -7, 11], 4, 32))
+
+
+def test_sharded_bad_device_is_an_error():
+    with pytest.raises(fir_hip.FirHipError, match="out of range"):
+        fir_hip.fir1d_fixed_rows_sharded(np.zeros(64, np.uint8), [1, 2, 1], devices=[0, 99])

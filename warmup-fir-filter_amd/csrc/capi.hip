@@ -8,10 +8,13 @@
 // captured in a hipGraph.  No C++ exception crosses the boundary.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fir_hip.h"
@@ -97,16 +100,20 @@ int init_locked(DeviceState* st, int device) {
 size_t in_size(int in_dtype) { return in_dtype == FIR_IN_I16 ? 2 : 1; }
 size_t out_size(int stage) { return stage == FIR_OUT_I32 ? 4 : 1; }
 
-// Run `launch(dx, dy, stream)` between an H2D copy of `in_bytes` and a D2H copy of `out_bytes`.
+// Run `launch(dx, dy, stream)` between an H2D copy of `in_bytes` and a D2H copy of `out_bytes`
+// (taken from byte `out_skip` of the device output).  The device buffers hold at least
+// in_cap / out_cap bytes (scratch after the input, outputs not copied back).
 template <typename F>
-int run_host(int device, const void* x, size_t in_bytes, void* y, size_t out_bytes, F launch) {
+int run_host(int device, const void* x, size_t in_bytes, void* y, size_t out_bytes, F launch, size_t out_skip = 0,
+             size_t in_cap = 0, size_t out_cap = 0) {
     DeviceState* st = nullptr;
     int rc = device_state(device, &st);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(st->mu);
     rc = init_locked(st, device);
     if (rc) return rc;
-    if ((rc = ensure(st->in, in_bytes)) || (rc = ensure(st->out, out_bytes))) return rc;
+    if ((rc = ensure(st->in, std::max(in_bytes, in_cap))) || (rc = ensure(st->out, std::max(out_skip + out_bytes, out_cap))))
+        return rc;
     HIP_TRY(hipMemcpyAsync(st->in.ptr, x, in_bytes, hipMemcpyHostToDevice, st->stream));
     std::string err;
     rc = launch(st->in.ptr, st->out.ptr, st->stream, &err);
@@ -114,7 +121,7 @@ int run_host(int device, const void* x, size_t in_bytes, void* y, size_t out_byt
         (void)hipStreamSynchronize(st->stream);
         return fail(rc, err);
     }
-    HIP_TRY(hipMemcpyAsync(y, st->out.ptr, out_bytes, hipMemcpyDeviceToHost, st->stream));
+    HIP_TRY(hipMemcpyAsync(y, (char*)st->out.ptr + out_skip, out_bytes, hipMemcpyDeviceToHost, st->stream));
     HIP_TRY(hipStreamSynchronize(st->stream));
     return FIR_OK;
 }
@@ -163,6 +170,84 @@ int fir1d_fixed_rows(const void* x, int in_dtype, int64_t rows, int64_t width, i
                             return fir::launch_fir1d_rows(dx, in_dtype, rows, width, channels, hq, taps, frac_bits,
                                                           acc_bits, out_stage, dy, s, err);
                         });
+    } catch (const std::exception& ex) {
+        return fail(FIR_EHIP, std::string("internal error: ") + ex.what());
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int fir1d_fixed_rows_sharded(const void* x, int in_dtype, int64_t rows, int64_t width, int channels,
+                             const int32_t* hq, int taps, int frac_bits, int acc_bits, int out_stage, void* y,
+                             const int* devices, int ndev) {
+    try {
+        if (ndev < 1 || !devices) return fail(FIR_EINVAL, "devices must list ndev >= 1 device ids");
+        int64_t n = 0, rw = 0;
+        if (channels < 1 || !mul_ok(rows, width, &rw) || !mul_ok(rw, channels, &n))
+            return fail(FIR_EINVAL, "invalid rows/width/channels");
+        {
+            std::string err;  // the scalar arguments, once
+            int rc = fir::launch_fir1d_rows(nullptr, in_dtype, 0, 0, channels, hq, taps, frac_bits, acc_bits,
+                                            out_stage, nullptr, nullptr, &err);
+            if (rc) return fail(rc, err);
+        }
+        if (n == 0) return FIR_OK;
+        if (!x || !y) return fail(FIR_EINVAL, "x and y must not be NULL");
+        const size_t isz = in_size(in_dtype), osz = out_size(out_stage);
+        struct Shard {
+            int64_t in0, rows, width;  // launch: rows x width (x channels) samples from sample in0
+            int64_t skip, out0, len;   // copy outputs [skip, skip + len) of the launch to y[out0 ...]
+        };
+        std::map<int, std::vector<Shard>> by_dev;
+        if (rows > 1) {  // independent rows: contiguous row blocks
+            for (int i = 0; i < ndev; ++i) {
+                const int64_t r0 = rows * i / ndev, r1 = rows * (i + 1) / ndev;
+                if (r1 > r0)
+                    by_dev[devices[i]].push_back({r0 * width * channels, r1 - r0, width, 0, r0 * width * channels,
+                                                  (r1 - r0) * width * channels});
+            }
+        } else {  // one row: segments widened by their halos (zero padding only at the row ends)
+            const int64_t hl = taps - 1 - taps / 2, hr = taps / 2;
+            for (int i = 0; i < ndev; ++i) {
+                const int64_t s0 = width * i / ndev, s1 = width * (i + 1) / ndev;
+                if (s1 <= s0) continue;
+                const int64_t a = std::max<int64_t>(0, s0 - hl), b = std::min<int64_t>(width, s1 + hr);
+                by_dev[devices[i]].push_back({a * channels, 1, b - a, (s0 - a) * channels, s0 * channels,
+                                              (s1 - s0) * channels});
+            }
+        }
+        std::vector<std::thread> workers;
+        std::vector<int> rcs(by_dev.size(), FIR_OK);
+        std::vector<std::string> msgs(by_dev.size());
+        size_t wi = 0;
+        for (auto& kv : by_dev) {
+            const int dev = kv.first;
+            const std::vector<Shard>* list = &kv.second;
+            int* rc = &rcs[wi];
+            std::string* msg = &msgs[wi];
+            ++wi;
+            workers.emplace_back([=]() {
+                for (const Shard& sh : *list) {
+                    const int64_t cnt = sh.rows * sh.width * channels;
+                    *rc = run_host(
+                        dev, (const char*)x + sh.in0 * isz, (size_t)cnt * isz, (char*)y + sh.out0 * osz,
+                        (size_t)sh.len * osz,
+                        [&](void* dx, void* dy, hipStream_t s, std::string* err) {
+                            return fir::launch_fir1d_rows(dx, in_dtype, sh.rows, sh.width, channels, hq, taps,
+                                                          frac_bits, acc_bits, out_stage, dy, s, err);
+                        },
+                        (size_t)sh.skip * osz, 0, (size_t)cnt * osz);
+                    if (*rc) {
+                        *msg = g_err;  // thread-local: this worker's message
+                        return;
+                    }
+                }
+            });
+        }
+        for (auto& t : workers) t.join();
+        for (size_t i = 0; i < rcs.size(); ++i)
+            if (rcs[i]) return fail(rcs[i], msgs[i]);
+        return FIR_OK;
     } catch (const std::exception& ex) {
         return fail(FIR_EHIP, std::string("internal error: ") + ex.what());
     } catch (...) {
@@ -337,6 +422,36 @@ int fir_compare_metrics_dev(const double* ideal_dev, const uint8_t* fixed_dev, i
     try {
         std::string err;
         int rc = fir::launch_metrics(ideal_dev, fixed_dev, n, out_dev, work_dev, (hipStream_t)stream, &err);
+        return rc ? fail(rc, err) : FIR_OK;
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int64_t fir_restore_work_bytes(void) { return (int64_t)fir::restore_work_bytes(); }
+
+int fir_restore_u8(const double* a, int64_t n, int policy, uint8_t* out, int device) {
+    try {
+        if (n < 0 || (n > 0 && (!a || !out))) return fail(FIR_EINVAL, "invalid arguments");
+        if (n == 0) {
+            std::string err;
+            int rc = fir::launch_restore_u8(nullptr, 0, policy, nullptr, nullptr, nullptr, &err);
+            return rc ? fail(rc, err) : FIR_OK;
+        }
+        const size_t ab = (size_t)n * 8, wo = (ab + 255) / 256 * 256;
+        // device input = a, then the normalize scratch
+        return run_host(device, a, ab, out, (size_t)n, [&](void* da, void* dout, hipStream_t s, std::string* err) {
+            return fir::launch_restore_u8((const double*)da, n, policy, (uint8_t*)dout, (char*)da + wo, s, err);
+        }, 0, wo + fir::restore_work_bytes());
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int fir_restore_u8_dev(const double* a_dev, int64_t n, int policy, uint8_t* out_dev, void* work_dev, void* stream) {
+    try {
+        std::string err;
+        int rc = fir::launch_restore_u8(a_dev, n, policy, out_dev, work_dev, (hipStream_t)stream, &err);
         return rc ? fail(rc, err) : FIR_OK;
     } catch (...) {
         return fail(FIR_EHIP, "internal error");

@@ -35,4 +35,9 @@ size_t metrics_work_bytes();
 int launch_metrics(const double* ideal, const uint8_t* fixed, int64_t n, double* out, void* work,
                    hipStream_t stream, std::string* err);
 
+// f64 -> u8 restore conversion (FIR_RESTORE_*); `work` >= restore_work_bytes() for normalize.
+size_t restore_work_bytes();
+int launch_restore_u8(const double* a, int64_t n, int policy, uint8_t* out, void* work, hipStream_t stream,
+                      std::string* err);
+
 }  // namespace fir

@@ -2,9 +2,10 @@
 
 Mirror of the reference stage ``fir_1d/sim/vector/restore_images.py`` (same arguments,
 file-name pattern, output sub-directories ``{kind}_{tap}tap[_{policy}]``, skip / strict
-behaviour and summary dict).  PNG encoding is host I/O (Pillow), outside the GPU path;
-the u8 conversions are the reference's: ``clip`` = rint + clip to [0,255] (:51-54),
-``normalize`` = min/max rescale (:57-64); fixed outputs are already uint8.
+behaviour and summary dict).  The u8 conversions run on the GPU (``fir_restore_u8``,
+SURVEY §8(f) 4) with the reference's arithmetic: ``clip`` = rint + clip to [0,255]
+(:51-54), ``normalize`` = min/max rescale (:57-64); fixed outputs are already uint8.
+PNG encoding is host I/O (Pillow).
 """
 from __future__ import annotations
 
@@ -14,6 +15,8 @@ from pathlib import Path
 from typing import Any
 
 import numpy as np
+
+import fir_hip
 
 THIS_FILE = Path(__file__).resolve()
 DEFAULT_VECTOR_OUTPUT_DIR = THIS_FILE.parent / "output"
@@ -26,15 +29,11 @@ FILENAME_RE = re.compile(
 
 
 def _to_u8_clip(a: np.ndarray) -> np.ndarray:
-    return np.clip(np.rint(a), 0, 255).astype(np.uint8)
+    return fir_hip.restore_u8(a, fir_hip.RESTORE_CLIP)
 
 
 def _to_u8_normalized(a: np.ndarray) -> np.ndarray:
-    a = a.astype(np.float64, copy=False)
-    lo, hi = float(a.min()), float(a.max())
-    if hi <= lo:
-        return np.zeros(a.shape, dtype=np.uint8)
-    return np.rint(np.clip((a - lo) * (255.0 / (hi - lo)), 0, 255)).astype(np.uint8)
+    return fir_hip.restore_u8(a, fir_hip.RESTORE_NORMALIZE)
 
 
 def _to_image_u8(a: np.ndarray, kind: str, ideal_policy: str) -> np.ndarray:

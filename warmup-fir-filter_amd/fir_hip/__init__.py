@@ -6,7 +6,8 @@ library is missing, no gfx950 device is present, or a HIP call fails.  There is 
 CPU fallback: the product path fails loudly rather than computing elsewhere.
 
 Host-array entry points (NumPy in, NumPy out, synchronous):
-    fir1d_fixed_rows, fir2d_fixed, fir1d_ideal_rows
+    fir1d_fixed_rows, fir1d_fixed_rows_multi, fir1d_fixed_rows_sharded, fir2d_fixed,
+    fir1d_ideal_rows, compare_metrics, restore_u8
 Device entry points (torch tensors on a HIP device, enqueued on the current stream):
     see :mod:`fir_hip.torch_ops`.
 """
@@ -20,12 +21,14 @@ from pathlib import Path
 import numpy as np
 
 __all__ = [
-    "FirHipError", "lib", "lib_path", "device_count", "fir1d_fixed_rows", "fir1d_fixed_rows_multi", "fir2d_fixed",
-    "fir1d_ideal_rows", "compare_metrics", "IN_U8", "IN_I16", "OUT_U8_SAT", "OUT_I32", "MAX_TAPS", "EXPORTS",
+    "FirHipError", "lib", "lib_path", "device_count", "fir1d_fixed_rows", "fir1d_fixed_rows_multi",
+    "fir1d_fixed_rows_sharded", "fir2d_fixed", "fir1d_ideal_rows", "compare_metrics", "restore_u8", "IN_U8", "IN_I16",
+    "OUT_U8_SAT", "OUT_I32", "RESTORE_CLIP", "RESTORE_NORMALIZE", "MAX_TAPS", "EXPORTS",
 ]
 
 IN_U8, IN_I16 = 0, 1
 OUT_U8_SAT, OUT_I32 = 0, 1
+RESTORE_CLIP, RESTORE_NORMALIZE = 0, 1
 MAX_TAPS = 256
 ABI_VERSION = 1
 
@@ -59,6 +62,10 @@ EXPORTS = {
     "fir_metrics_work_bytes": (_i64, []),
     "fir_compare_metrics": (_i32, [_vp, _vp, _i64, _vp, _i32]),
     "fir_compare_metrics_dev": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp]),
+    "fir1d_fixed_rows_sharded": (_i32, [_vp, _i32, _i64, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _i32]),
+    "fir_restore_work_bytes": (_i64, []),
+    "fir_restore_u8": (_i32, [_vp, _i64, _i32, _vp, _i32]),
+    "fir_restore_u8_dev": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp]),
 }
 
 _lib = None
@@ -142,6 +149,34 @@ def fir1d_fixed_rows(x: np.ndarray, hq, frac_bits: int = 12, acc_bits: int = 32,
     _check(lib().fir1d_fixed_rows(_ptr(x), in_dtype, rows, rowlen // channels, channels, _ptr(h), h.size,
                                   int(frac_bits), int(acc_bits), int(out_stage), _ptr(y), int(device)),
            "fir1d_fixed_rows")
+    return y
+
+
+def fir1d_fixed_rows_sharded(x: np.ndarray, hq, frac_bits: int = 12, acc_bits: int = 32,
+                             out_stage: int = OUT_U8_SAT, channels: int = 1, devices=(0,)) -> np.ndarray:
+    """fir1d_fixed_rows spread over several devices of this process (``devices`` may repeat
+    an id): row blocks for images, halo-widened segments for one long row."""
+    x = np.ascontiguousarray(x)
+    if x.dtype == np.uint8:
+        in_dtype = IN_U8
+    elif x.dtype == np.int16:
+        in_dtype = IN_I16
+    else:
+        raise FirHipError(f"x dtype must be uint8 or int16, got {x.dtype}")
+    h = _taps_i32(hq)
+    devs = np.ascontiguousarray(np.asarray(list(devices), dtype=np.int32).reshape(-1))
+    if devs.size == 0:
+        raise FirHipError("devices must not be empty")
+    if x.ndim == 0:
+        x = x.reshape(1)
+    rowlen = x.shape[-1]
+    rows = x.size // rowlen if rowlen else 0
+    if rowlen % channels:
+        raise FirHipError("row length must be a multiple of channels")
+    y = np.empty(x.shape, dtype=np.uint8 if out_stage == OUT_U8_SAT else np.int32)
+    _check(lib().fir1d_fixed_rows_sharded(_ptr(x), in_dtype, rows, rowlen // channels, channels, _ptr(h), h.size,
+                                          int(frac_bits), int(acc_bits), int(out_stage), _ptr(y), _ptr(devs),
+                                          devs.size), "fir1d_fixed_rows_sharded")
     return y
 
 
@@ -229,3 +264,14 @@ def compare_metrics(y_ideal: np.ndarray, y_fixed: np.ndarray, device: int = 0) -
     out = np.zeros(9, dtype=np.float64)
     _check(lib().fir_compare_metrics(_ptr(yi), _ptr(yf), yi.size, _ptr(out), int(device)), "fir_compare_metrics")
     return metrics_from_sums(out, yi.size)
+
+
+def restore_u8(a: np.ndarray, policy: int = RESTORE_CLIP, device: int = 0) -> np.ndarray:
+    """restore_images._to_u8_clip / _to_u8_normalized (restore_images.py:51-64) on the GPU;
+    same shape, uint8."""
+    arr = np.ascontiguousarray(a, dtype=np.float64)
+    if policy == RESTORE_NORMALIZE and arr.size == 0:
+        raise ValueError("zero-size array to reduction operation minimum which has no identity")
+    out = np.empty(arr.shape, dtype=np.uint8)
+    _check(lib().fir_restore_u8(_ptr(arr), arr.size, int(policy), _ptr(out), int(device)), "fir_restore_u8")
+    return out

@@ -11,7 +11,8 @@ import ctypes
 import numpy as np
 import torch
 
-from . import IN_I16, IN_U8, OUT_I32, OUT_U8_SAT, FirHipError, _check, _taps_i32, lib
+from . import (IN_I16, IN_U8, OUT_I32, OUT_U8_SAT, RESTORE_CLIP, RESTORE_NORMALIZE, FirHipError, _check, _taps_i32,
+               lib)
 
 _IN = {torch.uint8: IN_U8, torch.int16: IN_I16}
 _OUT_DTYPE = {OUT_U8_SAT: torch.uint8, OUT_I32: torch.int32}
@@ -148,4 +149,21 @@ def fir1d_ideal_rows_dev(x: torch.Tensor, h, out: torch.Tensor | None = None, st
     _check(lib().fir1d_ideal_rows_dev(ctypes.c_void_p(x.data_ptr()), rows, width, hh.ctypes.data_as(ctypes.c_void_p),
                                       hh.size, ctypes.c_void_p(out.data_ptr()), _stream_ptr(x, stream)),
            "fir1d_ideal_rows_dev")
+    return out
+
+
+def restore_u8_dev(a: torch.Tensor, policy: int = RESTORE_CLIP, out: torch.Tensor | None = None,
+                   work: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """f64 -> u8 restore conversion of a device tensor (restore_images.py:51-64)."""
+    _check_dev(a, "a")
+    if a.dtype != torch.float64:
+        raise FirHipError("a must be float64")
+    if out is None:
+        out = torch.empty(a.shape, dtype=torch.uint8, device=a.device)
+    _check_dev(out, "out")
+    if policy == RESTORE_NORMALIZE and work is None:
+        work = torch.empty(int(lib().fir_restore_work_bytes()), dtype=torch.uint8, device=a.device)
+    wp = ctypes.c_void_p(work.data_ptr()) if work is not None else None
+    _check(lib().fir_restore_u8_dev(ctypes.c_void_p(a.data_ptr()), a.numel(), int(policy),
+                                    ctypes.c_void_p(out.data_ptr()), wp, _stream_ptr(a, stream)), "fir_restore_u8_dev")
     return out
