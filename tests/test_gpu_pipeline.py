@@ -107,9 +107,15 @@ def test_pipeline_restore_small_images(tmp_path, images):
 
     want = np.load(GOLDEN / "restore_u8.npz")
     small_out = np.load(GOLDEN / "small_image_outputs.npz")
+
+    def golden_key(files, png_name, tail):  # the pipeline renumbers cases: match past "case_NNN_"
+        body = png_name.replace(tail, "").split("_", 2)[2]
+        (key,) = [k for k in files if k.startswith("case_") and k.split("_", 2)[2] == body]
+        return key
+
     for png in (tmp_path / "img" / "ideal_5tap_normalize").glob("*.png"):
-        key = png.name.replace("_y_f64.png", "")
+        key = golden_key([k[:-4] for k in want.files if k.endswith("__in")], png.name, "_y_f64.png")
         assert np.array_equal(np.asarray(Image.open(png)), want[key + "__normalize"]), png.name
     for png in (tmp_path / "img" / "fixed_5tap").glob("*.png"):
-        key = png.name.replace("_y_u8.png", "")
+        key = golden_key(small_out.files, png.name, "_y_u8.png")
         assert np.array_equal(np.asarray(Image.open(png)), small_out[key]), png.name
