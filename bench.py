@@ -314,7 +314,7 @@ def main() -> int:
             f = torch.tensor([0 if ok else 1], device=red_dev)
             dist.all_reduce(f, op=dist.ReduceOp.MAX)
             ok = int(f.item()) == 0
-        parity = "bit-exact vs C oracle (full output, every rank)" if ok else "MISMATCH"
+        parity = "bit-exact vs oracle (full output, every rank)" if ok else "MISMATCH"
 
     cpu = cpu_np = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
