@@ -19,9 +19,10 @@ prints ONE JSON line.  Extra keys:
 Other workloads: `cplx_i16` / `fir2d_u8` measure configs[2] / configs[4]; `fir1d_u8` the
 reference's own u8 -> sat-u8 golden path (a1/a4) at scale; `ideal_u8` (the f64
 ideal model), `bank_u8` (the fused 4-filter 3-tap bank, §8(f) 3) and
-`restore_u8` (the f64 -> u8 clip conversion, §8(f) 4) measure the next rows on 2^28 samples in
-4096-sample rows (the reference's image-row layout).  For workloads without a C oracle leg
-(restore_u8) cpu_baseline times the NumPy restatement.
+`restore_u8` (the f64 -> u8 clip conversion, §8(f) 4) and `metrics_u8` (the report's
+_compute_metrics, §8(f) 2) measure the next rows on 2^28 samples (4096-sample rows for the
+image workloads, the reference's row layout).  For workloads without a C oracle leg
+(restore_u8, metrics_u8) cpu_baseline times the NumPy restatement.
 """
 from __future__ import annotations
 
@@ -55,7 +56,8 @@ BANK3 = [[1365] * 3, [1024, 2048, 1024], [-4096, 0, 4096], [-512, 5120, -512]]  
 ROW_W = 4096
 KERNELS = {"fir1d_i16": "fir1d_reg_kernel", "cplx_i16": "fir1d_reg_kernel", "fir2d_u8": "fir2d_reg_kernel",
            "fir1d_u8": "fir1d_reg_kernel", "ideal_u8": "fir1d_ideal_kernel", "bank_u8": "fir1d_reg_kernel",
-           "restore_u8": "restore_map_kernel"}
+           "restore_u8": "restore_map_kernel", "metrics_u8": "metrics_pass1+2"}
+NUMPY_ONLY = ("restore_u8", "metrics_u8")  # no C oracle leg: the NumPy restatement is the CPU baseline
 
 
 def _env_int(name: str, default: int) -> int:
@@ -140,6 +142,18 @@ class Workload:
             self.dtype = "f64 in, u8 out (rint, clip)"
             self.config = {"workload": "restore_f64_to_u8_clip_rows4096", "samples_per_gpu": self.n,
                            "parallelism": "single GPU (replicas when N > 1)"}
+        elif name == "metrics_u8":
+            self.n = 1 << log2n
+            self.x_host = rng.uniform(-64.0, 320.0, self.n)  # ideal-output-like f64
+            self.fixed_host = np.clip(np.rint(self.x_host) + rng.integers(-3, 4, self.n), 0, 255).astype(np.uint8)
+            self.fixed = torch.from_numpy(self.fixed_host).to(dev)
+            self.work = torch.empty(int(fir_hip.lib().fir_metrics_work_bytes()), dtype=torch.uint8, device=dev)
+            self.units = self.n
+            self.unit = "Gsamples/s"
+            self.bytes_per_unit = 8 + 1
+            self.dtype = "f64 (Neumaier-compensated sums; counts and max exact)"
+            self.config = {"workload": "compare_metrics_f64_u8", "samples_per_gpu": self.n,
+                           "parallelism": "single GPU (replicas when N > 1)"}
         else:
             raise SystemExit(f"unknown workload {name}")
         self.x = torch.from_numpy(self.x_host).to(dev)
@@ -149,6 +163,8 @@ class Workload:
             self.y = torch.empty((len(BANK3),) + tuple(self.x.shape), dtype=torch.uint8, device=dev)
         elif name == "restore_u8":
             self.y = torch.empty(self.x.shape, dtype=torch.uint8, device=dev)
+        elif name == "metrics_u8":
+            self.y = torch.empty(9, dtype=torch.float64, device=dev)
         else:
             u8 = name in ("fir2d_u8", "fir1d_u8")
             self.y = torch.empty(self.x.shape, dtype=torch.uint8 if u8 else torch.int32, device=dev)
@@ -169,6 +185,8 @@ class Workload:
             torch_ops.fir1d_fixed_rows_dev(self.x, self.taps, 12, 32, fir_hip.OUT_U8_SAT, out=self.y)
         elif self.name == "restore_u8":
             torch_ops.restore_u8_dev(self.x, fir_hip.RESTORE_CLIP, out=self.y)
+        elif self.name == "metrics_u8":
+            torch_ops.compare_metrics_dev(self.x, self.fixed, out=self.y, work=self.work)
         else:
             torch_ops.fir1d_fixed_rows_dev(self.x, self.taps, 12, 32, fir_hip.OUT_I32, self.channels, out=self.y)
 
@@ -203,6 +221,10 @@ class Workload:
                 from oracle import fir_oracle as fo
 
                 out = fo.to_u8_clip(self.x_host)
+            elif self.name == "metrics_u8":
+                from oracle import fir_oracle as fo
+
+                out = fo.compute_metrics(self.x_host, self.fixed_host)
             else:
                 hl = None if self.left is None else self.left.cpu().numpy()
                 hr = None if self.right is None else self.right.cpu().numpy()
@@ -218,6 +240,10 @@ class Workload:
             rows = max(1, min(self.h, max_units // self.w))
             fo.fir2d_fixed(self.x_host[:rows], self.hq2, 12, 32, fo.OUT_U8_SAT)
             return rows * self.w
+        if self.name == "metrics_u8":
+            m = min(self.n, max_units)
+            fo.compute_metrics(self.x_host[:m], self.fixed_host[:m])
+            return m
         if self.name in ("ideal_u8", "bank_u8", "fir1d_u8", "restore_u8"):
             rows = max(1, min(self.x_host.shape[0], max_units // ROW_W))
             if self.name == "restore_u8":
@@ -233,6 +259,16 @@ class Workload:
         n = min(self.units, max_units)
         fo.fir1d_i16_i32(self.x_host[:n * self.channels], self.taps.h, 12, 32, channels=self.channels)
         return n
+
+    def matches(self, ref) -> bool:
+        """Full-output parity; the metrics' float sums to 1e-12 relative (counts, max exact)."""
+        got = self.y.cpu().numpy()
+        if self.name != "metrics_u8":
+            return bool(np.array_equal(got, ref))
+        m = fir_hip.metrics_from_sums(got, self.n)
+        exact = ("num_samples", "max_abs_err", "sat_low_ratio", "sat_high_ratio", "sat_ratio", "clip_needed_ratio")
+        return all(m[k] == ref[k] for k in exact) and all(
+            abs(m[k] - ref[k]) <= 1e-12 * abs(ref[k]) + 1e-15 for k in ("mae", "rmse", "mean_err"))
 
 
 def main() -> int:
@@ -309,7 +345,7 @@ def main() -> int:
     parity = "skipped"
     if not args.no_parity:
         ref = wl.oracle(_cpu_threads())
-        ok = bool(np.array_equal(wl.y.cpu().numpy(), ref))
+        ok = wl.matches(ref)
         if world > 1:
             f = torch.tensor([0 if ok else 1], device=red_dev)
             dist.all_reduce(f, op=dist.ReduceOp.MAX)
@@ -327,7 +363,7 @@ def main() -> int:
             if time.perf_counter() - tc0 >= args.cpu_seconds:
                 break
         tc = time.perf_counter() - tc0
-        np_only = args.workload == "restore_u8"  # no C leg: the NumPy restatement, one thread
+        np_only = args.workload in NUMPY_ONLY
         what = "NumPy restatement (oracle/fir_oracle.py)" if np_only else \
             f"C oracle (oracle/fir_oracle.c, OpenMP {nthr} threads)"
         cpu = {"value": round(wl.units * reps / tc / 1e9, 4), "unit": wl.unit, "cores": 1 if np_only else nthr,

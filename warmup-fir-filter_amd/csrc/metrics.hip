@@ -4,10 +4,11 @@
 // d = fixed - ideal (float64), it needs max|d|, sum|d|, sum d^2, sum d, #(fixed == 0),
 // #(fixed == 255) and #(ideal < 0 or ideal > 255).  The reference takes each from a
 // separate NumPy reduction (seven passes over 9 bytes/sample); here one kernel reads
-// each sample once.  Sums are float64 with Neumaier compensation per thread and a fixed
-// reduction order (per-block tree, then one block over the partials), so results are
-// deterministic run to run; they differ from NumPy's pairwise summation only in the last
-// bits (tests use a 1e-12 relative tolerance).  Counts and max|d| are exact.
+// each sample once.  Sums are float64: plain per 8-sample tile, Neumaier-compensated across
+// tiles per thread, then a fixed reduction order (per-block tree, then one block over the
+// partials), so results are deterministic run to run; they differ from NumPy's pairwise
+// summation only in the last bits (tests use a 1e-12 relative tolerance).  Counts and
+// max|d| are exact.
 #include <string>
 
 #include "fir_common.h"
@@ -15,7 +16,7 @@
 
 namespace fir {
 
-constexpr int kMetricBlocks = 1024;
+constexpr int kMetricBlocks = 4096;
 
 struct Part {
     double sabs, cabs, ssq, csq, sd, cd, mx;
@@ -52,24 +53,74 @@ __device__ void reduce_block(Part& p) {
     p = sh[0];
 }
 
+// One sample's terms: |d| and d^2 and d into the tile partials, max and the three counts.
+__device__ __forceinline__ void metrics_term(double id, uint32_t fx, double& sabs, double& ssq, double& sd,
+                                             double& mx, uint32_t& lo, uint32_t& hi, uint32_t& clip) {
+    const double d = __dsub_rn((double)fx, id);
+    const double ad = fabs(d);
+    sabs = __dadd_rn(sabs, ad);
+    ssq = __dadd_rn(ssq, __dmul_rn(d, d));
+    sd = __dadd_rn(sd, d);
+    mx = fmax(mx, ad);
+    lo += fx == 0;
+    hi += fx == 255;
+    clip += (id < 0.0) | (id > 255.0);
+}
+
+// VEC (ideal 16-byte and fixed 2-byte aligned): a wave reads tiles of kMetricTile samples as
+// whole 1 KiB f64 rows plus 128 B u8 rows; each lane sums its 8 samples of a tile plainly
+// and adds the tile partials into its Neumaier-compensated accumulators (the compensated
+// add per sample made the kernel latency-bound).  The ragged tail and unaligned inputs take
+// the per-sample grid-stride loop.
+constexpr int kMetricTile = 4 * kWave * 2;
+
+template <bool VEC>
 __global__ __launch_bounds__(kBlock) void metrics_pass1(const double* __restrict__ ideal,
                                                         const uint8_t* __restrict__ fixed, int64_t n,
                                                         Part* __restrict__ parts) {
+    typedef double d2 __attribute__((ext_vector_type(2)));
     Part p{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-        const double id = ideal[i];
-        const uint8_t fx = fixed[i];
-        const double d = __dsub_rn((double)fx, id);
-        const double ad = fabs(d);
-        neu_add(p.sabs, p.cabs, ad);
-        neu_add(p.ssq, p.csq, __dmul_rn(d, d));
-        neu_add(p.sd, p.cd, d);
-        p.mx = fmax(p.mx, ad);
-        p.lo += fx == 0;
-        p.hi += fx == 255;
-        p.clip += (id < 0.0) | (id > 255.0);
+    double mx = 0.0;
+    uint32_t lo = 0, hi = 0, clip = 0;
+    int64_t start = 0;
+    if constexpr (VEC) {
+        const int lane = threadIdx.x & (kWave - 1);
+        const int64_t ntile = n / kMetricTile;
+        const int64_t nwaves = (int64_t)gridDim.x * (kBlock / kWave);
+        for (int64_t t = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6); t < ntile; t += nwaves) {
+            const d2* pi = reinterpret_cast<const d2*>(ideal + t * kMetricTile);
+            const uint16_t* pf = reinterpret_cast<const uint16_t*>(fixed + t * kMetricTile);
+            d2 a[4];
+            uint32_t f[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                a[i] = pi[i * kWave + lane];
+                f[i] = pf[i * kWave + lane];
+            }
+            double sabs = 0.0, ssq = 0.0, sd = 0.0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                metrics_term(a[i].x, f[i] & 0xFFu, sabs, ssq, sd, mx, lo, hi, clip);
+                metrics_term(a[i].y, f[i] >> 8, sabs, ssq, sd, mx, lo, hi, clip);
+            }
+            neu_add(p.sabs, p.cabs, sabs);
+            neu_add(p.ssq, p.csq, ssq);
+            neu_add(p.sd, p.cd, sd);
+        }
+        start = ntile * kMetricTile;
     }
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = start + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        double sabs = 0.0, ssq = 0.0, sd = 0.0;
+        metrics_term(ideal[i], fixed[i], sabs, ssq, sd, mx, lo, hi, clip);
+        neu_add(p.sabs, p.cabs, sabs);
+        neu_add(p.ssq, p.csq, ssq);
+        neu_add(p.sd, p.cd, sd);
+    }
+    p.mx = mx;
+    p.lo = lo;
+    p.hi = hi;
+    p.clip = clip;
     reduce_block(p);
     if (threadIdx.x == 0) parts[blockIdx.x] = p;
 }
@@ -113,7 +164,10 @@ int launch_metrics(const double* ideal, const uint8_t* fixed, int64_t n, double*
     if (!out || !work || (n > 0 && (!ideal || !fixed))) return *err = "null pointer argument", FIR_EINVAL;
     int64_t want = (n + kBlock - 1) / kBlock;
     const int blocks = (int)(want < 1 ? 1 : (want > kMetricBlocks ? kMetricBlocks : want));
-    hipLaunchKernelGGL(metrics_pass1, dim3(blocks), dim3(kBlock), 0, stream, ideal, fixed, n, (Part*)work);
+    if ((uintptr_t)ideal % 16 == 0 && (uintptr_t)fixed % 2 == 0)
+        hipLaunchKernelGGL(metrics_pass1<true>, dim3(blocks), dim3(kBlock), 0, stream, ideal, fixed, n, (Part*)work);
+    else
+        hipLaunchKernelGGL(metrics_pass1<false>, dim3(blocks), dim3(kBlock), 0, stream, ideal, fixed, n, (Part*)work);
     hipLaunchKernelGGL(metrics_pass2, dim3(1), dim3(kBlock), 0, stream, (const Part*)work, blocks, n, out);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return *err = std::string("metrics launch failed: ") + hipGetErrorString(e), FIR_EHIP;

@@ -167,3 +167,22 @@ def restore_u8_dev(a: torch.Tensor, policy: int = RESTORE_CLIP, out: torch.Tenso
     _check(lib().fir_restore_u8_dev(ctypes.c_void_p(a.data_ptr()), a.numel(), int(policy),
                                     ctypes.c_void_p(out.data_ptr()), wp, _stream_ptr(a, stream)), "fir_restore_u8_dev")
     return out
+
+
+def compare_metrics_dev(ideal: torch.Tensor, fixed: torch.Tensor, out: torch.Tensor | None = None,
+                        work: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """The 9 report sums of _compute_metrics (gen_3tap_compare_report.py:67-112) of device
+    tensors, into a float64 device tensor of 9 (see fir_hip.metrics_from_sums)."""
+    _check_dev(ideal, "ideal")
+    _check_dev(fixed, "fixed")
+    if ideal.dtype != torch.float64 or fixed.dtype != torch.uint8 or ideal.shape != fixed.shape:
+        raise FirHipError("ideal must be float64 and fixed uint8 of the same shape")
+    if out is None:
+        out = torch.empty(9, dtype=torch.float64, device=ideal.device)
+    if work is None:
+        work = torch.empty(int(lib().fir_metrics_work_bytes()), dtype=torch.uint8, device=ideal.device)
+    _check(lib().fir_compare_metrics_dev(ctypes.c_void_p(ideal.data_ptr()), ctypes.c_void_p(fixed.data_ptr()),
+                                         ideal.numel(), ctypes.c_void_p(out.data_ptr()),
+                                         ctypes.c_void_p(work.data_ptr()), _stream_ptr(ideal, stream)),
+           "fir_compare_metrics_dev")
+    return out
