@@ -65,48 +65,59 @@ int oracle_fir1d_rows(const void* x, int in_dtype, int64_t rows, int64_t width, 
 #else
     (void)nthreads;
 #endif
-    /* fast path for the benchmark shape: int16 -> int32, 32-bit wrap, interior samples */
-    const int fast = (in_dtype == OR_IN_I16 && out_stage == OR_OUT_I32 && acc_bits == 32 &&
-                      frac_bits >= 1 && frac_bits <= 31 && L <= 64);
-    for (int64_t r = 0; r < rows; ++r) {
+    /* fast path (acc_bits == 32): interior outputs in vectorisable uint32 wrap-around
+     * arithmetic (exact mod 2^32, which is all the 32-bit wrap needs) */
+    const int fast = (acc_bits == 32 && frac_bits >= 1 && frac_bits <= 31 && L <= 64);
+    const int64_t nblk = (width + 4095) / 4096;
+    /* one parallel loop over (row, 4096-output block) so narrow rows parallelise too */
+#pragma omp parallel for schedule(static)
+    for (int64_t t = 0; t < rows * nblk; ++t) {
+        const int64_t r = t / nblk, blk = t % nblk;
         const int64_t base = r * rowlen;
         const int64_t lo = (int64_t)HL, hi = width - c; /* outputs with no padding */
-#pragma omp parallel for schedule(static)
-        for (int64_t blk = 0; blk < (width + 4095) / 4096; ++blk) {
-            const int64_t n0 = blk * 4096;
-            const int64_t n1 = n0 + 4096 < width ? n0 + 4096 : width;
-            for (int64_t n = n0; n < n1; ++n) {
-                if (fast && n >= lo && n < hi) {
-                    /* contiguous interior run: vectorisable uint32 wrap-around arithmetic */
-                    const int64_t run_end = hi < n1 ? hi : n1;
-                    const int16_t* xs = (const int16_t*)x;
-                    int32_t* ys = (int32_t*)y;
-                    for (int64_t m = n * channels; m < run_end * channels; ++m) {
+        const int64_t n0 = blk * 4096;
+        const int64_t n1 = n0 + 4096 < width ? n0 + 4096 : width;
+        for (int64_t n = n0; n < n1; ++n) {
+            if (fast && n >= lo && n < hi) {
+                const int64_t run_end = hi < n1 ? hi : n1;
+                const int64_t m0 = n * channels, m1 = run_end * channels;
+                if (in_dtype == OR_IN_I16) {
+                    const int16_t* xs = (const int16_t*)x + base;
+                    for (int64_t m = m0; m < m1; ++m) {
                         uint32_t a = 0;
                         for (int k = 0; k < L; ++k)
-                            a += (uint32_t)hq[k] * (uint32_t)(int32_t)xs[base + m + (int64_t)(c - k) * channels];
+                            a += (uint32_t)hq[k] * (uint32_t)(int32_t)xs[m + (int64_t)(c - k) * channels];
                         const int32_t s = (int32_t)a;
-                        ys[base + m] = (s >> frac_bits) + ((s >> (frac_bits - 1)) & 1);
+                        store_out(y, out_stage, base + m, (s >> frac_bits) + ((s >> (frac_bits - 1)) & 1));
                     }
-                    n = run_end - 1;
-                    continue;
-                }
-                for (int ch = 0; ch < channels; ++ch) {
-                    int64_t acc = 0;
-                    for (int k = 0; k < L; ++k) {
-                        const int64_t idx = n - k + c;
-                        int64_t v = 0;
-                        if (idx >= 0 && idx < width) {
-                            v = load_sample(x, in_dtype, base + idx * channels + ch);
-                        } else if (idx < 0 && halo_left) {
-                            v = load_sample(halo_left, in_dtype, (HL + idx) * channels + ch);
-                        } else if (idx >= width && halo_right) {
-                            v = load_sample(halo_right, in_dtype, (idx - width) * channels + ch);
-                        }
-                        acc += (int64_t)hq[k] * v;
+                } else {
+                    const uint8_t* xs = (const uint8_t*)x + base;
+                    for (int64_t m = m0; m < m1; ++m) {
+                        uint32_t a = 0;
+                        for (int k = 0; k < L; ++k)
+                            a += (uint32_t)hq[k] * (uint32_t)xs[m + (int64_t)(c - k) * channels];
+                        const int32_t s = (int32_t)a;
+                        store_out(y, out_stage, base + m, (s >> frac_bits) + ((s >> (frac_bits - 1)) & 1));
                     }
-                    store_out(y, out_stage, base + n * channels + ch, wrap_round(acc, frac_bits, acc_bits));
                 }
+                n = run_end - 1;
+                continue;
+            }
+            for (int ch = 0; ch < channels; ++ch) {
+                int64_t acc = 0;
+                for (int k = 0; k < L; ++k) {
+                    const int64_t idx = n - k + c;
+                    int64_t v = 0;
+                    if (idx >= 0 && idx < width) {
+                        v = load_sample(x, in_dtype, base + idx * channels + ch);
+                    } else if (idx < 0 && halo_left) {
+                        v = load_sample(halo_left, in_dtype, (HL + idx) * channels + ch);
+                    } else if (idx >= width && halo_right) {
+                        v = load_sample(halo_right, in_dtype, (idx - width) * channels + ch);
+                    }
+                    acc += (int64_t)hq[k] * v;
+                }
+                store_out(y, out_stage, base + n * channels + ch, wrap_round(acc, frac_bits, acc_bits));
             }
         }
     }
