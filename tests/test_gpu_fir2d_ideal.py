@@ -66,6 +66,30 @@ def test_fir2d_wrap_and_bit_widths():
         assert np.array_equal(fir_hip.fir2d_fixed(x, hq, frac, acc, 1), co.fir2d(x, hq, frac, acc, 1))
 
 
+SEP_KERNELS = [  # (col, row): rank-1 kernels reaching each separable variant
+    ([16, 64, 96, 64, 16], [1, 4, 6, 4, 1]),            # int16 row sums, no wrap (the bench kernel)
+    ([-3, 7, 11, 7, -3], [2, -5, 9, -5, 2]),            # signed, int16 row sums
+    ([1, 2, 1], [1000, -3000, 1000]),                   # row sums beyond int16: 32-bit column pass
+    ([3, -1, 3], [200, 300, -100, 300, 200]),          # 32-bit column pass, 3x5
+    ([127] * 5, [255, 255, 255]),                       # near-int16 taps; wraps at acc_bits = 24
+    ([40000, -1, 3], [1, 1, 1]),                        # taps beyond int16: generic kernel
+]
+
+
+@pytest.mark.parametrize("k", range(len(SEP_KERNELS)))
+@pytest.mark.parametrize("shape", [(1, 16), (29, 64), (64, 1280), (300, 4096 + 16)])
+def test_fir2d_separable_variants_vs_oracle(k, shape):
+    col, row = SEP_KERNELS[k]
+    hq = np.outer(np.array(col, np.int64), np.array(row, np.int64))
+    rng = np.random.default_rng(k * 7 + shape[0])
+    x = rng.integers(0, 256, shape, dtype=np.uint8)
+    co = c_oracle()
+    for frac, acc in ((12, 32), (8, 24), (16, 32)):
+        for stage in (fir_hip.OUT_U8_SAT, fir_hip.OUT_I32):
+            assert np.array_equal(fir_hip.fir2d_fixed(x, hq, frac, acc, stage),
+                                  co.fir2d(x, hq, frac, acc, stage)), (frac, acc, stage)
+
+
 def test_fir2d_full_frame_8192():
     """BASELINE configs[4]: 8192 x 8192 u8 frame, 5x5 unity-gain kernel."""
     x = np.random.default_rng(20260227).integers(0, 256, (8192, 8192), dtype=np.uint8)

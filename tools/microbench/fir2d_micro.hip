@@ -36,6 +36,8 @@ static void launch(const uint8_t* x, uint8_t* y, int64_t H, int64_t W, hipStream
     for (int m = 0; m < 5; ++m) t.col[m] = g_col[m];
     for (int p = 0; p < 3; ++p)
         t.rowp[p] = ((uint32_t)g_row[4 - 2 * p] & 0xFFFFu) | ((uint32_t)(3 - 2 * p >= 0 ? g_row[3 - 2 * p] : 0) << 16);
+    for (int p = 0; p < 3; ++p)
+        t.colp[p] = ((uint32_t)g_col[2 * p] & 0xFFFFu) | ((uint32_t)(2 * p + 1 < 5 ? g_col[2 * p + 1] : 0) << 16);
     const dim3 grid = fir2d_reg_grid<VEC, STRIP>(H, W);
     hipLaunchKernelGGL((fir2d_reg_kernel<5, 5, FIR_OUT_U8_SAT, VEC, STRIP, MODE>), grid, dim3(kBlock), 0, s, x, y, H,
                        W, t, 0, 12);
@@ -70,13 +72,14 @@ int main(int argc, char** argv) {
     hipStream_t st;
     CK(hipStreamCreate(&st));
     std::vector<V> vs = {
-        {"dot2 vec16 strip8", launch<16, 8, kMode2dDot2>, {}},
         {"dot2+nowrap vec16 s8", launch<16, 8, kMode2dDot2 | kMode2dNoWrap>, {}},
-        {"sep vec16 strip8", launch<16, 8, kMode2dSep>, {}},
-        {"sep+nowrap vec16 s8", launch<16, 8, kMode2dSep | kMode2dNoWrap>, {}},
+        {"sep vec16 s16", launch<16, 16, kMode2dSep>, {}},
         {"sep+nowrap vec16 s16", launch<16, 16, kMode2dSep | kMode2dNoWrap>, {}},
-        {"sep+nowrap vec8 s16", launch<8, 16, kMode2dSep | kMode2dNoWrap>, {}},
-        {"sep+nowrap vec8 s8", launch<8, 8, kMode2dSep | kMode2dNoWrap>, {}},
+        {"sep16 vec16 s16", launch<16, 16, kMode2dSep | kMode2dSep16>, {}},
+        {"sep16+nowrap vec16 s16", launch<16, 16, kMode2dSep | kMode2dSep16 | kMode2dNoWrap>, {}},
+        {"sep16+nowrap vec16 s8", launch<16, 8, kMode2dSep | kMode2dSep16 | kMode2dNoWrap>, {}},
+        {"sep16+nowrap vec8 s16", launch<8, 16, kMode2dSep | kMode2dSep16 | kMode2dNoWrap>, {}},
+        {"sep16+nowrap vec16 s24", launch<16, 24, kMode2dSep | kMode2dSep16 | kMode2dNoWrap>, {}},
     };
     auto ref = [&](int64_t i, int64_t j) {
         uint32_t a = 0;

@@ -1,0 +1,136 @@
+// fir_u8_micro.hip — A/B microbenchmark for the 1:1 u8 -> sat-u8 path (dev tool, not the
+// product): fir1d_reg_kernel<u8, U8_SAT, 5> with U chunks per wave over 2^28 samples in
+// 4096-sample rows, next to plain 16-byte copies with the same layouts and hipMemcpy.
+// Every FIR variant's full output is checked against a CPU evaluation.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "fir1d_reg.h"
+
+using namespace fir;
+
+#define CK(e)                                                                              \
+    do {                                                                                   \
+        hipError_t _e = (e);                                                               \
+        if (_e != hipSuccess) {                                                            \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #e, hipGetErrorString(_e)); \
+            exit(1);                                                                       \
+        }                                                                                  \
+    } while (0)
+
+static const int32_t kTaps[5] = {-256, -1024, 6656, -1024, -256};
+static const int64_t kW = 4096;
+
+template <int U, int FLAGS>
+static void launch_fir(const uint8_t* x, uint8_t* y, int64_t n, hipStream_t s) {
+    RowGeom g{n, (uint32_t)kW, 1, 1};
+    TapsN<5> t;
+    for (int k = 0; k < 5; ++k) t.h[0][k] = kTaps[k];
+    pack_taps(t);
+    int64_t ntiles, blocks;
+    reg_launch_geometry<uint8_t, U, FLAGS>(n, 2048, &ntiles, &blocks);
+    hipLaunchKernelGGL((fir1d_reg_kernel<uint8_t, FIR_OUT_U8_SAT, 5, 1, U, FLAGS>), dim3((unsigned)blocks),
+                       dim3(kBlock), 0, s, x, y, g, t, 0, 12, ntiles);
+}
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void copy16(const uint8_t* __restrict__ x, uint8_t* __restrict__ y, int64_t nvec) {
+    typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x & 63;
+    const int64_t w = ((int64_t)blockIdx.x * kBlock + threadIdx.x - lane) * U;  // wave's first vector
+    v4 d[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) d[u] = reinterpret_cast<const v4*>(x)[w + u * 64 + lane];
+#pragma unroll
+    for (int u = 0; u < U; ++u) reinterpret_cast<v4*>(y)[w + u * 64 + lane] = d[u];
+}
+template <int U>
+static void launch_copy(const uint8_t* x, uint8_t* y, int64_t n, hipStream_t s) {
+    const int64_t nvec = n / 16;
+    hipLaunchKernelGGL((copy16<U>), dim3((unsigned)(nvec / U / kBlock)), dim3(kBlock), 0, s, x, y, nvec);
+}
+
+static void launch_memcpy(const uint8_t* x, uint8_t* y, int64_t n, hipStream_t s) {
+    CK(hipMemcpyAsync(y, x, n, hipMemcpyDeviceToDevice, s));
+}
+
+struct V {
+    std::string name;
+    bool fir;
+    void (*fn)(const uint8_t*, uint8_t*, int64_t, hipStream_t);
+    std::vector<float> us;
+};
+
+int main(int argc, char** argv) {
+    const int rounds = argc > 1 ? atoi(argv[1]) : 15;
+    const int64_t n = (int64_t)1 << 28;
+    std::vector<uint8_t> hx(n), ref(n), got(n);
+    uint64_t s = 88172645463325252ull;
+    for (auto& v : hx) {
+        s ^= s << 13, s ^= s >> 7, s ^= s << 17;
+        v = (uint8_t)s;
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t r = i / kW, c = i % kW;
+        int64_t acc = 0;
+        for (int k = 0; k < 5; ++k) {
+            const int64_t j = c - k + 2;
+            if (j >= 0 && j < kW) acc += (int64_t)kTaps[k] * hx[r * kW + j];
+        }
+        const int64_t q = (acc + 2048) >> 12;
+        ref[i] = (uint8_t)(q < 0 ? 0 : q > 255 ? 255 : q);
+    }
+    uint8_t *dx, *dy;
+    CK(hipMalloc(&dx, n));
+    CK(hipMalloc(&dy, n));
+    CK(hipMemcpy(dx, hx.data(), n, hipMemcpyHostToDevice));
+    hipStream_t st;
+    CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    std::vector<V> vs = {{"fir U1", true, launch_fir<1, kU8Dot2>, {}},
+                         {"fir U2", true, launch_fir<2, kU8Dot2>, {}},
+                         {"fir U4", true, launch_fir<4, kU8Dot2>, {}},
+                         {"fir U1 persist", true, launch_fir<1, kU8Dot2 | kPersist>, {}},
+                         {"copy16 U1", false, launch_copy<1>, {}},
+                         {"copy16 U2", false, launch_copy<2>, {}},
+                         {"copy16 U4", false, launch_copy<4>, {}},
+                         {"hipMemcpy D2D", false, launch_memcpy, {}}};
+    for (auto& v : vs) {
+        if (!v.fir) continue;
+        CK(hipMemset(dy, 0x5A, n));
+        v.fn(dx, dy, n, st);
+        CK(hipStreamSynchronize(st));
+        CK(hipMemcpy(got.data(), dy, n, hipMemcpyDeviceToHost));
+        int64_t bad = 0;
+        for (int64_t i = 0; i < n; ++i) bad += got[i] != ref[i];
+        printf("check %-16s %s (%lld bad)\n", v.name.c_str(), bad ? "FAIL" : "ok", (long long)bad);
+        if (bad) return 1;
+    }
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int w = 0; w < 80; ++w) vs[w % vs.size()].fn(dx, dy, n, st);
+    const int batch = 20;
+    for (int r = 0; r < rounds; ++r)
+        for (auto& v : vs) {
+            CK(hipEventRecord(e0, st));
+            for (int b = 0; b < batch; ++b) v.fn(dx, dy, n, st);
+            CK(hipEventRecord(e1, st));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            v.us.push_back(ms * 1e3f / batch);
+        }
+    printf("%-20s %10s %10s %10s %8s\n", "variant", "median_us", "min_us", "GB/s", "%8TB/s");
+    for (auto& v : vs) {
+        std::sort(v.us.begin(), v.us.end());
+        const double med = v.us[v.us.size() / 2];
+        printf("%-20s %10.1f %10.1f %10.1f %8.1f\n", v.name.c_str(), med, v.us[0], 2.0 * n / med / 1e3,
+               2.0 * n / med / 1e3 / 80.0);
+    }
+    return 0;
+}

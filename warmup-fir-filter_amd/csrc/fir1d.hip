@@ -6,7 +6,7 @@
 //
 // Two kernels:
 //  * fir1d_reg_kernel (fir1d_reg.h) — the hot path.  A lane owns one 16-byte vector of
-//    samples (16 u8 or 8 int16); a wave owns kRegU chunks of 64 vectors (1 KiB per load
+//    samples (16 u8 or 8 int16); a wave owns kRegU (4 for u8, 1 for int16) chunks of 64 vectors (1 KiB per load
 //    instruction).  The (L-1)-sample halo comes from the neighbouring lanes' registers by
 //    DPP wave shifts (v_mov_b32_dpp wave_shr:1 / wave_shl:1, wave_ror/rol at chunk seams),
 //    so every HBM byte is loaded once; only lanes 0 and 63 issue one extra 16-byte load for
@@ -21,7 +21,7 @@
 #include <algorithm>
 #include <string>
 
-#include "fir1d_reg.h"
+#include "fir1d_reg_launch.h"
 #include "fir_common.h"
 #include "fir_launch.h"
 
@@ -84,79 +84,6 @@ __global__ __launch_bounds__(kBlock) void fir1d_generic_kernel(const InT* __rest
 
 // ---------------------------------------------------------------------------------------
 // Host-side launchers.
-
-// Hot-kernel shape chosen by the A/B microbenchmark (tools/microbench; profiles/r01/micro_*.txt):
-// one 64-vector chunk per wave, default-policy loads and stores (non-temporal stores cost
-// 25-45 % on this 1:2 read:write stream; more chunks per wave or a persistent grid 3-15 %),
-// int32 outputs staged through LDS into whole 1 KiB store instructions (272 -> 257 us).
-constexpr int kRegU = 1;
-constexpr int kRegFlags = kCoal;
-constexpr int kPersistBlocks = 2048;
-
-template <typename InT, int STAGE, int L, int CH, int F, int FL>
-static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
-                                   const int32_t* hq, int frac, int acc_bits, hipStream_t stream) {
-    using OutT = typename OutTraits<STAGE>::T;
-    RowGeom g;
-    g.total = total;
-    g.rowlen32 = (uint32_t)(rows > 1 ? rowlen : 0);
-    g.multi_row = rows > 1;
-    g.aligned = rows == 1 || rowlen % (4 * InTraits<InT>::kPerDword) == 0;
-    TapsN<L, F> t;
-    for (int f = 0; f < F; ++f)
-        for (int k = 0; k < L; ++k) t.h[f][k] = hq[f * L + k];
-    pack_taps(t);
-    int64_t ntiles = 0, blocks = 0;
-    reg_launch_geometry<InT, kRegU, FL>(total, kPersistBlocks, &ntiles, &blocks);
-    hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, kRegU, FL, F>), dim3((unsigned)blocks), dim3(kBlock), 0,
-                       stream, (const InT*)x, (OutT*)y, g, t, 32 - acc_bits, frac, ntiles);
-    return hipGetLastError();
-}
-
-// Picks the kernel variant: acc_bits == 32 drops the wrap shifts; int16 samples with int16
-// taps (one channel) multiply on packed v_dot2_i32_i16; so do u8 samples (byte pairs) when
-// no accumulator can wrap: 255 * sum|h| + 2^(f-1) < 2^(acc_bits-1) for every filter.
-template <typename InT, int STAGE, int L, int CH, int F>
-static hipError_t launch_reg(const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
-                             const int32_t* hq, int frac, int acc_bits, hipStream_t stream) {
-    bool taps16 = true;
-    for (int k = 0; k < F * L; ++k) taps16 &= hq[k] >= -32768 && hq[k] <= 32767;
-    const bool acc32 = acc_bits == 32;
-    if constexpr (sizeof(InT) == 1 && CH == 1) {
-        bool nowrap = frac <= 22;
-        for (int f = 0; f < F; ++f) {
-            int64_t habs = 0;
-            for (int k = 0; k < L; ++k) habs += hq[f * L + k] < 0 ? -(int64_t)hq[f * L + k] : hq[f * L + k];
-            nowrap &= 255 * habs + ((int64_t)1 << (frac - 1)) < ((int64_t)1 << (acc_bits - 1));
-        }
-        if (taps16 && nowrap)
-            return launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kU8Dot2>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
-    }
-    if constexpr (sizeof(InT) == 2 && CH == 1) {
-        if (taps16)
-            return acc32 ? launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kDot2 | kAcc32>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream)
-                         : launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kDot2>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
-    }
-    return acc32 ? launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kAcc32>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream)
-                 : launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
-}
-
-template <typename InT, int STAGE, int CH, int F>
-static hipError_t launch_reg_taps(int L, const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
-                                  const int32_t* hq, int frac, int acc_bits, hipStream_t s) {
-    switch (L) {
-        case 1: return launch_reg<InT, STAGE, 1, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 2: return launch_reg<InT, STAGE, 2, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 3: return launch_reg<InT, STAGE, 3, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 4: return launch_reg<InT, STAGE, 4, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 5: return launch_reg<InT, STAGE, 5, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 6: return launch_reg<InT, STAGE, 6, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 7: return launch_reg<InT, STAGE, 7, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 8: return launch_reg<InT, STAGE, 8, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 9: return launch_reg<InT, STAGE, 9, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        default: return hipErrorInvalidValue;
-    }
-}
 
 template <typename InT, int STAGE>
 static hipError_t launch_generic(const void* x, void* y, int64_t start, int64_t end, int64_t total,

@@ -1,0 +1,91 @@
+// fir1d_reg_impl.h — host launchers of fir1d_reg_kernel (the register/DPP hot kernel).
+//
+// The kernel has one instantiation per (sample type, stage, channels, filters, taps,
+// variant); compiling them all in one translation unit took minutes, so
+// fir1d_reg_inst.hip includes this file once per (InT, STAGE, CH, F) with -D macros (see
+// the Makefile) and fir1d.hip only sees the declaration in fir1d_reg_launch.h.
+#pragma once
+
+#include "fir1d_reg.h"
+#include "fir1d_reg_launch.h"
+
+namespace fir {
+
+// Hot-kernel shape chosen by the A/B microbenchmark (tools/microbench; profiles/r01/micro_*.txt):
+// one 64-vector chunk per wave, default-policy loads and stores (non-temporal stores cost
+// 25-45 % on this 1:2 read:write stream; more chunks per wave or a persistent grid 3-15 %),
+// int32 outputs staged through LDS into whole 1 KiB store instructions (272 -> 257 us).
+// One u8 filter: 4 chunks per wave (the per-wave edge loads and row arithmetic amortised
+// over 4 KiB; 104.6 -> 94.0 us at 2^28, profiles/r01/micro_u8_chunks.txt); a fused bank
+// (F > 1) has 4x the math per byte and runs best at 1 chunk (248 vs 256 us for F = 4).
+template <typename InT, int F>
+constexpr int kRegU = sizeof(InT) == 1 && F == 1 ? 4 : 1;
+constexpr int kRegFlags = kCoal;
+constexpr int kPersistBlocks = 2048;
+
+template <typename InT, int STAGE, int L, int CH, int F, int FL>
+static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
+                                   const int32_t* hq, int frac, int acc_bits, hipStream_t stream) {
+    using OutT = typename OutTraits<STAGE>::T;
+    RowGeom g;
+    g.total = total;
+    g.rowlen32 = (uint32_t)(rows > 1 ? rowlen : 0);
+    g.multi_row = rows > 1;
+    g.aligned = rows == 1 || rowlen % (4 * InTraits<InT>::kPerDword) == 0;
+    TapsN<L, F> t;
+    for (int f = 0; f < F; ++f)
+        for (int k = 0; k < L; ++k) t.h[f][k] = hq[f * L + k];
+    pack_taps(t);
+    int64_t ntiles = 0, blocks = 0;
+    reg_launch_geometry<InT, kRegU<InT, F>, FL>(total, kPersistBlocks, &ntiles, &blocks);
+    hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, kRegU<InT, F>, FL, F>), dim3((unsigned)blocks), dim3(kBlock), 0,
+                       stream, (const InT*)x, (OutT*)y, g, t, 32 - acc_bits, frac, ntiles);
+    return hipGetLastError();
+}
+
+// Picks the kernel variant: acc_bits == 32 drops the wrap shifts; int16 samples with int16
+// taps (one channel) multiply on packed v_dot2_i32_i16; so do u8 samples (byte pairs) when
+// no accumulator can wrap: 255 * sum|h| + 2^(f-1) < 2^(acc_bits-1) for every filter.
+template <typename InT, int STAGE, int L, int CH, int F>
+static hipError_t launch_reg(const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
+                             const int32_t* hq, int frac, int acc_bits, hipStream_t stream) {
+    bool taps16 = true;
+    for (int k = 0; k < F * L; ++k) taps16 &= hq[k] >= -32768 && hq[k] <= 32767;
+    const bool acc32 = acc_bits == 32;
+    if constexpr (sizeof(InT) == 1 && CH == 1) {
+        bool nowrap = frac <= 22;
+        for (int f = 0; f < F; ++f) {
+            int64_t habs = 0;
+            for (int k = 0; k < L; ++k) habs += hq[f * L + k] < 0 ? -(int64_t)hq[f * L + k] : hq[f * L + k];
+            nowrap &= 255 * habs + ((int64_t)1 << (frac - 1)) < ((int64_t)1 << (acc_bits - 1));
+        }
+        if (taps16 && nowrap)
+            return launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kU8Dot2>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
+    }
+    if constexpr (sizeof(InT) == 2 && CH == 1) {
+        if (taps16)
+            return acc32 ? launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kDot2 | kAcc32>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream)
+                         : launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kDot2>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
+    }
+    return acc32 ? launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kAcc32>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream)
+                 : launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
+}
+
+template <typename InT, int STAGE, int CH, int F>
+hipError_t launch_reg_taps(int L, const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
+                                  const int32_t* hq, int frac, int acc_bits, hipStream_t s) {
+    switch (L) {
+        case 1: return launch_reg<InT, STAGE, 1, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 2: return launch_reg<InT, STAGE, 2, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 3: return launch_reg<InT, STAGE, 3, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 4: return launch_reg<InT, STAGE, 4, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 5: return launch_reg<InT, STAGE, 5, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 6: return launch_reg<InT, STAGE, 6, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 7: return launch_reg<InT, STAGE, 7, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 8: return launch_reg<InT, STAGE, 8, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 9: return launch_reg<InT, STAGE, 9, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace fir

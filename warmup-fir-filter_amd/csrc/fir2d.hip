@@ -113,7 +113,25 @@ static hipError_t launch2d_reg(const uint8_t* x, void* y, int64_t H, int64_t W, 
             const int hi = C - 2 - 2 * p >= 0 ? rowt[C - 2 - 2 * p] : 0;
             t.rowp[p] = ((uint32_t)lo & 0xFFFFu) | ((uint32_t)hi << 16);
         }
-        if (nowrap)
+        // int16 row sums (255 * sum|row| <= 32767) and int16 column taps: the column pass packs
+        // two rows' sums per dword and runs on v_dot2 too
+        int64_t sr = 0;
+        for (int n = 0; n < C; ++n) sr += rowt[n] < 0 ? -(int64_t)rowt[n] : rowt[n];
+        bool sep16 = 255 * sr <= 32767;
+        for (int m = 0; m < R; ++m) sep16 &= t.col[m] >= -32768 && t.col[m] <= 32767;
+        for (int p = 0; p < (R + 1) / 2; ++p) {
+            const int lo = t.col[2 * p];
+            const int hi = 2 * p + 1 < R ? t.col[2 * p + 1] : 0;
+            t.colp[p] = ((uint32_t)lo & 0xFFFFu) | ((uint32_t)hi << 16);
+        }
+        constexpr int S16 = kMode2dSep | kMode2dSep16;
+        if (sep16 && nowrap)
+            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, S16 | kMode2dNoWrap>), grid,
+                               dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
+        else if (sep16)
+            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, S16>), grid, dim3(kBlock), 0, s, x,
+                               (OutT*)y, H, W, t, 32 - acc_bits, frac);
+        else if (nowrap)
             hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, kMode2dSep | kMode2dNoWrap>), grid,
                                dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
         else

@@ -24,6 +24,8 @@ struct Taps2 {
     // SEP form (h[m][n] == col[m] * row[n] exactly): packed row taps, column taps
     uint32_t rowp[(C + 1) / 2];
     int32_t col[R];
+    // SEP16 form: column taps packed in pairs (col[2p], col[2p+1]) for v_dot2 over row-sum pairs
+    uint32_t colp[(R + 1) / 2];
 };
 
 // 2-D kernel arithmetic: general 5x5 on v_mad_i32_i24 / packed v_dot2, or rank-1 separable
@@ -31,7 +33,10 @@ struct Taps2 {
 // MODE = arithmetic (low 2 bits) | kMode2dNoWrap: the host proved |acc| + 2^(f-1) can never
 // reach the wrap limit, so every accumulator starts at the rounding bias 2^(f-1) and the
 // epilogue is one arithmetic shift (exactly fir_1d_fixed_ref.py:110-120 when no wrap occurs).
-enum Fir2dMode : int { kMode2dMad = 0, kMode2dDot2 = 1, kMode2dSep = 2, kMode2dNoWrap = 4 };
+// kMode2dSep16 (with kMode2dSep): the row sums fit int16 (255 * sum|row| <= 32767, host-checked),
+// so two consecutive rows' sums pack into one dword and the column pass is (R+1)/2 v_dot2 per
+// output pixel instead of R v_mad_i32_i24.
+enum Fir2dMode : int { kMode2dMad = 0, kMode2dDot2 = 1, kMode2dSep = 2, kMode2dNoWrap = 4, kMode2dSep16 = 8 };
 
 template <int R, int C>
 inline void pack_taps2(Taps2<R, C>& t) {
@@ -41,6 +46,25 @@ inline void pack_taps2(Taps2<R, C>& t) {
             const int hi = (C - 2 - 2 * p) >= 0 ? t.h[m][C - 2 - 2 * p] : 0;
             t.p2[m][p] = ((uint32_t)lo & 0xFFFFu) | ((uint32_t)hi << 16);
         }
+}
+
+// Four clamped NOWRAP accumulators (each <= 256 * 2^frac - 1) -> four u8 in one dword: the
+// shift of pixels 1..3 writes straight into its byte (SDWA dst_sel, other bytes preserved).
+__device__ __forceinline__ uint32_t pack4_shifted(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, int frac) {
+    uint32_t d = c0 >> frac;
+    asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+        : "+v"(d) : "s"(frac), "v"(c1));
+    asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+        : "+v"(d) : "s"(frac), "v"(c2));
+    asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+        : "+v"(d) : "s"(frac), "v"(c3));
+    return d;
+}
+
+__device__ __forceinline__ uint32_t clamp_u8_acc(uint32_t acc, int32_t sat_hi) {
+    uint32_t c;
+    asm("v_med3_i32 %0, %1, 0, %2" : "=v"(c) : "v"(acc), "s"(sat_hi));
+    return c;
 }
 
 // Branch-free row load: the address is always in bounds (the caller clamps it) and the
@@ -85,11 +109,13 @@ __global__ __launch_bounds__(kBlock) void fir2d_reg_kernel(const uint8_t* __rest
     const uint32_t acc0 = NOWRAP ? (1u << (frac - 1)) : 0u;  // rounding bias folded into the init
     uint32_t acc0v;  // the same in a VGPR, for dot2_from
     asm("v_mov_b32 %0, %1" : "=v"(acc0v) : "s"(acc0));
+    constexpr bool SEP16 = (MODE & 3) == kMode2dSep && (MODE & kMode2dSep16);
     uint32_t acc[R][VEC];
 #pragma unroll
     for (int s = 0; s < R; ++s)
 #pragma unroll
         for (int j = 0; j < VEC; ++j) acc[s][j] = acc0;
+    uint32_t qr[R][VEC] = {}, rsprev[VEC] = {};  // SEP16: packed (rs_t, rs_t-1) ring and rs_t-1
 
     auto row_ptr = [&](int64_t row) { return x + (row < 0 ? 0 : (row >= H ? H - 1 : row)) * W; };
     uint32_t cur[ND], hcur;
@@ -139,6 +165,24 @@ __global__ __launch_bounds__(kBlock) void fir2d_reg_kernel(const uint8_t* __rest
 #pragma unroll
                             for (int p = 1; p < (C + 1) / 2; ++p) a = dot2_acc(P[j + 2 * p], taps.p2[m][p], a);
                             acc[slot][j] = a;
+                        }
+                    }
+                } else if constexpr (SEP16) {  // int16 row sums packed with the previous row's
+#pragma unroll
+                    for (int j = 0; j < VEC; ++j) {
+                        uint32_t r = dot2_from0(P[j], taps.rowp[0]);
+#pragma unroll
+                        for (int p = 1; p < (C + 1) / 2; ++p) r = dot2_acc(P[j + 2 * p], taps.rowp[p], r);
+                        qr[t % R][j] = __builtin_amdgcn_perm(rsprev[j], r, 0x05040100u);  // (rs_t, rs_t-1)
+                        rsprev[j] = r;
+                    }
+                    if (t >= R - 1) {  // output t-(R-1) = sum_m col[m] rs_{t-m}: (R+1)/2 dot2 per pixel
+#pragma unroll
+                        for (int j = 0; j < VEC; ++j) {
+                            uint32_t a = dot2_from(qr[t % R][j], taps.colp[0], acc0v);
+#pragma unroll
+                            for (int p = 1; p < (R + 1) / 2; ++p) a = dot2_acc(qr[(t - 2 * p) % R][j], taps.colp[p], a);
+                            acc[(s + 1) % R][j] = a;
                         }
                     }
                 } else {  // separable: exact row sums (|r| < 2^23, host-checked), then the column taps
@@ -192,11 +236,17 @@ __global__ __launch_bounds__(kBlock) void fir2d_reg_kernel(const uint8_t* __rest
                         vN val;
 #pragma unroll
                         for (int i = 0; i < ND; ++i) {
-                            uint32_t o4 = 0;
+                            if constexpr (NOWRAP) {
+                                const uint32_t* a4 = &acc[slot][4 * i];
+                                val[i] = pack4_shifted(clamp_u8_acc(a4[0], sat_hi), clamp_u8_acc(a4[1], sat_hi),
+                                                       clamp_u8_acc(a4[2], sat_hi), clamp_u8_acc(a4[3], sat_hi), frac);
+                            } else {
+                                uint32_t o4 = 0;
 #pragma unroll
-                            for (int b = 0; b < 4; ++b)
-                                o4 |= sat_u8_pixel<NOWRAP>(acc[slot][4 * i + b], shl, frac, sat_hi) << (8 * b);
-                            val[i] = o4;
+                                for (int b = 0; b < 4; ++b)
+                                    o4 |= sat_u8_pixel<NOWRAP>(acc[slot][4 * i + b], shl, frac, sat_hi) << (8 * b);
+                                val[i] = o4;
+                            }
                         }
                         *reinterpret_cast<vN*>(dst) = val;
                     } else {
