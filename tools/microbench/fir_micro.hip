@@ -87,6 +87,32 @@ __global__ __launch_bounds__(kBlock) void widen_copy_split(const int16_t* __rest
     }
 }
 
+// widen copy whose int32 stores go through LDS as whole 1 KiB rows (the kCoal store path)
+__global__ __launch_bounds__(kBlock) void widen_copy_coal(const int16_t* __restrict__ x, int32_t* __restrict__ y,
+                                                          int64_t nvec) {
+    __shared__ u32x4 sb[kBlock * 2];
+    const int lane = threadIdx.x & 63;
+    const int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t w0 = v - lane;
+    if (w0 + 64 > nvec) return;
+    const u32x4 d = reinterpret_cast<const u32x4*>(x)[v];
+    u32x4* wb = sb + (threadIdx.x - lane) * 2;
+    wb[2 * lane] = u32x4{(uint32_t)(int32_t)(int16_t)d.x, (uint32_t)((int32_t)d.x >> 16),
+                         (uint32_t)(int32_t)(int16_t)d.y, (uint32_t)((int32_t)d.y >> 16)};
+    wb[2 * lane + 1] = u32x4{(uint32_t)(int32_t)(int16_t)d.z, (uint32_t)((int32_t)d.z >> 16),
+                             (uint32_t)(int32_t)(int16_t)d.w, (uint32_t)((int32_t)d.w >> 16)};
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    u32x4* yw = reinterpret_cast<u32x4*>(y + w0 * 8);
+    yw[lane] = wb[lane];
+    yw[64 + lane] = wb[64 + lane];
+}
+
+static void launch_copy_coal(const int16_t* x, int32_t* y, int64_t n, hipStream_t s, int) {
+    const int64_t nvec = n / 8;
+    hipLaunchKernelGGL(widen_copy_coal, dim3((unsigned)((nvec + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, x, y, nvec);
+}
+
 template <int U>
 static void launch_copy_split(const int16_t* x, int32_t* y, int64_t n, hipStream_t s, int) {
     const int64_t ntiles = (n + 512 * U - 1) / (512 * U);
@@ -204,6 +230,8 @@ int main(int argc, char** argv) {
         {"fir U2 dot2 acc32", true, launch_fir<2, kDot2 | kAcc32>, 0, {}},
         {"fir U1 dot2 acc32 nt-ld", true, launch_fir<1, kDot2 | kAcc32 | kNtLoad>, 0, {}},
         {"copy U1 plain", false, launch_copy<1, 0>, 0, {}},
+        {"copy U1 coal (LDS)", false, launch_copy_coal, 0, {}},
+        {"copy split U1", false, launch_copy_split<1>, 0, {}},
     };
 
     // correctness (FIR variants): sampled positions + both ends
