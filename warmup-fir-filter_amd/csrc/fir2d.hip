@@ -18,9 +18,10 @@
 namespace fir {
 
 // Shape chosen by the A/B microbenchmark (tools/microbench/fir2d_micro.hip, profiles/).
-constexpr int kVec2d = 16;
-constexpr int kStrip2d = 8;      // general (dot2) path: 16-row strips raise VGPRs past 128
-constexpr int kStrip2dSep = 16;  // separable path: 118 VGPRs at 16 rows, 6% faster than 8
+constexpr int kVec2d = 16;       // separable path: 16 pixels per lane, 16-row strips
+constexpr int kStrip2dSep = 16;
+constexpr int kVec2dGen = 8;     // general (dot2) path: 8 pixels per lane, 16-row strips, <= 128
+constexpr int kStrip2dGen = 16;  // VGPRs (4 waves/SIMD): 45.8 vs 48.5 us for 16 px x 8 rows
 
 // Generic: one output per thread, exact int64 sum, global loads (L1/L2 absorb the reuse).
 struct Taps2G {
@@ -138,13 +139,13 @@ static hipError_t launch2d_reg(const uint8_t* x, void* y, int64_t H, int64_t W, 
             hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, kMode2dSep>), grid, dim3(kBlock), 0, s,
                                x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
     } else {
-        const dim3 grid = fir2d_reg_grid<kVec2d, kStrip2d>(H, W);
+        const dim3 grid = fir2d_reg_grid<kVec2dGen, kStrip2dGen>(H, W);
         if (nowrap)
-            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2d, kMode2dDot2 | kMode2dNoWrap>), grid,
-                               dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
+            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dGen, kStrip2dGen, kMode2dDot2 | kMode2dNoWrap, 4>),
+                               grid, dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
         else
-            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2d, kMode2dDot2>), grid, dim3(kBlock), 0,
-                               s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
+            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dGen, kStrip2dGen, kMode2dDot2, 4>), grid,
+                               dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
     }
     return hipGetLastError();
 }
@@ -171,7 +172,7 @@ int launch_fir2d(const uint8_t* x, int64_t H, int64_t W, const int32_t* hq, int 
     if (frac < 1 || acc_bits < 1) return *err = "frac_bits and acc_bits must be >= 1", FIR_EINVAL;
     if (H == 0 || W == 0) return FIR_OK;
     if (!x || !y) return *err = "x and y must not be NULL", FIR_EINVAL;
-    if (H > 65535 * (int64_t)kStrip2d) return *err = "height too large", FIR_EINVAL;
+    if (H > 65535 * (int64_t)kStrip2dSep) return *err = "height too large", FIR_EINVAL;
     bool taps16 = true;  // the register kernel multiplies on v_dot2_i32_i16
     for (int k = 0; k < R * C; ++k) taps16 &= (hq[k] >= -32768 && hq[k] <= 32767);
     const bool fast = reg2d_shape(R, C) && W % kVec2d == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)y % 16 == 0 &&

@@ -78,8 +78,8 @@ __device__ __forceinline__ void load_row_px(const uint8_t* __restrict__ p, bool 
     for (int i = 0; i < ND; ++i) d[i] = ok ? q[i] : 0u;
 }
 
-template <int R, int C, int STAGE, int VEC, int STRIP, int MODE>
-__global__ __launch_bounds__(kBlock) void fir2d_reg_kernel(const uint8_t* __restrict__ x,
+template <int R, int C, int STAGE, int VEC, int STRIP, int MODE, int MINW = 1>
+__global__ __launch_bounds__(kBlock, MINW) void fir2d_reg_kernel(const uint8_t* __restrict__ x,
                                                            typename OutTraits<STAGE>::T* __restrict__ y, int64_t H,
                                                            int64_t W, Taps2<R, C> taps, int shl, int frac) {
     using OutT = typename OutTraits<STAGE>::T;
