@@ -5,11 +5,15 @@ file-name pattern, output sub-directories ``{kind}_{tap}tap[_{policy}]``, skip /
 behaviour and summary dict).  The u8 conversions run on the GPU (``fir_restore_u8``,
 SURVEY §8(f) 4) with the reference's arithmetic: ``clip`` = rint + clip to [0,255]
 (:51-54), ``normalize`` = min/max rescale (:57-64); fixed outputs are already uint8.
-PNG encoding is host I/O (Pillow).
+PNG encoding is host I/O (Pillow, whose zlib step releases the GIL): the files are
+encoded on a small thread pool while the next arrays convert on the GPU; the summary and
+its order are the reference's.
 """
 from __future__ import annotations
 
+import os
 import re
+from concurrent.futures import ThreadPoolExecutor
 from datetime import datetime, timezone
 from pathlib import Path
 from typing import Any
@@ -65,7 +69,28 @@ def restore_images(*, vector_output_dir: Path = DEFAULT_VECTOR_OUTPUT_DIR, outpu
         from PIL import Image
     except ModuleNotFoundError as exc:
         raise RuntimeError("Pillow is required to write PNG images.") from exc
-    converted, skipped = [], []
+    converted, skipped, pending = [], [], []
+    pool = ThreadPoolExecutor(max_workers=max(1, min(8, os.cpu_count() or 1)))
+    try:
+        _restore_all(kinds, taps, vector_output_dir, output_img_dir, ideal_policy, overwrite, strict, Image, pool,
+                     converted, skipped, pending)
+    except BaseException:
+        for f in pending:  # let the queued writes finish, then raise the stage's own error
+            f.exception()
+        pool.shutdown()
+        raise
+    for f in pending:  # every PNG written (or its write error raised) before returning
+        f.result()
+    pool.shutdown()
+    return {"generated_at_utc": datetime.now(timezone.utc).isoformat(),
+            "config": {"vector_output_dir": str(vector_output_dir), "output_img_dir": str(output_img_dir),
+                       "kind": kind, "tap": tap, "ideal_policy": ideal_policy, "overwrite": bool(overwrite),
+                       "strict": bool(strict)},
+            "num_converted": len(converted), "num_skipped": len(skipped), "converted": converted, "skipped": skipped}
+
+
+def _restore_all(kinds, taps, vector_output_dir, output_img_dir, ideal_policy, overwrite, strict, Image, pool,
+                 converted, skipped, pending):
     for k in kinds:
         for t in taps:
             src = vector_output_dir / f"{k}_{t}tap"
@@ -95,13 +120,8 @@ def restore_images(*, vector_output_dir: Path = DEFAULT_VECTOR_OUTPUT_DIR, outpu
                     skipped.append({"reason": "exists", "path": str(out)})
                     continue
                 img = _to_image_u8(np.load(p), k, ideal_policy)
-                Image.fromarray(img, mode="L").save(out)
+                pending.append(pool.submit(lambda im, o: Image.fromarray(im, mode="L").save(o), img, out))
                 converted.append({"input_npy": str(p), "output_img": str(out), "kind": k, "tap": f"{t}tap",
                                   "ideal_policy": ideal_policy if k == "ideal" else "n/a",
                                   "height": int(img.shape[0]), "width": int(img.shape[1]), "dtype": str(img.dtype),
                                   "pixel_min": int(img.min()), "pixel_max": int(img.max())})
-    return {"generated_at_utc": datetime.now(timezone.utc).isoformat(),
-            "config": {"vector_output_dir": str(vector_output_dir), "output_img_dir": str(output_img_dir),
-                       "kind": kind, "tap": tap, "ideal_policy": ideal_policy, "overwrite": bool(overwrite),
-                       "strict": bool(strict)},
-            "num_converted": len(converted), "num_skipped": len(skipped), "converted": converted, "skipped": skipped}
