@@ -226,21 +226,29 @@ int fir1d_fixed_rows_sharded(const void* x, int in_dtype, int64_t rows, int64_t 
             int* rc = &rcs[wi];
             std::string* msg = &msgs[wi];
             ++wi;
-            workers.emplace_back([=]() {
-                for (const Shard& sh : *list) {
-                    const int64_t cnt = sh.rows * sh.width * channels;
-                    *rc = run_host(
-                        dev, (const char*)x + sh.in0 * isz, (size_t)cnt * isz, (char*)y + sh.out0 * osz,
-                        (size_t)sh.len * osz,
-                        [&](void* dx, void* dy, hipStream_t s, std::string* err) {
-                            return fir::launch_fir1d_rows(dx, in_dtype, sh.rows, sh.width, channels, hq, taps,
-                                                          frac_bits, acc_bits, out_stage, dy, s, err);
-                        },
-                        (size_t)sh.skip * osz, 0, (size_t)cnt * osz);
-                    if (*rc) {
-                        *msg = g_err;  // thread-local: this worker's message
-                        return;
+            workers.emplace_back([=]() noexcept {
+                try {
+                    for (const Shard& sh : *list) {
+                        const int64_t cnt = sh.rows * sh.width * channels;
+                        *rc = run_host(
+                            dev, (const char*)x + sh.in0 * isz, (size_t)cnt * isz, (char*)y + sh.out0 * osz,
+                            (size_t)sh.len * osz,
+                            [&](void* dx, void* dy, hipStream_t s, std::string* err) {
+                                return fir::launch_fir1d_rows(dx, in_dtype, sh.rows, sh.width, channels, hq, taps,
+                                                              frac_bits, acc_bits, out_stage, dy, s, err);
+                            },
+                            (size_t)sh.skip * osz, 0, (size_t)cnt * osz);
+                        if (*rc) {
+                            *msg = g_err;  // thread-local: this worker's message
+                            return;
+                        }
                     }
+                } catch (const std::exception& ex) {  // never let an exception end the process
+                    *rc = FIR_EHIP;
+                    *msg = std::string("internal error: ") + ex.what();
+                } catch (...) {
+                    *rc = FIR_EHIP;
+                    *msg = "internal error";
                 }
             });
         }
