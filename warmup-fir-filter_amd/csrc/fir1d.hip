@@ -5,15 +5,16 @@
 //   q = (acc + 2^(f-1)) >> f, then saturated to u8 or kept as int32.
 //
 // Two kernels:
-//  * fir1d_reg_kernel (fir1d_reg.h) — the hot path.  A lane owns one 16-byte vector of
-//    samples (16 u8 or 8 int16); a wave owns kRegU (4 for u8, 1 for int16) chunks of 64 vectors (1 KiB per load
+//  * fir1d_reg_kernel (fir1d_reg.h; launchers in fir1d_reg_impl.h, instantiated per
+//    configuration by fir1d_reg_inst.hip) — the hot path.  A lane owns one 16-byte vector
+//    of samples (16 u8 or 8 int16); a wave owns kRegU chunks of 64 vectors (1 KiB per load
 //    instruction).  The (L-1)-sample halo comes from the neighbouring lanes' registers by
-//    DPP wave shifts (v_mov_b32_dpp wave_shr:1 / wave_shl:1, wave_ror/rol at chunk seams),
-//    so every HBM byte is loaded once; only lanes 0 and 63 issue one extra 16-byte load for
-//    the adjacent tile's edge vector (an L2 hit).  32-bit wrap-around MACs on
-//    v_mad_i32_i24 (taps checked to fit 24 bits on the host), overflow-free rounding,
-//    16-byte stores.  Row edges (images) are handled by a per-vector column
-//    test; vectors whose window lies inside one row take the unmasked path.
+//    DPP wave shifts, so every HBM byte is loaded once; only lanes 0 and 63 issue one extra
+//    16-byte load for the adjacent tile's edge vector (an L2 hit).  MACs on packed
+//    v_dot2_i32_i16 (int16 samples, or u8 byte pairs when no accumulator can wrap) or
+//    v_mad_i32_i24, overflow-free rounding, int32 outputs stored through LDS as whole
+//    1 KiB rows.  Rows that are a whole number of vectors zero the out-of-row halo and
+//    stay on the unmasked path; other widths mask the vectors that straddle a row edge.
 //  * fir1d_generic_kernel — every other configuration (any tap count up to FIR_MAX_TAPS,
 //    any acc_bits / frac_bits, unaligned buffers, narrow rows, halo segments): a
 //    workgroup stages an LDS sliding-window tile of 1024 outputs + (L-1)*channels halo

@@ -1,5 +1,5 @@
 // fir1d_reg.h — the register/DPP 1-D FIR kernel template (hot path), shared by the library
-// (fir1d.hip) and the A/B microbenchmark (tools/microbench).
+// (fir1d_reg_impl.h) and the A/B microbenchmarks (tools/microbench).
 //
 // Work unit: a wave owns a "tile" of U chunks; chunk u is 64 consecutive 16-byte vectors,
 // one per lane, so every load instruction is 1 KiB contiguous.  The (L-1)-sample halo of a
@@ -8,9 +8,11 @@
 // outer edges cost an extra (L2-served) 16-byte load, issued by lane 0 and lane 63.
 //
 // Arithmetic: fir_1d/model/python/fir_1d_fixed_ref.py:95-126 (reference root) with a
-// 32-bit accumulator: wrap-around MACs on v_mad_i32_i24 (taps < 2^23 checked on the
-// host), wrap to acc_bits by shl/ashr, overflow-free round (floor(a/2^f) + bit f-1),
-// saturate (u8) or keep (int32).
+// 32-bit accumulator: wrap-around MACs (v_mad_i32_i24 with taps < 2^23 checked on the host;
+// packed v_dot2_i32_i16 for int16 taps over int16 samples [kDot2] or over zero-extended u8
+// byte pairs when no accumulator can wrap [kU8Dot2, bias preloaded, v_med3 saturation]),
+// wrap to acc_bits by shl/ashr (skipped for acc_bits = 32 [kAcc32]), overflow-free round
+// (floor(a/2^f) + bit f-1), saturate (u8) or keep (int32; stored through LDS [kCoal]).
 #pragma once
 
 #include "fir_common.h"
