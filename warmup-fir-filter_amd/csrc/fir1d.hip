@@ -83,6 +83,35 @@ __global__ __launch_bounds__(kBlock) void fir1d_generic_kernel(const InT* __rest
     }
 }
 
+// Both edges of a single-row segment in one launch (multi-GPU step): output j < hle is the
+// left edge, j >= hle maps to the right edge total - hre + (j - hle).  Samples left of the
+// segment come from halo_l, right of it from halo_r (zeros when NULL).  Exact int64 sums.
+template <typename InT, int STAGE>
+__global__ __launch_bounds__(kBlock) void fir1d_edges_kernel(const InT* __restrict__ x,
+                                                             typename OutTraits<STAGE>::T* __restrict__ y,
+                                                             int64_t total, int ch, const InT* __restrict__ halo_l,
+                                                             const InT* __restrict__ halo_r, TapsG taps, int L,
+                                                             int hle, int hre, int frac, int acc_bits) {
+    const int c = L / 2;
+    for (int j = threadIdx.x; j < hle + hre; j += kBlock) {
+        const int64_t gi = j < hle ? j : total - hre + (j - hle);
+        int64_t acc = 0;
+        for (int k = 0; k < L; ++k) {
+            const int64_t si = gi + (int64_t)(c - k) * ch;
+            int32_t v = 0;
+            if (si >= 0 && si < total) {
+                v = (int32_t)x[si];
+            } else if (si < 0) {
+                if (halo_l) v = (int32_t)halo_l[hle + si];
+            } else if (halo_r) {
+                v = (int32_t)halo_r[si - total];
+            }
+            acc += (int64_t)taps.h[k] * v;
+        }
+        y[gi] = stage_out<STAGE>(round64(acc, frac, acc_bits));
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // Host-side launchers.
 
@@ -118,6 +147,16 @@ static hipError_t dispatch_generic(int in_dtype, int stage, const void* x, void*
                                                          hq, L, frac, acc_bits, s)
                : launch_generic<int16_t, FIR_OUT_I32>(x, y, start, end, total, rowlen, multi_row, ch, hl, hr, hq,
                                                       L, frac, acc_bits, s);
+}
+
+template <typename InT, int STAGE>
+static hipError_t launch_edges(const void* x, void* y, int64_t total, int ch, const void* hl, const void* hr,
+                               const TapsG& t, int L, int64_t hle, int64_t hre, int frac, int acc_bits,
+                               hipStream_t stream) {
+    hipLaunchKernelGGL((fir1d_edges_kernel<InT, STAGE>), dim3(1), dim3(kBlock), 0, stream, (const InT*)x,
+                       (typename OutTraits<STAGE>::T*)y, total, ch, (const InT*)hl, (const InT*)hr, t, L, (int)hle,
+                       (int)hre, frac, acc_bits);
+    return hipGetLastError();
 }
 
 static int check_common(int in_dtype, int64_t rows, int64_t width, int ch, const int32_t* hq, int L, int frac,
@@ -231,16 +270,20 @@ int launch_fir1d_edges(const void* x, int in_dtype, int64_t n, int ch, const int
     const int c = L / 2;
     const int64_t hle = (int64_t)(L - 1 - c) * ch, hre = (int64_t)c * ch;
     hipError_t e = hipSuccess;
-    if (total <= hle + hre) {
+    if (total <= hle + hre) {  // the whole segment is edge
         e = dispatch_generic(in_dtype, stage, x, y, 0, total, total, total, false, ch, hl, hr, hq, L, frac, acc_bits,
                              stream);
-    } else {
-        if (hle > 0)
-            e = dispatch_generic(in_dtype, stage, x, y, 0, hle, total, total, false, ch, hl, hr, hq, L, frac,
-                                 acc_bits, stream);
-        if (e == hipSuccess && hre > 0)
-            e = dispatch_generic(in_dtype, stage, x, y, total - hre, total, total, total, false, ch, hl, hr, hq, L,
-                                 frac, acc_bits, stream);
+    } else if (hle + hre > 0) {  // both edges, one launch
+        TapsG t;
+        for (int k = 0; k < FIR_MAX_TAPS; ++k) t.h[k] = k < L ? hq[k] : 0;
+        if (in_dtype == FIR_IN_U8)
+            e = stage == FIR_OUT_U8_SAT
+                    ? launch_edges<uint8_t, FIR_OUT_U8_SAT>(x, y, total, ch, hl, hr, t, L, hle, hre, frac, acc_bits, stream)
+                    : launch_edges<uint8_t, FIR_OUT_I32>(x, y, total, ch, hl, hr, t, L, hle, hre, frac, acc_bits, stream);
+        else
+            e = stage == FIR_OUT_U8_SAT
+                    ? launch_edges<int16_t, FIR_OUT_U8_SAT>(x, y, total, ch, hl, hr, t, L, hle, hre, frac, acc_bits, stream)
+                    : launch_edges<int16_t, FIR_OUT_I32>(x, y, total, ch, hl, hr, t, L, hle, hre, frac, acc_bits, stream);
     }
     if (e != hipSuccess) return *err = std::string("fir1d edge launch failed: ") + hipGetErrorString(e), FIR_EHIP;
     return FIR_OK;
