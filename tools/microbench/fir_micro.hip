@@ -225,6 +225,7 @@ int main(int argc, char** argv) {
         {"fir U1 mad acc32", true, launch_fir<1, kAcc32>, 0, {}},
         {"fir U1 dot2 acc32", true, launch_fir<1, kDot2 | kAcc32>, 0, {}},
         {"fir U1 dot2 acc32 coal", true, launch_fir<1, kDot2 | kAcc32 | kCoal>, 0, {}},
+        {"fir U1 dot2 acc32 coal xcd", true, launch_fir<1, kDot2 | kAcc32 | kCoal | kXcd>, 0, {}},
         {"fir U2 dot2 acc32 coal", true, launch_fir<2, kDot2 | kAcc32 | kCoal>, 0, {}},
         {"fir U1 dot2", true, launch_fir<1, kDot2>, 0, {}},
         {"fir U2 dot2 acc32", true, launch_fir<2, kDot2 | kAcc32>, 0, {}},

@@ -32,7 +32,18 @@ enum RegFlags : int {
     kU8Dot2 = 32,  // u8 samples, 1 channel, int16 taps, no wrap possible: byte-pair v_dot2 MACs
     kCoal = 64,    // int32 outputs of a full 64-vector chunk go out through LDS as contiguous
                    // 1 KiB store instructions (instead of 16 B per lane at a 16*VEC/4-byte stride)
+    kXcd = 128,    // XCD-aware block order: the hardware deals consecutive blocks round-robin
+                   // to the 8 XCDs; remap so each XCD (own L2) streams one contiguous eighth
 };
+
+constexpr int kNumXcd = 8;
+
+// Block id -> position in the tile order.  Blocks b and b + 8 run on the same XCD; with
+// kXcd they get adjacent positions, so a wave's edge vector usually sits in the same L2.
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
+    const int64_t q = nb / kNumXcd;
+    return b < q * kNumXcd ? (b % kNumXcd) * q + b / kNumXcd : b;
+}
 
 constexpr int kDppWaveRol1 = 0x134;  // lane i <- lane i+1, lane 63 <- lane 0
 constexpr int kDppWaveRor1 = 0x13C;  // lane i <- lane i-1, lane 0 <- lane 63
@@ -295,7 +306,8 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
     const int64_t total = g.total;
     const int64_t nvec = total / VEC;
     const int64_t stride = PERSIST ? (int64_t)gridDim.x * WPB : ntiles;
-    int64_t tile = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);  // wave-uniform
+    const int64_t bpos = (FLAGS & kXcd) ? xcd_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    int64_t tile = bpos * WPB + (threadIdx.x >> 6);  // wave-uniform
 
     uint32_t own[U][4];
     if (tile < ntiles) {
