@@ -119,3 +119,28 @@ def test_pipeline_restore_small_images(tmp_path, images):
     for png in (tmp_path / "img" / "fixed_5tap").glob("*.png"):
         key = golden_key(small_out.files, png.name, "_y_u8.png")
         assert np.array_equal(np.asarray(Image.open(png)), small_out[key]), png.name
+
+
+def test_stage_clis_end_to_end(tmp_path, images, capsys):
+    """Each stage's CLI (the reference's flags and [OK] status line) on the two 64x64 images."""
+    from fir_1d.sim.vector import (gen_3tap_compare_report, gen_fixed_output, gen_ideal_output, gen_input_vectors,
+                                   restore_images)
+
+    small = {k: v for k, v in images.items() if v.size <= 64 * 64}
+    np.savez(tmp_path / "small.npz", **small)
+    inp, out, img = tmp_path / "in", tmp_path / "out", tmp_path / "img"
+    assert gen_input_vectors.main(["--image-dir", str(tmp_path / "small.npz"), "--output-dir", str(inp)]) == 0
+    assert gen_ideal_output.main(["--input-dir", str(inp), "--output-dir", str(out), "--tap", "3"]) == 0
+    assert gen_fixed_output.main(["--input-dir", str(inp), "--output-dir", str(out), "--tap", "3"]) == 0
+    assert gen_3tap_compare_report.main(["--ideal-dir", str(out / "ideal_3tap"), "--fixed-dir", str(out / "fixed_3tap"),
+                                         "--report-dir", str(out / "report_3tap"), "--strict"]) == 0
+    summary = tmp_path / "restore.json"
+    assert restore_images.main(["--vector-output-dir", str(out), "--output-img-dir", str(img), "--tap", "3",
+                                "--summary-json", str(summary)]) == 0
+    lines = [ln for ln in capsys.readouterr().out.splitlines() if ln.startswith(("[OK]", "[FAIL]"))]
+    assert len(lines) == 5 and all(ln.startswith("[OK]") for ln in lines), lines
+    res = json.loads(summary.read_text())
+    assert res["num_converted"] == 16 and res["num_skipped"] == 0
+    # second restore without --overwrite: everything skipped, nothing rewritten
+    assert restore_images.main(["--vector-output-dir", str(out), "--output-img-dir", str(img), "--tap", "3"]) == 0
+    assert "generated=0 skipped=16" in capsys.readouterr().out

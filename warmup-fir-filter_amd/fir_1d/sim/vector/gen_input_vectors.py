@@ -10,8 +10,11 @@ pipeline runs without re-decoding JPEGs (libjpeg versions can differ).
 """
 from __future__ import annotations
 
+import argparse
+
 import json
 from pathlib import Path
+from time import perf_counter
 
 import numpy as np
 
@@ -86,3 +89,30 @@ def generate_input_vector_jsons(image_dir: Path = DEFAULT_IMAGE_DIR, output_dir:
                 "overwrite": bool(overwrite), "generated_cases": generated, "skipped_cases": skipped, "cases": cases}
     (output_dir / "input_vector_manifest.json").write_text(json.dumps(manifest, indent=2) + "\n", encoding="utf-8")
     return manifest
+
+
+def _build_argparser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(description="Generate FIR 1D input vectors (.npy) and preview/manifest JSON files.")
+    ap.add_argument("--image-dir", type=Path, default=DEFAULT_IMAGE_DIR,
+                    help="image folder, or a .npz of decoded uint8 images")
+    ap.add_argument("--output-dir", type=Path, default=DEFAULT_OUTPUT_DIR)
+    ap.add_argument("--overwrite", action="store_true")
+    return ap
+
+
+def main(argv=None) -> int:
+    t0 = perf_counter()
+    args = _build_argparser().parse_args(argv)
+    try:
+        m = generate_input_vector_jsons(image_dir=args.image_dir, output_dir=args.output_dir, overwrite=args.overwrite)
+    except Exception as exc:
+        print(f"[FAIL] gen_input_vectors file=gen_input_vectors.py generated=0 skipped=0 failed=1 "
+              f"elapsed={perf_counter() - t0:.2f}s out={args.output_dir.resolve()} error=\"{exc}\"")
+        raise
+    print(f"[OK] gen_input_vectors file=gen_input_vectors.py generated={m['generated_cases']} "
+          f"skipped={m['skipped_cases']} failed=0 elapsed={perf_counter() - t0:.2f}s out={m['output_dir']}")
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

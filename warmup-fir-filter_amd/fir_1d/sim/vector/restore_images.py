@@ -11,11 +11,14 @@ its order are the reference's.
 """
 from __future__ import annotations
 
+import argparse
+import json
 import os
 import re
 from concurrent.futures import ThreadPoolExecutor
 from datetime import datetime, timezone
 from pathlib import Path
+from time import perf_counter
 from typing import Any
 
 import numpy as np
@@ -125,3 +128,43 @@ def _restore_all(kinds, taps, vector_output_dir, output_img_dir, ideal_policy, o
                                   "ideal_policy": ideal_policy if k == "ideal" else "n/a",
                                   "height": int(img.shape[0]), "width": int(img.shape[1]), "dtype": str(img.dtype),
                                   "pixel_min": int(img.min()), "pixel_max": int(img.max())})
+
+
+def _build_argparser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(description="Restore output images from FIR ideal/fixed vector .npy files.")
+    ap.add_argument("--vector-output-dir", type=Path, default=DEFAULT_VECTOR_OUTPUT_DIR)
+    ap.add_argument("--output-img-dir", type=Path, default=DEFAULT_OUTPUT_IMG_DIR)
+    ap.add_argument("--kind", choices=("all",) + VALID_KINDS, default="all")
+    ap.add_argument("--tap", choices=("all",) + VALID_TAPS, default="all")
+    ap.add_argument("--ideal-policy", choices=IDEAL_POLICIES, default="clip")
+    ap.add_argument("--overwrite", action="store_true")
+    ap.add_argument("--strict", action="store_true")
+    ap.add_argument("--summary-json", type=Path, default=None, help="optional path for the JSON summary")
+    return ap
+
+
+def main(argv=None) -> int:
+    args = _build_argparser().parse_args(argv)
+    t0 = perf_counter()
+    try:
+        res = restore_images(vector_output_dir=args.vector_output_dir, output_img_dir=args.output_img_dir,
+                             kind=args.kind, tap=args.tap, ideal_policy=args.ideal_policy, overwrite=args.overwrite,
+                             strict=args.strict)
+        extra = ""
+        if args.summary_json is not None:
+            path = args.summary_json.resolve()
+            path.parent.mkdir(parents=True, exist_ok=True)
+            path.write_text(json.dumps(res, indent=2, ensure_ascii=False) + "\n", encoding="utf-8")
+            extra = f" summary_json={path}"
+    except Exception as exc:
+        print(f"[FAIL] restore_images file=restore_images.py generated=0 skipped=0 failed=1 "
+              f"elapsed={perf_counter() - t0:.2f}s out={args.output_img_dir.resolve()} error=\"{exc}\"")
+        raise
+    print(f"[OK] restore_images file=restore_images.py generated={res['num_converted']} "
+          f"skipped={res['num_skipped']} failed=0 elapsed={perf_counter() - t0:.2f}s "
+          f"out={args.output_img_dir.resolve()}{extra}")
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
