@@ -1,0 +1,84 @@
+/* capi_check.c — host AddressSanitizer exercise of the C ABI (include/fir_hip.h).
+ *
+ * Built by `make -C warmup-fir-filter_amd/csrc asan-check` against a copy of the library
+ * whose host code (capi.hip: buffer cache, sharding threads, validation) is compiled with
+ * -Xarch_host -fsanitize=address; device code is unchanged.  Without a GPU it covers the
+ * argument validation and error paths; with one it also runs every host-pointer entry on
+ * small ragged inputs (results are checked elsewhere; here only memory safety and status
+ * codes matter).  Exit status 0 = no failure; ASan aborts on any host memory error. */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "fir_hip.h"
+
+static int failures = 0;
+
+static void expect(int cond, const char* what) {
+    if (!cond) {
+        fprintf(stderr, "FAIL: %s (%s)\n", what, fir_last_error());
+        ++failures;
+    }
+}
+
+int main(void) {
+    expect(fir_abi_version() == FIR_HIP_ABI_VERSION, "abi version");
+    int ndev = 0;
+    const int have = fir_device_count(&ndev) == FIR_OK && ndev > 0;
+    const int32_t h3[3] = {1024, 2048, 1024};
+    const int devs[3] = {0, 0, 0};
+
+    /* validation paths (no device needed) */
+    expect(fir1d_fixed_rows_dev(NULL, 7, 1, 16, 1, h3, 3, 12, 32, 0, NULL, NULL) == FIR_EINVAL, "bad in_dtype");
+    expect(fir1d_fixed_rows_dev(NULL, 0, 1, 16, 1, h3, 0, 12, 32, 0, NULL, NULL) == FIR_EINVAL, "zero taps");
+    expect(fir1d_fixed_rows_dev(NULL, 0, 1, 16, 1, h3, 3, 12, 32, 0, NULL, NULL) == FIR_EINVAL, "null x");
+    expect(fir1d_fixed_rows_sharded(NULL, 0, 1, 16, 1, h3, 3, 12, 32, 0, NULL, devs, 0) == FIR_EINVAL, "ndev 0");
+    expect(fir1d_fixed_rows_sharded(NULL, 0, 0, 16, 1, h3, 3, 12, 32, 0, NULL, devs, 3) == FIR_OK, "empty sharded");
+    expect(fir_restore_u8_dev(NULL, 8, 9, NULL, NULL, NULL) == FIR_EINVAL, "bad policy");
+    expect(fir2d_fixed_dev(NULL, 4, 4, h3, 0, 3, 12, 32, 0, NULL, NULL) == FIR_EINVAL, "2d zero rows");
+    expect(strlen(fir_last_error()) > 0, "error text");
+    if (!have) {
+        uint8_t x[64] = {0}, y[64];
+        expect(fir1d_fixed_rows(x, 0, 1, 64, 1, h3, 3, 12, 32, 0, y, 0) == FIR_ENODEV, "no device -> ENODEV");
+        printf("capi_check: no device, %d failure(s)\n", failures);
+        return failures != 0;
+    }
+
+    /* every host entry on small ragged shapes */
+    for (int64_t w = 1; w <= 300; w += 37) {
+        const int64_t rows = 3, n = rows * w;
+        uint8_t* x8 = malloc((size_t)n);
+        int16_t* x16 = malloc((size_t)n * 4);
+        uint8_t* y8 = malloc((size_t)n * 4);
+        int32_t* y32 = malloc((size_t)n * 8);
+        double* yd = malloc((size_t)n * 8);
+        for (int64_t i = 0; i < n; ++i) x8[i] = (uint8_t)(i * 37);
+        for (int64_t i = 0; i < 2 * n; ++i) x16[i] = (int16_t)(i * 4099);
+        expect(fir1d_fixed_rows(x8, FIR_IN_U8, rows, w, 1, h3, 3, 12, 32, FIR_OUT_U8_SAT, y8, 0) == FIR_OK, "u8");
+        expect(fir1d_fixed_rows(x16, FIR_IN_I16, rows, w, 2, h3, 3, 12, 32, FIR_OUT_I32, y32, 0) == FIR_OK, "cplx");
+        expect(fir1d_fixed_rows_sharded(x16, FIR_IN_I16, 1, n, 1, h3, 3, 12, 32, FIR_OUT_I32, y32, devs, 3) == FIR_OK,
+               "sharded row");
+        expect(fir1d_fixed_rows_sharded(x8, FIR_IN_U8, rows, w, 1, h3, 3, 12, 32, FIR_OUT_U8_SAT, y8, devs, 3) ==
+                   FIR_OK, "sharded rows");
+        const int32_t bank[6] = {1, 2, 1, -1, 0, 1};
+        expect(fir1d_fixed_rows_multi(x8, FIR_IN_U8, rows, w, 1, bank, 3, 2, 12, 32, FIR_OUT_U8_SAT, y8, 0) == FIR_OK,
+               "multi");
+        const double hd[3] = {0.25, 0.5, 0.25};
+        expect(fir1d_ideal_rows(x8, rows, w, hd, 3, yd, 0) == FIR_OK, "ideal");
+        double m[9];
+        expect(fir_compare_metrics(yd, x8, n, m, 0) == FIR_OK, "metrics");
+        expect(fir_restore_u8(yd, n, FIR_RESTORE_NORMALIZE, y8, 0) == FIR_OK, "restore");
+        const int32_t k2[9] = {1, 2, 1, 2, 4, 2, 1, 2, 1};
+        expect(fir2d_fixed(x8, rows, w, k2, 3, 3, 4, 32, FIR_OUT_U8_SAT, y8, 0) == FIR_OK, "2d");
+        free(x8);
+        free(x16);
+        free(y8);
+        free(y32);
+        free(yd);
+    }
+    static uint8_t one = 1;
+    expect(fir1d_fixed_rows_sharded(&one, 0, 1, 1, 1, h3, 3, 12, 32, 0, NULL, devs, 1) == FIR_EINVAL, "null y");
+    printf("capi_check: device present, %d failure(s)\n", failures);
+    return failures != 0;
+}

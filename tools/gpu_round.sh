@@ -53,6 +53,7 @@ for s in $STEPS; do
                      --output-format csv -- python bench.py --workload "$wl" --steps 10 --warmup 2 --cpu-seconds 0 \
                      --no-parity; fatal $? || exit
              done ;;
+        asan) run asan 600 make -C warmup-fir-filter_amd/csrc asan-check; fatal $? ;;
         micro) run micro 300 tools/microbench/fir_micro 28 20; fatal $? ;;
         micro2d) run micro2d 300 tools/microbench/fir2d_micro 15; fatal $? ;;
         microideal) run microideal 300 tools/microbench/ideal_micro 15; fatal $? ;;
