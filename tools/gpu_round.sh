@@ -57,6 +57,7 @@ for s in $STEPS; do
         micro) run micro 300 tools/microbench/fir_micro 28 20; fatal $? ;;
         micro2d) run micro2d 300 tools/microbench/fir2d_micro 15; fatal $? ;;
         microideal) run microideal 300 tools/microbench/ideal_micro 15; fatal $? ;;
+        microread) run microread 300 tools/microbench/read_micro 15; fatal $? ;;
         microu8) run microu8 300 tools/microbench/fir_u8_micro 15; fatal $? ;;
         dist2|dist4) n=${s#dist}
              run "dist$n" 300 env FIR_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 \

@@ -68,11 +68,13 @@ __device__ __forceinline__ void metrics_term(double id, uint32_t fx, double& sab
 }
 
 // VEC (ideal 16-byte and fixed 2-byte aligned): a wave reads tiles of kMetricTile samples as
-// whole 1 KiB f64 rows plus 128 B u8 rows; each lane sums its 8 samples of a tile plainly
-// and adds the tile partials into its Neumaier-compensated accumulators (the compensated
-// add per sample made the kernel latency-bound).  The ragged tail and unaligned inputs take
-// the per-sample grid-stride loop.
-constexpr int kMetricTile = 4 * kWave * 2;
+// whole 1 KiB f64 rows plus 128 B u8 rows, 16 non-temporal f64 loads in flight per lane
+// (the read-stream A/B, tools/microbench/read_micro.hip); each lane sums its 32 samples of
+// a tile plainly and adds the tile partials into its Neumaier-compensated accumulators
+// (a compensated add per sample made the kernel latency-bound).  The ragged tail and
+// unaligned inputs take the per-sample grid-stride loop.
+constexpr int kMetricLoads = 16;
+constexpr int kMetricTile = kMetricLoads * kWave * 2;
 
 template <bool VEC>
 __global__ __launch_bounds__(kBlock) void metrics_pass1(const double* __restrict__ ideal,
@@ -90,16 +92,16 @@ __global__ __launch_bounds__(kBlock) void metrics_pass1(const double* __restrict
         for (int64_t t = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6); t < ntile; t += nwaves) {
             const d2* pi = reinterpret_cast<const d2*>(ideal + t * kMetricTile);
             const uint16_t* pf = reinterpret_cast<const uint16_t*>(fixed + t * kMetricTile);
-            d2 a[4];
-            uint32_t f[4];
+            d2 a[kMetricLoads];
+            uint32_t f[kMetricLoads];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                a[i] = pi[i * kWave + lane];
-                f[i] = pf[i * kWave + lane];
+            for (int i = 0; i < kMetricLoads; ++i) {
+                a[i] = __builtin_nontemporal_load(pi + i * kWave + lane);
+                f[i] = __builtin_nontemporal_load(pf + i * kWave + lane);
             }
             double sabs = 0.0, ssq = 0.0, sd = 0.0;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < kMetricLoads; ++i) {
                 metrics_term(a[i].x, f[i] & 0xFFu, sabs, ssq, sd, mx, lo, hi, clip);
                 metrics_term(a[i].y, f[i] >> 8, sabs, ssq, sd, mx, lo, hi, clip);
             }
