@@ -311,6 +311,7 @@ def main() -> int:
             else:
                 dist.barrier()
 
+    barrier()  # every rank's communicator is up before the first halo exchange
     for _ in range(args.warmup):
         wl.step()
     barrier()
@@ -407,7 +408,7 @@ def main() -> int:
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": KERNELS[args.workload],
-                     "limiter": "VALU (~11.6 integer VALU ops/pixel, DESIGN.md §5)" if args.workload == "fir2d_u8"
+                     "limiter": "VALU (~8.8 VALU instructions/pixel on packed 16-bit pixel pairs, DESIGN.md §5)" if args.workload == "fir2d_u8"
                      else "HBM",
                      "kernel_avg_us": round(kern_avg_s * 1e6, 2), "algorithmic_bytes_per_launch": alg_bytes,
                      "timing": f"HIP events around {args.steps} back-to-back launches of the kernel"},

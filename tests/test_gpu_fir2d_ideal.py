@@ -73,7 +73,11 @@ SEP_KERNELS = [  # (col, row): rank-1 kernels reaching each separable variant
     ([3, -1, 3], [200, 300, -100, 300, 200]),          # 32-bit column pass, 3x5
     ([127] * 5, [255, 255, 255]),                       # near-int16 taps; wraps at acc_bits = 24
     ([40000, -1, 3], [1, 1, 1]),                        # taps beyond int16: generic kernel
+    ([-1, 3, -1], [1, -2, 5, -2, 1]),                   # packed 16-bit pairs, signed sum
+    ([1, 2, 1], [1, 2, 1]),                             # packed 16-bit pairs, unsigned, shift 12
 ]
+# Kernel 0 reaches the packed 16-bit path with f - s = 8 (high-byte output) at frac 12, with a
+# clamped shift of 4 at frac 8, and sep16 at frac 16 (its 16-bit sum would overflow there).
 
 
 @pytest.mark.parametrize("k", range(len(SEP_KERNELS)))

@@ -27,7 +27,7 @@ static int32_t g_h[5][5];
 
 static int32_t g_col[5], g_row[5];
 
-template <int VEC, int STRIP, int MODE, int MINW = 1>
+template <int VEC, int STRIP, int MODE, int MINW = 1, int PD = 1>
 static void launch(const uint8_t* x, uint8_t* y, int64_t H, int64_t W, hipStream_t s) {
     Taps2<5, 5> t = {};
     for (int m = 0; m < 5; ++m)
@@ -38,8 +38,12 @@ static void launch(const uint8_t* x, uint8_t* y, int64_t H, int64_t W, hipStream
         t.rowp[p] = ((uint32_t)g_row[4 - 2 * p] & 0xFFFFu) | ((uint32_t)(3 - 2 * p >= 0 ? g_row[3 - 2 * p] : 0) << 16);
     for (int p = 0; p < 3; ++p)
         t.colp[p] = ((uint32_t)g_col[2 * p] & 0xFFFFu) | ((uint32_t)(2 * p + 1 < 5 ? g_col[2 * p + 1] : 0) << 16);
+    if ((MODE & kMode2dPk16) && !(plan_pk16(t, g_col, g_row, 12) & kMode2dPk16)) {
+        fprintf(stderr, "pk16 not applicable\n");
+        exit(1);
+    }
     const dim3 grid = fir2d_reg_grid<VEC, STRIP>(H, W);
-    hipLaunchKernelGGL((fir2d_reg_kernel<5, 5, FIR_OUT_U8_SAT, VEC, STRIP, MODE, MINW>), grid, dim3(kBlock), 0, s, x, y, H,
+    hipLaunchKernelGGL((fir2d_reg_kernel<5, 5, FIR_OUT_U8_SAT, VEC, STRIP, MODE, MINW, PD>), grid, dim3(kBlock), 0, s, x, y, H,
                        W, t, 0, 12);
 }
 
@@ -72,19 +76,17 @@ int main(int argc, char** argv) {
     hipStream_t st;
     CK(hipStreamCreate(&st));
     std::vector<V> vs = {
-        {"dot2+nowrap vec16 s8", launch<16, 8, kMode2dDot2 | kMode2dNoWrap>, {}},
-        {"sep vec16 s16", launch<16, 16, kMode2dSep>, {}},
-        {"sep+nowrap vec16 s16", launch<16, 16, kMode2dSep | kMode2dNoWrap>, {}},
-        {"sep16 vec16 s16", launch<16, 16, kMode2dSep | kMode2dSep16>, {}},
-        {"sep16+nowrap vec16 s16", launch<16, 16, kMode2dSep | kMode2dSep16 | kMode2dNoWrap>, {}},
-        {"sep16+nowrap vec16 s8", launch<16, 8, kMode2dSep | kMode2dSep16 | kMode2dNoWrap>, {}},
-        {"sep16+nowrap vec8 s16", launch<8, 16, kMode2dSep | kMode2dSep16 | kMode2dNoWrap>, {}},
-        {"sep16+nowrap vec16 s24", launch<16, 24, kMode2dSep | kMode2dSep16 | kMode2dNoWrap>, {}},
-        {"sep16+nw v16 s16 w4", launch<16, 16, kMode2dSep | kMode2dSep16 | kMode2dNoWrap, 4>, {}},
-        {"sep16+nw v16 s32 w4", launch<16, 32, kMode2dSep | kMode2dSep16 | kMode2dNoWrap, 4>, {}},
-        {"sep16+nw v8 s32 w4", launch<8, 32, kMode2dSep | kMode2dSep16 | kMode2dNoWrap, 4>, {}},
-        {"dot2+nw v16 s8 w4", launch<16, 8, kMode2dDot2 | kMode2dNoWrap, 4>, {}},
-        {"dot2+nw v8 s16 w4", launch<8, 16, kMode2dDot2 | kMode2dNoWrap, 4>, {}},
+        {"sep16 v16 s16 pd1", launch<16, 16, kMode2dSep | kMode2dSep16 | kMode2dNoWrap, 1, 1>, {}},
+        {"sep16 v16 s16 pd3", launch<16, 16, kMode2dSep | kMode2dSep16 | kMode2dNoWrap, 1, 3>, {}},
+        {"pk16hi8 v16 s16 pd1", launch<16, 16, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 1>, {}},
+        {"pk16hi8 v16 s16 pd2", launch<16, 16, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 2>, {}},
+        {"pk16hi8 v16 s16 pd3", launch<16, 16, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 3>, {}},
+        {"pk16hi8 v16 s32 pd3", launch<16, 32, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 3>, {}},
+        {"pk16hi8 v16 s8 pd2", launch<16, 8, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 2>, {}},
+        {"pk16hi8 v8 s16 pd3", launch<8, 16, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 3>, {}},
+        {"pk16hi8 v8 s32 pd3", launch<8, 32, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 3>, {}},
+        {"pk16 v16 s16 pd3", launch<16, 16, kMode2dSep | kMode2dPk16 | kMode2dNoWrap, 1, 3>, {}},
+        {"pk16 v8 s16 pd3", launch<8, 16, kMode2dSep | kMode2dPk16 | kMode2dNoWrap, 1, 3>, {}},
     };
     auto ref = [&](int64_t i, int64_t j) {
         uint32_t a = 0;

@@ -22,6 +22,10 @@ constexpr int kVec2d = 16;       // separable path: 16 pixels per lane, 16-row s
 constexpr int kStrip2dSep = 16;
 constexpr int kVec2dGen = 8;     // general (dot2) path: 8 pixels per lane, 16-row strips, <= 128
 constexpr int kStrip2dGen = 16;  // VGPRs (4 waves/SIMD): 45.8 vs 48.5 us for 16 px x 8 rows
+// input rows loaded this many rows ahead (8192^2 frame: separable 32.9 -> 31.0 us at 3,
+// packed-16 25.7 -> 23.9 us at 3, general dot2 45.5 -> 43.9 us at 2; profiles/r01/micro2d_pk16.txt)
+constexpr int kPdSep = 3;
+constexpr int kPdGen = 2;
 
 // Generic: one output per thread, exact int64 sum, global loads (L1/L2 absorb the reuse).
 struct Taps2G {
@@ -126,25 +130,45 @@ static hipError_t launch2d_reg(const uint8_t* x, void* y, int64_t H, int64_t W, 
             t.colp[p] = ((uint32_t)lo & 0xFFFFu) | ((uint32_t)hi << 16);
         }
         constexpr int S16 = kMode2dSep | kMode2dSep16;
+        constexpr int SNW = kMode2dSep | kMode2dNoWrap;
+        // packed 16-bit pixel pairs when the whole sum provably fits 16 bits (u8 stage only)
+        if constexpr (STAGE == FIR_OUT_U8_SAT) {
+            const int pk = nowrap ? plan_pk16(t, t.col, rowt, frac) : 0;
+            if (pk == (kMode2dPk16 | kMode2dPkHi8)) {
+                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, SNW | kMode2dPk16 | kMode2dPkHi8, 1, kPdSep>),
+                                   grid, dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
+                return hipGetLastError();
+            }
+            if (pk == kMode2dPk16) {
+                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, SNW | kMode2dPk16, 1, kPdSep>), grid,
+                                   dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
+                return hipGetLastError();
+            }
+            if (pk == (kMode2dPk16 | kMode2dPkSigned)) {
+                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, SNW | kMode2dPk16 | kMode2dPkSigned, 1, kPdSep>),
+                                   grid, dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
+                return hipGetLastError();
+            }
+        }
         if (sep16 && nowrap)
-            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, S16 | kMode2dNoWrap>), grid,
+            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, S16 | kMode2dNoWrap, 1, kPdSep>), grid,
                                dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
         else if (sep16)
-            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, S16>), grid, dim3(kBlock), 0, s, x,
+            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, S16, 1, kPdSep>), grid, dim3(kBlock), 0, s, x,
                                (OutT*)y, H, W, t, 32 - acc_bits, frac);
         else if (nowrap)
-            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, kMode2dSep | kMode2dNoWrap>), grid,
+            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, kMode2dSep | kMode2dNoWrap, 1, kPdSep>), grid,
                                dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
         else
-            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, kMode2dSep>), grid, dim3(kBlock), 0, s,
+            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, kMode2dSep, 1, kPdSep>), grid, dim3(kBlock), 0, s,
                                x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
     } else {
         const dim3 grid = fir2d_reg_grid<kVec2dGen, kStrip2dGen>(H, W);
         if (nowrap)
-            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dGen, kStrip2dGen, kMode2dDot2 | kMode2dNoWrap, 4>),
+            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dGen, kStrip2dGen, kMode2dDot2 | kMode2dNoWrap, 4, kPdGen>),
                                grid, dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
         else
-            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dGen, kStrip2dGen, kMode2dDot2, 4>), grid,
+            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dGen, kStrip2dGen, kMode2dDot2, 4, kPdGen>), grid,
                                dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
     }
     return hipGetLastError();

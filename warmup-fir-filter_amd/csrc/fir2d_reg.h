@@ -8,8 +8,8 @@
 // 0 / 63 load one dword of the neighbouring wave's pixels); the vertical (R-1)-row halo is a
 // register ring of R partial output rows: each input row is loaded once per STRIP-row strip
 // and scattered into the R output rows it feeds (input-stationary).  Strips overlap by R-1
-// input rows (served from the Infinity Cache).  The next input row is loaded before the
-// current one is consumed.
+// input rows (served from the Infinity Cache).  Input rows are loaded PD rows ahead of the
+// one being consumed.
 #pragma once
 
 #include "fir_common.h"
@@ -26,6 +26,12 @@ struct Taps2 {
     int32_t col[R];
     // SEP16 form: column taps packed in pairs (col[2p], col[2p+1]) for v_dot2 over row-sum pairs
     uint32_t colp[(R + 1) / 2];
+    // PK16 form (h = 2^s * colq[m] * rowq[n]): every tap replicated into both 16-bit halves,
+    // rowb[i] = rowq[C-1-i] (multiplies window pixel j+i of output j), colb[m] = colq[m];
+    // pkbias = 2^(f-1-s) and pkshift = f-s in both halves, pkmax = 255 in both halves
+    uint32_t rowb[C];
+    uint32_t colb[R];
+    uint32_t pkbias, pkshift, pkmax;
 };
 
 // 2-D kernel arithmetic: general 5x5 on v_mad_i32_i24 / packed v_dot2, or rank-1 separable
@@ -36,7 +42,48 @@ struct Taps2 {
 // kMode2dSep16 (with kMode2dSep): the row sums fit int16 (255 * sum|row| <= 32767, host-checked),
 // so two consecutive rows' sums pack into one dword and the column pass is (R+1)/2 v_dot2 per
 // output pixel instead of R v_mad_i32_i24.
-enum Fir2dMode : int { kMode2dMad = 0, kMode2dDot2 = 1, kMode2dSep = 2, kMode2dNoWrap = 4, kMode2dSep16 = 8 };
+// kMode2dPk16 (with kMode2dSep, u8 stage): the host proved that the final sum
+// V = 2^(f-1-s) + sum colq*rowq*x of every pixel lies in [0, 2^16) (unsigned) or, with
+// kMode2dPkSigned, in [-2^15, 2^15).  Both passes then run on packed 16-bit v_pk_mad_u16 over
+// pixel PAIRS, exact mod 2^16 (so intermediate row sums may wrap), and the u8 stage is
+// (V >> (f-s)) clamped to [0, 255] = sat((2^s V_true + 2^(f-1)) >> f), the reference's value.
+// kMode2dPkHi8: unsigned with f-s == 8, the output byte is V's high byte (one v_perm per 4 px).
+enum Fir2dMode : int {
+    kMode2dMad = 0,
+    kMode2dDot2 = 1,
+    kMode2dSep = 2,
+    kMode2dNoWrap = 4,
+    kMode2dSep16 = 8,
+    kMode2dPk16 = 16,
+    kMode2dPkSigned = 32,
+    kMode2dPkHi8 = 64,
+};
+
+typedef unsigned short fir_u16x2 __attribute__((ext_vector_type(2)));
+typedef short fir_i16x2 __attribute__((ext_vector_type(2)));
+
+// a * b + c in each 16-bit half, mod 2^16 (v_pk_mad_u16)
+__device__ __forceinline__ uint32_t pk_mad16(uint32_t a, uint32_t b, uint32_t c) {
+    const fir_u16x2 r = __builtin_bit_cast(fir_u16x2, a) * __builtin_bit_cast(fir_u16x2, b) + __builtin_bit_cast(fir_u16x2, c);
+    return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ uint32_t pk_mul16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(fir_u16x2, a) * __builtin_bit_cast(fir_u16x2, b));
+}
+// u8 stage of two packed sums: (V >> k) clamped to [0, 255] in each half (signed or unsigned V)
+template <bool SIGNED>
+__device__ __forceinline__ uint32_t pk_stage_u8(uint32_t v, uint32_t k2, uint32_t max2) {
+    if constexpr (SIGNED) {
+        fir_i16x2 a = __builtin_bit_cast(fir_i16x2, v) >> __builtin_bit_cast(fir_i16x2, k2);
+        a = __builtin_elementwise_max(a, (fir_i16x2){0, 0});
+        a = __builtin_elementwise_min(a, __builtin_bit_cast(fir_i16x2, max2));
+        return __builtin_bit_cast(uint32_t, a);
+    } else {
+        fir_u16x2 a = __builtin_bit_cast(fir_u16x2, v) >> __builtin_bit_cast(fir_u16x2, k2);
+        a = __builtin_elementwise_min(a, __builtin_bit_cast(fir_u16x2, max2));
+        return __builtin_bit_cast(uint32_t, a);
+    }
+}
 
 template <int R, int C>
 inline void pack_taps2(Taps2<R, C>& t) {
@@ -46,6 +93,49 @@ inline void pack_taps2(Taps2<R, C>& t) {
             const int hi = (C - 2 - 2 * p) >= 0 ? t.h[m][C - 2 - 2 * p] : 0;
             t.p2[m][p] = ((uint32_t)lo & 0xFFFFu) | ((uint32_t)hi << 16);
         }
+}
+
+// PK16 planning (host): given an exact factorisation h[m][n] == col[m] * row[n], move the
+// largest power of two 2^s (s <= frac - 1) common to all taps into the shift, check that the
+// final 16-bit sum V cannot leave [0, 2^16) (or [-2^15, 2^15) signed) for any u8 input, and
+// fill the PK16 tap fields.  Returns the extra mode bits (kMode2dPk16 | ...) or 0 if unusable.
+template <int R, int C>
+inline int plan_pk16(Taps2<R, C>& t, const int32_t* col, const int32_t* row, int frac) {
+    if (frac < 1 || frac > 22) return 0;
+    auto tz = [](int64_t v) {
+        int z = 0;
+        while (v != 0 && (v & 1) == 0 && z < 40) v >>= 1, ++z;
+        return v == 0 ? 40 : z;
+    };
+    int zc = 40, zr = 40;
+    for (int m = 0; m < R; ++m) zc = zc < tz(col[m]) ? zc : tz(col[m]);
+    for (int n = 0; n < C; ++n) zr = zr < tz(row[n]) ? zr : tz(row[n]);
+    if (zc >= 40 || zr >= 40) return 0;  // an all-zero factor: leave it to the other paths
+    int s = zc + zr < frac - 1 ? zc + zr : frac - 1;
+    const int sc = s < zc ? s : zc, sr = s - sc;
+    int64_t cq[R], rq[C], vmax = (int64_t)1 << (frac - 1 - s), vmin = vmax;
+    for (int m = 0; m < R; ++m) cq[m] = (int64_t)col[m] >> sc;
+    for (int n = 0; n < C; ++n) rq[n] = (int64_t)row[n] >> sr;
+    for (int m = 0; m < R; ++m)
+        for (int n = 0; n < C; ++n) {
+            const int64_t p = cq[m] * rq[n];
+            (p > 0 ? vmax : vmin) += 255 * p;
+        }
+    if (frac - s > 15) return 0;  // 16-bit shifts take the amount mod 16
+    int mode;
+    if (vmin >= 0 && vmax <= 65535)
+        mode = kMode2dPk16 | (frac - s == 8 ? kMode2dPkHi8 : 0);
+    else if (vmin >= -32768 && vmax <= 32767)
+        mode = kMode2dPk16 | kMode2dPkSigned;
+    else
+        return 0;
+    auto rep = [](int64_t v) { return ((uint32_t)v & 0xFFFFu) * 0x10001u; };
+    for (int i = 0; i < C; ++i) t.rowb[i] = rep(rq[C - 1 - i]);
+    for (int m = 0; m < R; ++m) t.colb[m] = rep(cq[m]);
+    t.pkbias = rep((int64_t)1 << (frac - 1 - s));
+    t.pkshift = rep(frac - s);
+    t.pkmax = rep(255);
+    return mode;
 }
 
 // Four clamped NOWRAP accumulators (each <= 256 * 2^frac - 1) -> four u8 in one dword: the
@@ -78,7 +168,7 @@ __device__ __forceinline__ void load_row_px(const uint8_t* __restrict__ p, bool 
     for (int i = 0; i < ND; ++i) d[i] = ok ? q[i] : 0u;
 }
 
-template <int R, int C, int STAGE, int VEC, int STRIP, int MODE, int MINW = 1>
+template <int R, int C, int STAGE, int VEC, int STRIP, int MODE, int MINW = 1, int PD = 1>
 __global__ __launch_bounds__(kBlock, MINW) void fir2d_reg_kernel(const uint8_t* __restrict__ x,
                                                            typename OutTraits<STAGE>::T* __restrict__ y, int64_t H,
                                                            int64_t W, Taps2<R, C> taps, int shl, int frac) {
@@ -116,31 +206,32 @@ __global__ __launch_bounds__(kBlock, MINW) void fir2d_reg_kernel(const uint8_t* 
 #pragma unroll
         for (int j = 0; j < VEC; ++j) acc[s][j] = acc0;
     uint32_t qr[R][VEC] = {}, rsprev[VEC] = {};  // SEP16: packed (rs_t, rs_t-1) ring and rs_t-1
+    constexpr bool PK16 = (MODE & 3) == kMode2dSep && (MODE & kMode2dPk16);
+    static_assert(!PK16 || STAGE == FIR_OUT_U8_SAT, "PK16 is a u8-stage form");
+    uint32_t rs2[R][VEC / 2] = {}, pko[VEC / 2] = {};  // PK16: row-sum pair ring, output pairs
 
     auto row_ptr = [&](int64_t row) { return x + (row < 0 ? 0 : (row >= H ? H - 1 : row)) * W; };
-    uint32_t cur[ND], hcur;
-    {
-        const int64_t row = r0 - TOP;
+    // input rows of the strip: row t is loaded PD steps before it is consumed (the unrolled
+    // array indices are compile-time, so only the PD + 1 live rows occupy registers)
+    uint32_t rows[T][ND], hrows[T];
+    auto load_row = [&](int t) {
+        const int64_t row = r0 - TOP + t;
         const bool rok = row >= 0 && row < H;
         const uint8_t* rp = row_ptr(row);
-        load_row_px<ND>(rp + colc, rok && active, cur);
+        load_row_px<ND>(rp + colc, rok && active, rows[t]);
         const uint32_t hv = *reinterpret_cast<const uint32_t*>(rp + hcol);
-        hcur = (hok && rok) ? hv : 0u;
-    }
+        hrows[t] = (hok && rok) ? hv : 0u;
+    };
+#pragma unroll
+    for (int t = 0; t < PD && t < T; ++t) load_row(t);
 
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         {
             const int s = t % R;
-            uint32_t nxt[ND] = {}, hnxt = 0;
-            if (t + 1 < T) {  // compile-time after the unroll
-                const int64_t row = r0 - TOP + t + 1;
-                const bool rok = row >= 0 && row < H;
-                const uint8_t* rp = row_ptr(row);
-                load_row_px<ND>(rp + colc, rok && active, nxt);
-                const uint32_t hv = *reinterpret_cast<const uint32_t*>(rp + hcol);
-                hnxt = (hok && rok) ? hv : 0u;
-            }
+            if (t + PD < T) load_row(t + PD);  // compile-time after the unroll
+            const uint32_t* cur = rows[t];
+            const uint32_t hcur = hrows[t];
             if constexpr ((MODE & 3) != kMode2dMad) {
                 // byte stream: [left-halo dword | own dwords | right-halo dword]; window pixel i
                 // is stream byte i + (4 - HLE).  P[k] = (w[k], w[k+1]) as int16 halves.
@@ -166,6 +257,28 @@ __global__ __launch_bounds__(kBlock, MINW) void fir2d_reg_kernel(const uint8_t* 
                             for (int p = 1; p < (C + 1) / 2; ++p) a = dot2_acc(P[j + 2 * p], taps.p2[m][p], a);
                             acc[slot][j] = a;
                         }
+                    }
+                } else if constexpr (PK16) {  // pixel pairs (j, j+1) on packed 16-bit MACs
+                    // tap-outer loops: the VEC/2 independent chains interleave (a dependent
+                    // v_pk_mad right after its producer costs an s_nop on gfx950)
+                    uint32_t* r = rs2[t % R];
+#pragma unroll
+                    for (int q = 0; q < VEC / 2; ++q) r[q] = pk_mul16(P[2 * q], taps.rowb[0]);
+#pragma unroll
+                    for (int i = 1; i < C; ++i)
+#pragma unroll
+                        for (int q = 0; q < VEC / 2; ++q) r[q] = pk_mad16(P[2 * q + i], taps.rowb[i], r[q]);
+                    if (t >= R - 1) {  // output t-(R-1) = bias + sum_m colq[m] rs_{t-m}
+#pragma unroll
+                        for (int q = 0; q < VEC / 2; ++q) pko[q] = pk_mad16(r[q], taps.colb[0], taps.pkbias);
+#pragma unroll
+                        for (int m = 1; m < R; ++m)
+#pragma unroll
+                            for (int q = 0; q < VEC / 2; ++q) pko[q] = pk_mad16(rs2[(t - m) % R][q], taps.colb[m], pko[q]);
+                        // keep the column pass here, interleaved: sunk into the store's branch
+                        // the compiler serialises its chains (an s_nop per dependent v_pk_mad)
+#pragma unroll
+                        for (int q = 0; q < VEC / 2; ++q) asm volatile("" : "+v"(pko[q]));
                     }
                 } else if constexpr (SEP16) {  // int16 row sums packed with the previous row's
 #pragma unroll
@@ -236,7 +349,16 @@ __global__ __launch_bounds__(kBlock, MINW) void fir2d_reg_kernel(const uint8_t* 
                         vN val;
 #pragma unroll
                         for (int i = 0; i < ND; ++i) {
-                            if constexpr (NOWRAP) {
+                            if constexpr (PK16) {  // pairs (4i, 4i+1), (4i+2, 4i+3) -> 4 bytes
+                                if constexpr ((MODE & kMode2dPkHi8) != 0) {
+                                    val[i] = __builtin_amdgcn_perm(pko[2 * i + 1], pko[2 * i], 0x07050301u);
+                                } else {
+                                    constexpr bool SG = (MODE & kMode2dPkSigned) != 0;
+                                    const uint32_t lo = pk_stage_u8<SG>(pko[2 * i], taps.pkshift, taps.pkmax);
+                                    const uint32_t hi = pk_stage_u8<SG>(pko[2 * i + 1], taps.pkshift, taps.pkmax);
+                                    val[i] = __builtin_amdgcn_perm(hi, lo, 0x06040200u);
+                                }
+                            } else if constexpr (NOWRAP) {
                                 const uint32_t* a4 = &acc[slot][4 * i];
                                 val[i] = pack4_shifted(clamp_u8_acc(a4[0], sat_hi), clamp_u8_acc(a4[1], sat_hi),
                                                        clamp_u8_acc(a4[2], sat_hi), clamp_u8_acc(a4[3], sat_hi), frac);
@@ -261,9 +383,6 @@ __global__ __launch_bounds__(kBlock, MINW) void fir2d_reg_kernel(const uint8_t* 
                     }
                 }
             }
-#pragma unroll
-            for (int i = 0; i < ND; ++i) cur[i] = nxt[i];
-            hcur = hnxt;
         }
     }
 }
