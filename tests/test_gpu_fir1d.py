@@ -318,6 +318,33 @@ def test_multi_filter_random_vs_oracle(F, dtype, L):
             assert np.array_equal(ys[f], fo.fir1d_rows(x, hq[f], 12, 32, stage)), (f, stage)
 
 
+@pytest.mark.parametrize("width", [1283, 4096, 640])
+@pytest.mark.parametrize("frac", [12, 8, 15, 20])
+def test_multi_filter_packed16_forms_vs_oracle(width, frac):
+    """u8 banks whose filters fit the packed-16 form (taps = small ints x 2^s): unsigned,
+    signed, high-byte and v_dot2 filters mixed in one fused launch, bit-exact."""
+    rng = np.random.default_rng(width + frac)
+    x = rng.integers(0, 256, (37, width), dtype=np.uint8)
+    x[0, :] = 255  # extremes of every sum
+    x[1, :] = 0
+    x[2, ::2] = 255
+    for L in (2, 3, 5, 9):
+        for trial in range(4):
+            F = int(rng.integers(2, 5))
+            small = rng.integers(-12, 13, (F, L))
+            small[0] = np.abs(small[0])  # an unsigned-sum filter
+            shifts = rng.integers(0, frac, (F, 1))
+            hq = small << shifts
+            hq[-1] = rng.integers(-3000, 3000, L) | 1  # odd taps: the v_dot2 form
+            for f in range(F):
+                if not hq[f].any():
+                    hq[f, 0] = 1 << int(shifts[f, 0])
+            for stage in (fir_hip.OUT_U8_SAT, fir_hip.OUT_I32):
+                ys = fir_hip.fir1d_fixed_rows_multi(x, hq, frac, 32, stage)
+                for f in range(F):
+                    assert np.array_equal(ys[f], fo.fir1d_rows(x, hq[f], frac, 32, stage)), (L, trial, f, stage)
+
+
 def test_generator_over_golden_images_uses_fused_path(tmp_path, images, image_outputs):
     inp = tmp_path / "input"
     inp.mkdir()

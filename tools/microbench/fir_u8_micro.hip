@@ -1,7 +1,8 @@
 // fir_u8_micro.hip — A/B microbenchmark for the 1:1 u8 -> sat-u8 path (dev tool, not the
 // product): fir1d_reg_kernel<u8, U8_SAT, 5> with U chunks per wave over 2^28 samples in
-// 4096-sample rows, next to plain 16-byte copies with the same layouts and hipMemcpy.
-// Every FIR variant's full output is checked against a CPU evaluation.
+// 4096-sample rows, next to plain 16-byte copies with the same layouts and hipMemcpy; and
+// the fused 4-filter 3-tap bank (1 B in, 4 B out per sample), byte-pair v_dot2 vs the
+// per-filter packed-16 form.  Every FIR variant's full output is checked against a CPU evaluation.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -26,15 +27,39 @@ using namespace fir;
 static const int32_t kTaps[5] = {-256, -1024, 6656, -1024, -256};
 static const int64_t kW = 4096;
 
-template <int U, int FLAGS>
+template <int U, int FLAGS, bool ONEROW = false>
 static void launch_fir(const uint8_t* x, uint8_t* y, int64_t n, hipStream_t s) {
-    RowGeom g{n, (uint32_t)kW, 1, 1};
+    RowGeom g{n, ONEROW ? 0u : (uint32_t)kW, ONEROW ? 0 : 1, 1};
     TapsN<5> t;
     for (int k = 0; k < 5; ++k) t.h[0][k] = kTaps[k];
     pack_taps(t);
+    if ((FLAGS & kU8Pk16) && plan_u8_pk16(t, 12) != (FLAGS & (kU8Pk16 | kU8PkHi8))) {
+        fprintf(stderr, "pk16 plan mismatch\n");
+        exit(1);
+    }
     int64_t ntiles, blocks;
     reg_launch_geometry<uint8_t, U, FLAGS>(n, 2048, &ntiles, &blocks);
     hipLaunchKernelGGL((fir1d_reg_kernel<uint8_t, FIR_OUT_U8_SAT, 5, 1, U, FLAGS>), dim3((unsigned)blocks),
+                       dim3(kBlock), 0, s, x, y, g, t, 0, 12, ntiles);
+}
+
+// BANK3 of the reference (h_coeff.py): moving_avg, simple_lp, edge, sharpen in Q4.12
+static const int32_t kBank[4][3] = {{1365, 1365, 1365}, {1024, 2048, 1024}, {-4096, 0, 4096}, {-512, 5120, -512}};
+
+template <int U, int FLAGS>
+static void launch_bank(const uint8_t* x, uint8_t* y, int64_t n, hipStream_t s) {
+    RowGeom g{n, (uint32_t)kW, 1, 1};
+    TapsN<3, 4> t;
+    for (int f = 0; f < 4; ++f)
+        for (int k = 0; k < 3; ++k) t.h[f][k] = kBank[f][k];
+    pack_taps(t);
+    if ((FLAGS & kU8Pk16) && plan_u8_pk16(t, 12) != kU8Pk16) {
+        fprintf(stderr, "bank pk16 plan mismatch\n");
+        exit(1);
+    }
+    int64_t ntiles, blocks;
+    reg_launch_geometry<uint8_t, U, FLAGS>(n, 2048, &ntiles, &blocks);
+    hipLaunchKernelGGL((fir1d_reg_kernel<uint8_t, FIR_OUT_U8_SAT, 3, 1, U, FLAGS, 4>), dim3((unsigned)blocks),
                        dim3(kBlock), 0, s, x, y, g, t, 0, 12, ntiles);
 }
 
@@ -61,7 +86,7 @@ static void launch_memcpy(const uint8_t* x, uint8_t* y, int64_t n, hipStream_t s
 
 struct V {
     std::string name;
-    bool fir;
+    int kind;  // 0 copy (unchecked), 1 single filter, 2 four-filter bank
     void (*fn)(const uint8_t*, uint8_t*, int64_t, hipStream_t);
     std::vector<float> us;
 };
@@ -69,44 +94,61 @@ struct V {
 int main(int argc, char** argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 15;
     const int64_t n = (int64_t)1 << 28;
-    std::vector<uint8_t> hx(n), ref(n), got(n);
+    std::vector<uint8_t> hx(n), ref(n), refb(4 * n), got(4 * n);
     uint64_t s = 88172645463325252ull;
     for (auto& v : hx) {
         s ^= s << 13, s ^= s >> 7, s ^= s << 17;
         v = (uint8_t)s;
     }
-    for (int64_t i = 0; i < n; ++i) {
+    auto fir = [&](const int32_t* h, int L, int64_t i) {
         const int64_t r = i / kW, c = i % kW;
         int64_t acc = 0;
-        for (int k = 0; k < 5; ++k) {
-            const int64_t j = c - k + 2;
-            if (j >= 0 && j < kW) acc += (int64_t)kTaps[k] * hx[r * kW + j];
+        for (int k = 0; k < L; ++k) {
+            const int64_t j = c - k + L / 2;
+            if (j >= 0 && j < kW) acc += (int64_t)h[k] * hx[r * kW + j];
         }
         const int64_t q = (acc + 2048) >> 12;
-        ref[i] = (uint8_t)(q < 0 ? 0 : q > 255 ? 255 : q);
+        return (uint8_t)(q < 0 ? 0 : q > 255 ? 255 : q);
+    };
+    for (int64_t i = 0; i < n; ++i) {
+        ref[i] = fir(kTaps, 5, i);
+        for (int f = 0; f < 4; ++f) refb[f * n + i] = fir(kBank[f], 3, i);
     }
     uint8_t *dx, *dy;
     CK(hipMalloc(&dx, n));
-    CK(hipMalloc(&dy, n));
+    CK(hipMalloc(&dy, 4 * n));
     CK(hipMemcpy(dx, hx.data(), n, hipMemcpyHostToDevice));
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    std::vector<V> vs = {{"fir U1", true, launch_fir<1, kU8Dot2>, {}},
-                         {"fir U2", true, launch_fir<2, kU8Dot2>, {}},
-                         {"fir U4", true, launch_fir<4, kU8Dot2>, {}},
-                         {"fir U1 persist", true, launch_fir<1, kU8Dot2 | kPersist>, {}},
-                         {"copy16 U1", false, launch_copy<1>, {}},
-                         {"copy16 U2", false, launch_copy<2>, {}},
-                         {"copy16 U4", false, launch_copy<4>, {}},
-                         {"hipMemcpy D2D", false, launch_memcpy, {}}};
+    constexpr int PK = kU8Dot2 | kU8Pk16;
+    std::vector<V> vs = {{"fir U1", 1, launch_fir<1, kU8Dot2>, {}},
+                         {"fir U2", 1, launch_fir<2, kU8Dot2>, {}},
+                         {"fir U4", 1, launch_fir<4, kU8Dot2>, {}},
+                         {"pk16 U1", 1, launch_fir<1, PK>, {}},
+                         {"pk16 U2", 1, launch_fir<2, PK>, {}},
+                         {"pk16 U4", 1, launch_fir<4, PK>, {}},
+                         {"bank dot2 U1", 2, launch_bank<1, kU8Dot2>, {}},
+                         {"bank dot2 U2", 2, launch_bank<2, kU8Dot2>, {}},
+                         {"bank pk16 U1", 2, launch_bank<1, PK>, {}},
+                         {"bank pk16 U2", 2, launch_bank<2, PK>, {}},
+                         {"copy16 U1", 0, launch_copy<1>, {}},
+                         {"copy16 U2", 0, launch_copy<2>, {}},
+                         {"copy16 U4", 0, launch_copy<4>, {}},
+                         {"hipMemcpy D2D", 0, launch_memcpy, {}}};
     for (auto& v : vs) {
-        if (!v.fir) continue;
-        CK(hipMemset(dy, 0x5A, n));
+        if (v.kind == 0) continue;
+        const int64_t nb = v.kind == 2 ? 4 * n : n;
+        CK(hipMemset(dy, 0x5A, nb));
+        CK(hipDeviceSynchronize());  // the memset runs on the null stream, st is non-blocking
         v.fn(dx, dy, n, st);
         CK(hipStreamSynchronize(st));
-        CK(hipMemcpy(got.data(), dy, n, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(got.data(), dy, nb, hipMemcpyDeviceToHost));
+        const uint8_t* r = v.kind == 2 ? refb.data() : ref.data();
         int64_t bad = 0;
-        for (int64_t i = 0; i < n; ++i) bad += got[i] != ref[i];
+        for (int64_t i = 0; i < nb; ++i)
+            if (got[i] != r[i] && bad++ < 6)
+                printf("  %s: [%lld] plane %lld col %lld: got %d want %d\n", v.name.c_str(), (long long)i,
+                       (long long)(i / n), (long long)(i % n % kW), got[i], r[i]);
         printf("check %-16s %s (%lld bad)\n", v.name.c_str(), bad ? "FAIL" : "ok", (long long)bad);
         if (bad) return 1;
     }
@@ -129,8 +171,9 @@ int main(int argc, char** argv) {
     for (auto& v : vs) {
         std::sort(v.us.begin(), v.us.end());
         const double med = v.us[v.us.size() / 2];
-        printf("%-20s %10.1f %10.1f %10.1f %8.1f\n", v.name.c_str(), med, v.us[0], 2.0 * n / med / 1e3,
-               2.0 * n / med / 1e3 / 80.0);
+        const double bytes = (v.kind == 2 ? 5.0 : 2.0) * n;
+        printf("%-20s %10.1f %10.1f %10.1f %8.1f\n", v.name.c_str(), med, v.us[0], bytes / med / 1e3,
+               bytes / med / 1e3 / 80.0);
     }
     return 0;
 }

@@ -34,6 +34,12 @@ enum RegFlags : int {
                    // 1 KiB store instructions (instead of 16 B per lane at a 16*VEC/4-byte stride)
     kXcd = 128,    // XCD-aware block order: the hardware deals consecutive blocks round-robin
                    // to the 8 XCDs; remap so each XCD (own L2) streams one contiguous eighth
+    // with kU8Dot2, u8 stage: filters whose V = 2^(f-1-s) + sum h'[k] x (h = 2^s h') provably
+    // stays in [0, 2^16) or [-2^15, 2^15) for every u8 input (plan_u8_pk16, TapsN::pkmode)
+    // compute their outputs in PAIRS on v_pk_mad_u16 (exact mod 2^16); u8 stage =
+    // clamp(V >> (f-s), 0, 255).  The other filters keep the byte-pair v_dot2 form.
+    kU8Pk16 = 256,
+    kU8PkHi8 = 1024,  // every filter unsigned with f - s == 8: the output byte is V's high byte
 };
 
 constexpr int kNumXcd = 8;
@@ -62,7 +68,54 @@ template <int L, int F = 1>
 struct TapsN {
     int32_t h[F][L];
     uint32_t pk[F][(L + 1) / 2];
+    // kU8Pk16: hb[f][i] = h'[f][L-1-i] (multiplies window byte i of an output) in both 16-bit
+    // halves; pkbias = 2^(f-1-s), pkshift = f - s, pkmax = 255, each in both halves
+    uint32_t hb[F][L];
+    uint32_t pkbias[F], pkshift[F], pkmax;
+    uint32_t pkmode[F];  // 0: v_dot2 form, 1: packed-16 unsigned V, 2: packed-16 signed V
 };
+
+// Packed-16 planning for the u8 stage (host).  Per filter: s = the largest power of two
+// common to its taps (s <= frac - 1, frac - s <= 15), h' = h / 2^s, and the range of
+// V = 2^(frac-1-s) + sum h' x over u8 x, decided per filter (pkmode).  Returns the flag bits
+// to add (0: no filter qualifies) and fills the packed fields.
+template <int L, int F>
+inline int plan_u8_pk16(TapsN<L, F>& t, int frac) {
+    int any = 0;
+    for (int f = 0; f < F; ++f) t.pkmode[f] = 0;
+    t.pkmax = 0x00FF00FFu;
+    if (frac < 1 || frac > 22) return 0;
+    for (int f = 0; f < F; ++f) {
+        int s = 40;
+        for (int k = 0; k < L; ++k) {
+            int64_t v = t.h[f][k];
+            int z = 0;
+            if (v == 0) continue;
+            while ((v & 1) == 0) v >>= 1, ++z;
+            s = z < s ? z : s;
+        }
+        if (s == 40) continue;  // an all-zero filter keeps the dot2 form
+        s = s < frac - 1 ? s : frac - 1;
+        if (frac - s > 15) continue;  // 16-bit shifts take the amount mod 16
+        int64_t vmax = (int64_t)1 << (frac - 1 - s), vmin = vmax;
+        for (int k = 0; k < L; ++k) {
+            const int64_t hp = (int64_t)t.h[f][k] >> s;
+            (hp > 0 ? vmax : vmin) += 255 * hp;
+        }
+        const bool u = vmin >= 0 && vmax <= 65535, sg = vmin >= -32768 && vmax <= 32767;
+        if (!u && !sg) continue;
+        t.pkmode[f] = u ? 1u : 2u;
+        ++any;
+        auto rep = [](int64_t v) { return ((uint32_t)v & 0xFFFFu) * 0x10001u; };
+        for (int i = 0; i < L; ++i) t.hb[f][i] = rep((int64_t)t.h[f][L - 1 - i] >> s);
+        t.pkbias[f] = rep((int64_t)1 << (frac - 1 - s));
+        t.pkshift[f] = rep(frac - s);
+    }
+    if (!any) return 0;
+    bool hi8 = any == F;
+    for (int f = 0; f < F; ++f) hi8 &= t.pkmode[f] == 1 && t.pkshift[f] == 8u * 0x10001u;
+    return kU8Pk16 | (hi8 ? kU8PkHi8 : 0);
+}
 
 template <int L, int F>
 inline void pack_taps(TapsN<L, F>& t) {
@@ -152,6 +205,28 @@ __device__ __forceinline__ void store_vec(typename OutTraits<STAGE>::T* __restri
     }
 }
 
+// VEC u8 outputs already packed 4 per dword: one VEC-byte store, bytewise at the ragged end.
+template <int VEC, bool NT>
+__device__ __forceinline__ void store_u8_dwords(uint8_t* __restrict__ y, int64_t g0, int64_t total, bool full,
+                                                const uint32_t (&o)[VEC / 4]) {
+    if (full) {
+        if constexpr (VEC == 16) {
+            const u32x4 val = {o[0], o[1], o[2], o[3]};
+            u32x4* p = reinterpret_cast<u32x4*>(y + g0);
+            if (NT) __builtin_nontemporal_store(val, p); else *p = val;
+        } else {
+            const u32x2 val = {o[0], o[1]};
+            u32x2* p = reinterpret_cast<u32x2*>(y + g0);
+            if (NT) __builtin_nontemporal_store(val, p); else *p = val;
+        }
+    } else if (g0 < total) {
+        const int n = (int)min((int64_t)VEC, total - g0);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j)
+            if (j < n) y[g0 + j] = (uint8_t)(o[j / 4] >> (8 * (j % 4)));
+    }
+}
+
 // Sample pair (s, s+1) of the window as two int16 halves; window dword i holds samples
 // 2i - 2*NDL and 2i - 2*NDL + 1.  LAST_ZERO: the caller multiplies the high half by 0, so it
 // may come from outside the window.
@@ -219,6 +294,44 @@ struct U8Dot2Row {  // sum over tap pairs p >= P for output J, continuing from a
         }
     }
 };
+
+// Packed-16 u8 form: the window byte pairs (w[k], w[k+1]) for k = 0 .. VEC+L-3 (stream byte
+// K0 + k), shared by every output pair and filter.
+template <int NW, int K0, int N>
+struct BytePairs {
+    __device__ static __forceinline__ void run(const uint32_t* Wd, uint32_t* P) {
+        if constexpr (N > 0) {
+            P[0] = byte_pair<NW, K0>(Wd);
+            BytePairs<NW, K0 + 1, N - 1>::run(Wd, P + 1);
+        }
+    }
+};
+
+// Output pairs (2q, 2q+1) of one filter: bias + sum_i h'[L-1-i] * (w[2q+i], w[2q+1+i]) mod 2^16,
+// taps outer so the VEC/2 chains interleave; then the u8 stage and 4 bytes per dword.
+template <int L, int VEC, int FLAGS>
+__device__ __forceinline__ void u8_pk16_vec(const uint32_t* P, const uint32_t* hb, uint32_t bias, uint32_t k2,
+                                            uint32_t max2, bool sg, uint32_t (&o)[VEC / 4]) {
+    uint32_t a[VEC / 2];
+#pragma unroll
+    for (int q = 0; q < VEC / 2; ++q) a[q] = pk_mad16(P[2 * q], hb[0], bias);
+#pragma unroll
+    for (int i = 1; i < L; ++i)
+#pragma unroll
+        for (int q = 0; q < VEC / 2; ++q) a[q] = pk_mad16(P[2 * q + i], hb[i], a[q]);
+#pragma unroll
+    for (int d = 0; d < VEC / 4; ++d) {
+        if constexpr ((FLAGS & kU8PkHi8) != 0) {
+            o[d] = __builtin_amdgcn_perm(a[2 * d + 1], a[2 * d], 0x07050301u);
+        } else if (sg) {
+            o[d] = __builtin_amdgcn_perm(pk_stage_u8<true>(a[2 * d + 1], k2, max2),
+                                         pk_stage_u8<true>(a[2 * d], k2, max2), 0x06040200u);
+        } else {
+            o[d] = __builtin_amdgcn_perm(pk_stage_u8<false>(a[2 * d + 1], k2, max2),
+                                         pk_stage_u8<false>(a[2 * d], k2, max2), 0x06040200u);
+        }
+    }
+}
 
 // No-wrap u8 form: every chain starts at the rounding bias (a VGPR), the u8 stage is
 // v_med3 clamp then shift (sat_u8_pixel), the int32 stage one arithmetic shift.
@@ -293,6 +406,7 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
     constexpr bool DOT2 = (FLAGS & kDot2) && sizeof(InT) == 2 && CH == 1;
     constexpr bool ACC32 = FLAGS & kAcc32;
     constexpr bool U8DOT2 = (FLAGS & kU8Dot2) && sizeof(InT) == 1 && CH == 1;
+    constexpr bool U8PK = U8DOT2 && (FLAGS & kU8Pk16) && STAGE == FIR_OUT_U8_SAT;
     constexpr bool COAL = (FLAGS & kCoal) && STAGE == FIR_OUT_I32;
     constexpr int WPB = kBlock / kWave;
     uint32_t bias = 0;
@@ -382,8 +496,20 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
                     constexpr int off = NDL * EPD - HLE;
                     w[i] = IT::get(Wd[(off + i) / EPD], (off + i) % EPD);
                 }
+                uint32_t Pp[VEC + L - 2];  // U8PK: byte pairs of the window, shared by the filters
+                if constexpr (U8PK) BytePairs<NW, 4 * NDL - HLE, VEC + L - 2>::run(Wd, Pp);
 #pragma unroll
                 for (int f = 0; f < F; ++f) {
+                    if constexpr (U8PK) {
+                        const uint32_t md = taps.pkmode[f];  // wave-uniform
+                        if (__builtin_expect(interior, 1) && md != 0) {
+                            uint32_t o[VEC / 4];
+                            u8_pk16_vec<L, VEC, FLAGS>(Pp, taps.hb[f], taps.pkbias[f], taps.pkshift[f], taps.pkmax,
+                                                       md == 2, o);
+                            store_u8_dwords<VEC, NTS>(reinterpret_cast<uint8_t*>(y + f * total), g0, total, v < nvec, o);
+                            continue;
+                        }
+                    }
                     int32_t q[VEC];
                     if (__builtin_expect(interior, 1)) {
                         if constexpr (DOT2) {

@@ -17,9 +17,10 @@ namespace fir {
 // int32 outputs staged through LDS into whole 1 KiB store instructions (272 -> 257 us).
 // One u8 filter: 4 chunks per wave (the per-wave edge loads and row arithmetic amortised
 // over 4 KiB; 104.6 -> 94.0 us at 2^28, profiles/r01/micro_u8_chunks.txt); a fused bank
-// (F > 1) has 4x the math per byte and runs best at 1 chunk (248 vs 256 us for F = 4).
+// (F > 1) runs best at 2 chunks with its packed-16 filters (4-filter 3-tap bank: 259 us at 1
+// chunk on v_dot2, 229 us at 2 chunks with packed-16; profiles/r01/micro_u8_pk16.txt).
 template <typename InT, int F>
-constexpr int kRegU = sizeof(InT) == 1 && F == 1 ? 4 : 1;
+constexpr int kRegU = sizeof(InT) == 1 ? (F == 1 ? 4 : 2) : 1;
 constexpr int kRegFlags = kCoal;
 constexpr int kPersistBlocks = 2048;
 
@@ -36,6 +37,8 @@ static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t
     for (int f = 0; f < F; ++f)
         for (int k = 0; k < L; ++k) t.h[f][k] = hq[f * L + k];
     pack_taps(t);
+    if constexpr ((FL & kU8Pk16) != 0)
+        if (!(plan_u8_pk16(t, frac) & kU8Pk16)) return hipErrorInvalidValue;  // caller checked
     int64_t ntiles = 0, blocks = 0;
     reg_launch_geometry<InT, kRegU<InT, F>, FL>(total, kPersistBlocks, &ntiles, &blocks);
     hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, kRegU<InT, F>, FL, F>), dim3((unsigned)blocks), dim3(kBlock), 0,
@@ -58,6 +61,14 @@ static hipError_t launch_reg(const void* x, void* y, int64_t rows, int64_t total
             int64_t habs = 0;
             for (int k = 0; k < L; ++k) habs += hq[f * L + k] < 0 ? -(int64_t)hq[f * L + k] : hq[f * L + k];
             nowrap &= 255 * habs + ((int64_t)1 << (frac - 1)) < ((int64_t)1 << (acc_bits - 1));
+        }
+        if constexpr (F > 1 && STAGE == FIR_OUT_U8_SAT) {
+            // a bank: filters whose 16-bit sum provably cannot overflow run on packed pairs
+            TapsN<L, F> probe;
+            for (int k = 0; k < F * L; ++k) probe.h[k / L][k % L] = hq[k];
+            if (taps16 && nowrap && (plan_u8_pk16(probe, frac) & kU8Pk16))
+                return launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kU8Dot2 | kU8Pk16>(x, y, rows, total, rowlen, hq,
+                                                                                          frac, acc_bits, stream);
         }
         if (taps16 && nowrap)
             return launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kU8Dot2>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream);

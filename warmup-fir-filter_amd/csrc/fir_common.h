@@ -164,4 +164,32 @@ __device__ __forceinline__ uint32_t sat_u8_pixel(uint32_t acc, int shl, int frac
     }
 }
 
+// Packed 16-bit pixel-pair arithmetic (v_pk_mad_u16: exact mod 2^16 in each half), shared by
+// the 1-D u8 and 2-D packed-16 forms.
+typedef unsigned short fir_u16x2 __attribute__((ext_vector_type(2)));
+typedef short fir_i16x2 __attribute__((ext_vector_type(2)));
+
+// a * b + c in each 16-bit half, mod 2^16 (v_pk_mad_u16)
+__device__ __forceinline__ uint32_t pk_mad16(uint32_t a, uint32_t b, uint32_t c) {
+    const fir_u16x2 r = __builtin_bit_cast(fir_u16x2, a) * __builtin_bit_cast(fir_u16x2, b) + __builtin_bit_cast(fir_u16x2, c);
+    return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ uint32_t pk_mul16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(fir_u16x2, a) * __builtin_bit_cast(fir_u16x2, b));
+}
+// u8 stage of two packed sums: (V >> k) clamped to [0, 255] in each half (signed or unsigned V)
+template <bool SIGNED>
+__device__ __forceinline__ uint32_t pk_stage_u8(uint32_t v, uint32_t k2, uint32_t max2) {
+    if constexpr (SIGNED) {
+        fir_i16x2 a = __builtin_bit_cast(fir_i16x2, v) >> __builtin_bit_cast(fir_i16x2, k2);
+        a = __builtin_elementwise_max(a, (fir_i16x2){0, 0});
+        a = __builtin_elementwise_min(a, __builtin_bit_cast(fir_i16x2, max2));
+        return __builtin_bit_cast(uint32_t, a);
+    } else {
+        fir_u16x2 a = __builtin_bit_cast(fir_u16x2, v) >> __builtin_bit_cast(fir_u16x2, k2);
+        a = __builtin_elementwise_min(a, __builtin_bit_cast(fir_u16x2, max2));
+        return __builtin_bit_cast(uint32_t, a);
+    }
+}
+
 }  // namespace fir
