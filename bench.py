@@ -5,7 +5,8 @@ Default workload (BASELINE.json configs[1]; configs[3] at --gpus 8): 5-tap int16
 FIR-1D (Q4.12 "sharpen" taps [-256,-1024,6656,-1024,-256], 32-bit wrap, round, no
 saturation) over 2^28 synthetic samples PER GPU (weak scaling: 2^31 samples on 8 GPUs),
 inputs resident in HBM before the timed region.  For N > 1 each rank owns one contiguous
-segment and a step includes the 2+2-sample halo exchange over RCCL plus the edge kernel.
+segment; a step is the bulk kernel plus the edge kernel, which reads the 2+2-sample halo
+from the neighbours' HBM over xGMI (mapped once; FIR_HALO=rccl: RCCL send/recv every step).
 
 Contract: `python bench.py --gpus N --steps K --warmup W` (torchrun for N > 1); rank 0
 prints ONE JSON line.  Extra keys:
@@ -54,6 +55,13 @@ SIMPLE_LP5 = [256, 1024, 1536, 1024, 256]    # h_coeff_5tap_map["simple_lp"] in 
 SHARPEN5_F64 = [-1 / 16, -4 / 16, 26 / 16, -4 / 16, -1 / 16]  # h_coeff_5tap_map["sharpen"]
 BANK3 = [[1365] * 3, [1024, 2048, 1024], [-4096, 0, 4096], [-512, 5120, -512]]  # h_coeff_3tap_map, Q4.12
 ROW_W = 4096
+# FIR_SELF_HALO=1 (N = 1 only): post the RCCL halo exchange every step with the segment as its
+# own neighbour (a ring of one), so the sharded step's exchange + edge kernel run and are timed
+# on a single GPU.  Rehearsal only; the JSON line says so in config.rehearsal.
+SELF_HALO = os.environ.get("FIR_SELF_HALO") == "1"
+# N > 1 halo source: "xgmi" (default: neighbours' HBM mapped once, read by the edge kernel) or
+# "rccl" (send/recv every step); xgmi falls back to rccl on every rank if any rank cannot map.
+HALO_PREF = os.environ.get("FIR_HALO", "xgmi")
 KERNELS = {"fir1d_i16": "fir1d_reg_kernel", "cplx_i16": "fir1d_reg_kernel", "fir2d_u8": "fir2d_reg_kernel",
            "fir1d_u8": "fir1d_reg_kernel", "ideal_u8": "fir1d_ideal_kernel", "bank_u8": "fir1d_reg_kernel",
            "restore_u8": "restore_map_kernel", "metrics_u8": "metrics_pass1+2"}
@@ -87,8 +95,7 @@ class Workload:
             self.dtype = "int32 (int16 in, int32 wrap-around acc, int32 out)"
             self.config = {"workload": "fir1d_int16_int32_5tap_sharpen_q4.12", "samples_per_gpu": self.n,
                            "total_samples": self.n * world, "taps": 5, "frac_bits": 12, "acc_bits": 32,
-                           "parallelism": f"contiguous shards x{world}, 2+2-sample halo over RCCL" if world > 1
-                           else "single GPU"}
+                           "parallelism": "single GPU"}  # sharded runs: set by the first step
         elif name == "cplx_i16":
             self.n = 1 << (log2n - 1)  # complex samples
             self.taps = torch_ops.Taps(SIMPLE_LP3)
@@ -168,11 +175,13 @@ class Workload:
         else:
             u8 = name in ("fir2d_u8", "fir1d_u8")
             self.y = torch.empty(self.x.shape, dtype=torch.uint8 if u8 else torch.int32, device=dev)
-        self.left = self.right = None
+        self.left = self.right = None  # the halos the last step used (host copies for the oracle)
+        self.halo_src, self.halo_kind = None, None
 
     @property
     def sharded_1d(self) -> bool:
-        return self.world > 1 and self.name in ("fir1d_i16", "cplx_i16")
+        # FIR_SELF_HALO=1 rehearses the RCCL exchange at N = 1 (the segment is its own neighbour)
+        return (self.world > 1 or SELF_HALO) and self.name in ("fir1d_i16", "cplx_i16")
 
     def bulk(self):
         if self.name == "fir2d_u8":
@@ -191,16 +200,33 @@ class Workload:
             torch_ops.fir1d_fixed_rows_dev(self.x, self.taps, 12, 32, fir_hip.OUT_I32, self.channels, out=self.y)
 
     def step(self):
-        """One pass of the hot path (for N > 1: halo exchange || bulk kernel, then edges)."""
-        sharded_1d = self.sharded_1d
-        works = []
-        if sharded_1d:
-            self.left, self.right, works = sharded.post_halo_exchange(self.x, self.taps.n, self.channels)
-        self.bulk()
-        if sharded_1d:
+        """One pass of the hot path (for N > 1: bulk kernel, then the halo-dependent edges)."""
+        if not self.sharded_1d:
+            self.bulk()
+            return
+        if self.halo_src is None:  # set up once (collectively), used every step
+            if self.world == 1:  # FIR_SELF_HALO rehearsal: RCCL ring of one
+                self.halo_kind = "rccl"
+                self.halo_src = sharded.HaloExchange(self.x, self.taps.n, self.channels, self_ring=True)
+            else:
+                self.halo_kind, self.halo_src = sharded.make_halo_source(self.x, self.taps.n, self.channels,
+                                                                         prefer=HALO_PREF)
+            self.config["parallelism"] = (
+                f"contiguous shards x{self.world}, halo " + ("read from the neighbours' HBM over xGMI (peer IPC "
+                                                             "mapping, edge kernel)" if self.halo_kind == "xgmi"
+                                                             else "exchanged by RCCL send/recv every step"))
+        if self.halo_kind == "xgmi":
+            self.bulk()
+            left, right = self.halo_src.halos()
+            self.left, self.right = self.halo_src.left_host, self.halo_src.right_host
+        else:
+            works = self.halo_src.post()
+            self.bulk()
             sharded.wait_all(works)
-            torch_ops.fir1d_fixed_edges_dev(self.x, self.taps, self.y, self.left, self.right, 12, 32,
-                                            fir_hip.OUT_I32, self.channels)
+            left, right = self.halo_src.halos()
+            self.left, self.right = left, right
+        torch_ops.fir1d_fixed_edges_dev(self.x, self.taps, self.y, left, right, 12, 32, fir_hip.OUT_I32,
+                                        self.channels)
 
     def oracle(self, nthreads: int, reps: int = 1):
         from oracle import c_oracle
@@ -226,8 +252,8 @@ class Workload:
 
                 out = fo.compute_metrics(self.x_host, self.fixed_host)
             else:
-                hl = None if self.left is None else self.left.cpu().numpy()
-                hr = None if self.right is None else self.right.cpu().numpy()
+                hl = None if self.left is None else np.asarray(self.left.cpu() if torch.is_tensor(self.left) else self.left)
+                hr = None if self.right is None else np.asarray(self.right.cpu() if torch.is_tensor(self.right) else self.right)
                 out = co.fir1d_rows(self.x_host, self.taps.h, 12, 32, co.OUT_I32, channels=self.channels,
                                     halo_left=hl, halo_right=hr, nthreads=nthreads)
         return out
@@ -292,9 +318,18 @@ def main() -> int:
     dev_index = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
-    if world > 1:
+    if SELF_HALO and world != 1:
+        raise SystemExit("FIR_SELF_HALO=1 rehearses the exchange at N = 1 only")
+    if world > 1 or SELF_HALO:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29561")
         if backend == "nccl":
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+            # RCCL's internal stream at high priority: it gets its own hardware queue, so the
+            # exchange's cross-stream wait does not block the queue the FIR kernels run on
+            # (measured with FIR_SELF_HALO=1)
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = os.environ.get("FIR_NCCL_HIPRI", "1") == "1"
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev, pg_options=opts)
         else:
             dist.init_process_group(backend, rank=rank, world_size=world)
     red_dev = dev if backend == "nccl" else torch.device("cpu")
@@ -311,7 +346,7 @@ def main() -> int:
             else:
                 dist.barrier()
 
-    barrier()  # every rank's communicator is up before the first halo exchange
+    barrier()  # every rank's segment is resident and its communicator up before the first step
     for _ in range(args.warmup):
         wl.step()
     barrier()
@@ -319,6 +354,7 @@ def main() -> int:
     t0 = time.perf_counter()
     for _ in range(args.steps):
         wl.step()
+    t_issue = time.perf_counter() - t0  # host time to issue the steps (diagnostic: host-bound?)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -415,10 +451,18 @@ def main() -> int:
         "cpu_baseline": cpu,
         "cpu_baseline_numpy": cpu_np,
         "parity": parity,
+        "host_issue_us_per_step": round(t_issue / args.steps * 1e6, 1),
     }
+    if wl.sharded_1d and world == 1:
+        line["config"] = dict(wl.config, rehearsal="FIR_SELF_HALO=1: RCCL halo exchange with itself every step "
+                                                    "(ring of one) + edge kernel")
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
+        torch.cuda.synchronize()
+        barrier()  # no rank unmaps or frees its segment while a neighbour may still read it
+        if isinstance(wl.halo_src, sharded.XgmiHalo):
+            wl.halo_src.close()
         dist.destroy_process_group()
     return 0 if parity != "MISMATCH" else 1
 

@@ -155,6 +155,21 @@ int fir_restore_u8(const double* a, int64_t n, int policy, uint8_t* out, int dev
 int fir_restore_u8_dev(const double* a_dev, int64_t n, int policy, uint8_t* out_dev, void* work_dev,
                        void* stream);
 
+/* ---- xGMI peer halos for sharded segments ---------------------------
+ * One process per GPU: each rank exports the device buffer holding its segment once, its
+ * neighbours map it, and every step's edge kernel (fir1d_fixed_edges_dev) reads its
+ * (taps-1)-sample halo straight out of the neighbours' HBM over xGMI -- no per-step message.
+ * fir_ipc_export: an opaque FIR_IPC_HANDLE_BYTES-byte handle of the allocation containing
+ *   dev_ptr, and dev_ptr's byte offset inside that allocation.
+ * fir_ipc_import: map a handle exported by ANOTHER process on this node for kernels on
+ *   `device`; *dev_ptr_out = mapped base + offset.  Release with fir_ipc_close(*dev_ptr_out).
+ * fir_peek: synchronous copy of `bytes` device bytes (own or imported) to host memory. */
+#define FIR_IPC_HANDLE_BYTES 64
+int fir_ipc_export(const void* dev_ptr, void* handle_out, int64_t* offset_out);
+int fir_ipc_import(const void* handle, int64_t offset, int device, void** dev_ptr_out);
+int fir_ipc_close(void* dev_ptr);
+int fir_peek(const void* dev_ptr, void* host_out, int64_t bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -100,3 +100,110 @@ def test_sharded_more_shards_than_work():
 def test_sharded_bad_device_is_an_error():
     with pytest.raises(fir_hip.FirHipError, match="out of range"):
         fir_hip.fir1d_fixed_rows_sharded(np.zeros(64, np.uint8), [1, 2, 1], devices=[0, 99])
+
+
+def test_rccl_halo_exchange_ring_of_one():
+    """The RCCL halo exchange of fir_hip.sharded on the box's one GPU: a world of one whose
+    segment is its own left and right neighbour (bench.py's FIR_SELF_HALO rehearsal).  The
+    grouped send/recv must deliver the segment's last HL samples as the left halo and its
+    first HR samples as the right halo on every repost, and the edge kernel fed with them
+    must match the oracle with the same halos."""
+    import socket
+
+    import torch.distributed as dist
+    from fir_hip import sharded
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+    try:
+        for taps, ch in (([-256, -1024, 6656, -1024, -256], 1), ([5, -7, 9, 11], 1), ([1024, 2048, 1024], 2)):
+            hl, hr = sharded.halo_sizes(len(taps), ch)
+            rng = np.random.default_rng(len(taps) * 10 + ch)
+            x = torch.from_numpy(rng.integers(-32768, 32768, 4099 * ch, dtype=np.int16)).to(dev)
+            y = torch.empty(x.shape, dtype=torch.int32, device=dev)
+            ex = sharded.HaloExchange(x, len(taps), ch, self_ring=True)
+            for step in range(3):
+                x.add_(step + 1)
+                works = ex.post()
+                torch_ops.fir1d_fixed_rows_dev(x, taps, 12, 32, fir_hip.OUT_I32, ch, out=y)
+                sharded.wait_all(works)
+                left, right = ex.halos()
+                torch_ops.fir1d_fixed_edges_dev(x, taps, y, left, right, 12, 32, fir_hip.OUT_I32, ch)
+                torch.cuda.synchronize()
+                xs = x.cpu().numpy()
+                assert np.array_equal(left.cpu().numpy(), xs[xs.size - hl:]), (taps, step)
+                if hr:
+                    assert np.array_equal(right.cpu().numpy(), xs[:hr]), (taps, step)
+                want = c_oracle().fir1d_rows(xs, taps, 12, 32, c_oracle().OUT_I32, channels=ch,
+                                             halo_left=xs[xs.size - hl:], halo_right=xs[:hr] if hr else None)
+                assert np.array_equal(y.cpu().numpy(), want), (taps, step)
+    finally:
+        dist.destroy_process_group()
+
+
+def _xgmi_worker(rank, world, port, taps, ch, q):
+    import os
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root), str(root / "warmup-fir-filter_amd")]
+    import torch.distributed as dist
+
+    import fir_hip as fh
+    from fir_hip import sharded, torch_ops as to
+    from oracle import c_oracle as co
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        n = 50_003
+        x = np.random.default_rng(7).integers(-32768, 32768, n * ch, dtype=np.int16)
+        lo, hi = sharded.segment_bounds(n, world, rank)
+        seg = torch.from_numpy(x[lo * ch:hi * ch].copy()).to(dev)
+        y = torch.empty(seg.shape, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        dist.barrier()  # every segment resident before it is mapped
+        kind, src = sharded.make_halo_source(seg, len(taps), ch)
+        for _ in range(3):  # the mapping is reused step after step
+            to.fir1d_fixed_rows_dev(seg, taps, 12, 32, fh.OUT_I32, ch, out=y)
+            to.fir1d_fixed_edges_dev(seg, taps, y, *src.halos(), 12, 32, fh.OUT_I32, ch)
+        torch.cuda.synchronize()
+        parts = [None] * world
+        dist.all_gather_object(parts, y.cpu().numpy())
+        dist.barrier()  # nobody unmaps / frees before every rank is done reading
+        src.close()
+        if rank == 0:
+            full = co().fir1d_rows(x, taps, 12, 32, co().OUT_I32, channels=ch)
+            q.put((kind, bool(np.array_equal(np.concatenate(parts), full))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,taps,ch", [(2, [-256, -1024, 6656, -1024, -256], 1), (3, [5, -7, 9, 11], 1),
+                                           (4, [1024, 2048, 1024], 2)])
+def test_xgmi_peer_halos_across_processes(world, taps, ch):
+    """fir_hip.sharded.XgmiHalo: ranks (processes) map their neighbours' segments through the
+    C ABI's IPC entries and the edge kernel reads the halos from them.  On the one-GPU box the
+    ranks share device 0 (the same mapping path as across GPUs, minus the xGMI hop)."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_xgmi_worker, args=(r, world, port, taps, ch, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=100)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    kind, ok = q.get(timeout=5)
+    assert kind == "xgmi" and ok

@@ -92,3 +92,96 @@ def test_segment_bounds_cover_exactly():
         spans = [sharded.segment_bounds(n, w, r) for r in range(w)]
         assert spans[0][0] == 0 and spans[-1][1] == n
         assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+
+
+def _exchange_worker(rank, world, port, taps, channels, self_ring, q):
+    """HaloExchange built once and posted on several steps (the bench's step loop)."""
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root), str(root / "warmup-fir-filter_amd")]
+    from fir_hip import sharded
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = 37 * channels
+        seg = torch.arange(rank * 1000, rank * 1000 + n, dtype=torch.int16)
+        ex = sharded.HaloExchange(seg, taps, channels, self_ring=self_ring)
+        hl, hr = sharded.halo_sizes(taps, channels)
+        ok = True
+        for step in range(3):
+            seg.add_(1)  # new data each step: the send views must see it
+            sharded.wait_all(ex.post())
+            left, right = ex.halos()
+            lrank = rank - 1 if rank > 0 else (rank if self_ring else None)
+            rrank = rank + 1 if rank < world - 1 else (rank if self_ring else None)
+            base = step + 1
+            if hl:
+                want_l = None if lrank is None else torch.arange(lrank * 1000 + n - hl, lrank * 1000 + n) + base
+                ok &= (left is None) if want_l is None else bool(torch.equal(left.long(), want_l))
+            if hr:
+                want_r = None if rrank is None else torch.arange(rrank * 1000, rrank * 1000 + hr) + base
+                ok &= (right is None) if want_r is None else bool(torch.equal(right.long(), want_r))
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,taps,channels,self_ring", [  # self_ring (RCCL only): test_gpu_restore_sharded
+    (3, 5, 1, False),
+    (4, 4, 2, False),
+    (2, 4, 1, False),
+])
+def test_halo_exchange_object_reposts_fresh_halos(world, taps, channels, self_ring):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, taps, channels, self_ring, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    got = dict(q.get(timeout=5) for _ in range(world))
+    assert all(got.values()), got
+
+
+def _fallback_worker(rank, world, port, q):
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root), str(root / "warmup-fir-filter_amd")]
+    from fir_hip import sharded
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        seg = torch.arange(rank * 100, rank * 100 + 40, dtype=torch.int16)
+        kind, src = sharded.make_halo_source(seg, 5)  # host tensors cannot be mapped: every rank -> rccl
+        left, right = (None, None)
+        sharded.wait_all(src.post())
+        left, right = src.halos()
+        ok = kind == "rccl" and isinstance(src, sharded.HaloExchange)
+        if rank > 0:
+            ok &= left.tolist() == list(range((rank - 1) * 100 + 38, (rank - 1) * 100 + 40))
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_halo_source_falls_back_to_rccl_on_every_rank():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fallback_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    got = dict(q.get(timeout=5) for _ in range(3))
+    assert all(got.values()), got

@@ -466,4 +466,81 @@ int fir_restore_u8_dev(const double* a_dev, int64_t n, int policy, uint8_t* out_
     }
 }
 
+// ---- xGMI peer halos (fir_hip.h) --------------------------------------------------------
+static_assert(sizeof(hipIpcMemHandle_t) == FIR_IPC_HANDLE_BYTES, "IPC handle size");
+
+namespace {
+std::mutex g_ipc_mu;
+std::map<void*, void*> g_ipc_base;  // pointer handed out by fir_ipc_import -> mapped base
+}  // namespace
+
+int fir_ipc_export(const void* dev_ptr, void* handle_out, int64_t* offset_out) {
+    try {
+        if (!dev_ptr || !handle_out || !offset_out) return fail(FIR_EINVAL, "NULL argument");
+        hipDeviceptr_t base = nullptr;
+        size_t size = 0;
+        hipError_t e = hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)dev_ptr);
+        if (e != hipSuccess) return fail(FIR_EHIP, std::string("hipMemGetAddressRange: ") + hipGetErrorString(e));
+        hipIpcMemHandle_t h;
+        e = hipIpcGetMemHandle(&h, (void*)base);
+        if (e != hipSuccess) return fail(FIR_EHIP, std::string("hipIpcGetMemHandle: ") + hipGetErrorString(e));
+        std::memcpy(handle_out, &h, sizeof(h));
+        *offset_out = (int64_t)((const char*)dev_ptr - (const char*)base);
+        return FIR_OK;
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int fir_ipc_import(const void* handle, int64_t offset, int device, void** dev_ptr_out) {
+    try {
+        if (!handle || !dev_ptr_out || offset < 0) return fail(FIR_EINVAL, "invalid argument");
+        *dev_ptr_out = nullptr;
+        hipError_t e = hipSetDevice(device);
+        if (e != hipSuccess) return fail(FIR_ENODEV, std::string("hipSetDevice: ") + hipGetErrorString(e));
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, handle, sizeof(h));
+        void* base = nullptr;
+        e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) return fail(FIR_EHIP, std::string("hipIpcOpenMemHandle: ") + hipGetErrorString(e));
+        void* p = (char*)base + offset;
+        std::lock_guard<std::mutex> g(g_ipc_mu);
+        g_ipc_base[p] = base;
+        *dev_ptr_out = p;
+        return FIR_OK;
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int fir_ipc_close(void* dev_ptr) {
+    try {
+        void* base = nullptr;
+        {
+            std::lock_guard<std::mutex> g(g_ipc_mu);
+            auto it = g_ipc_base.find(dev_ptr);
+            if (it == g_ipc_base.end()) return fail(FIR_EINVAL, "pointer was not returned by fir_ipc_import");
+            base = it->second;
+            g_ipc_base.erase(it);
+        }
+        hipError_t e = hipIpcCloseMemHandle(base);
+        if (e != hipSuccess) return fail(FIR_EHIP, std::string("hipIpcCloseMemHandle: ") + hipGetErrorString(e));
+        return FIR_OK;
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int fir_peek(const void* dev_ptr, void* host_out, int64_t bytes) {
+    try {
+        if (bytes < 0 || (bytes > 0 && (!dev_ptr || !host_out))) return fail(FIR_EINVAL, "invalid argument");
+        if (bytes == 0) return FIR_OK;
+        hipError_t e = hipMemcpy(host_out, dev_ptr, (size_t)bytes, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return fail(FIR_EHIP, std::string("hipMemcpy: ") + hipGetErrorString(e));
+        return FIR_OK;
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
 }  // extern "C"

@@ -23,13 +23,15 @@ import numpy as np
 __all__ = [
     "FirHipError", "lib", "lib_path", "device_count", "fir1d_fixed_rows", "fir1d_fixed_rows_multi",
     "fir1d_fixed_rows_sharded", "fir2d_fixed", "fir1d_ideal_rows", "compare_metrics", "restore_u8", "IN_U8", "IN_I16",
-    "OUT_U8_SAT", "OUT_I32", "RESTORE_CLIP", "RESTORE_NORMALIZE", "MAX_TAPS", "EXPORTS",
+    "OUT_U8_SAT", "OUT_I32", "RESTORE_CLIP", "RESTORE_NORMALIZE", "MAX_TAPS", "EXPORTS", "ipc_export", "ipc_import",
+    "ipc_close", "peek", "IPC_HANDLE_BYTES",
 ]
 
 IN_U8, IN_I16 = 0, 1
 OUT_U8_SAT, OUT_I32 = 0, 1
 RESTORE_CLIP, RESTORE_NORMALIZE = 0, 1
 MAX_TAPS = 256
+IPC_HANDLE_BYTES = 64
 ABI_VERSION = 1
 
 _HERE = Path(__file__).resolve().parent
@@ -66,6 +68,10 @@ EXPORTS = {
     "fir_restore_work_bytes": (_i64, []),
     "fir_restore_u8": (_i32, [_vp, _i64, _i32, _vp, _i32]),
     "fir_restore_u8_dev": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp]),
+    "fir_ipc_export": (_i32, [_vp, _vp, ctypes.POINTER(_i64)]),
+    "fir_ipc_import": (_i32, [_vp, _i64, _i32, ctypes.POINTER(_vp)]),
+    "fir_ipc_close": (_i32, [_vp]),
+    "fir_peek": (_i32, [_vp, _vp, _i64]),
 }
 
 _lib = None
@@ -275,3 +281,32 @@ def restore_u8(a: np.ndarray, policy: int = RESTORE_CLIP, device: int = 0) -> np
     out = np.empty(arr.shape, dtype=np.uint8)
     _check(lib().fir_restore_u8(_ptr(arr), arr.size, int(policy), _ptr(out), int(device)), "fir_restore_u8")
     return out
+
+
+# ---- xGMI peer halos (fir_hip.h; used by fir_hip.sharded.XgmiHalo) ---------------------
+def ipc_export(dev_ptr: int) -> tuple[bytes, int]:
+    """(handle, byte offset) of the device allocation holding ``dev_ptr``, for another process."""
+    h = ctypes.create_string_buffer(IPC_HANDLE_BYTES)
+    off = ctypes.c_int64(0)
+    _check(lib().fir_ipc_export(ctypes.c_void_p(dev_ptr), h, ctypes.byref(off)), "fir_ipc_export")
+    return h.raw, int(off.value)
+
+
+def ipc_import(handle: bytes, offset: int, device: int) -> int:
+    """Map a peer process's exported allocation on ``device``; returns base + ``offset``."""
+    if len(handle) != IPC_HANDLE_BYTES:
+        raise FirHipError(f"IPC handle must be {IPC_HANDLE_BYTES} bytes")
+    p = ctypes.c_void_p(0)
+    _check(lib().fir_ipc_import(handle, int(offset), int(device), ctypes.byref(p)), "fir_ipc_import")
+    return int(p.value)
+
+
+def ipc_close(dev_ptr: int) -> None:
+    _check(lib().fir_ipc_close(ctypes.c_void_p(dev_ptr)), "fir_ipc_close")
+
+
+def peek(dev_ptr: int, nbytes: int) -> bytes:
+    """Synchronous copy of ``nbytes`` device bytes (own or imported) to the host."""
+    buf = ctypes.create_string_buffer(max(1, nbytes))
+    _check(lib().fir_peek(ctypes.c_void_p(dev_ptr), buf, int(nbytes)), "fir_peek")
+    return buf.raw[:nbytes]

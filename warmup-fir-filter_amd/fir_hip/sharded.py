@@ -15,6 +15,7 @@ edge outputs once the halos have arrived (same stream, so it is ordered after bo
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -31,41 +32,183 @@ def segment_bounds(n: int, world: int, rank: int) -> tuple[int, int]:
     return lo, lo + base + (1 if rank < extra else 0)
 
 
+class HaloExchange:
+    """The neighbour exchange of one resident 1-D segment, set up once and posted every step.
+
+    The receive buffers and the point-to-point op list are built once (the segment, and so
+    the send views, stay the same between steps), so a step costs one ``batch_isend_irecv``
+    call on the host.  ``self_ring=True`` with a world of one rehearses the exchange on a
+    single device: the segment is its own left and right neighbour (a ring of one), so
+    RCCL's grouped send/recv runs for real; the received halos are then the segment's own
+    wrap-around samples, and the edge outputs are checked against them."""
+
+    def __init__(self, seg: torch.Tensor, taps: int, channels: int = 1, group=None, self_ring: bool = False):
+        seg = seg.reshape(-1)
+        world = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        hl, hr = halo_sizes(taps, channels)
+        if seg.numel() < max(hl, hr):
+            raise ValueError("segment shorter than the filter halo")
+        if self_ring and (world != 1 or dist.get_backend(group) != "nccl"):
+            raise ValueError("self_ring rehearses a world of one on RCCL (gloo has no send-to-self)")
+        self.staged = seg.is_cuda and dist.get_backend(group) == "gloo"
+        # gloo has no device point-to-point: the few halo samples are staged through the host
+        # (only to rehearse the multi-rank flow on a single-GPU box; RCCL sends device buffers)
+        buf_dev = torch.device("cpu") if self.staged else seg.device
+        self.seg, self.group, self.hl, self.hr = seg, group, hl, hr
+        self.left = self.right = None
+        self._sends = []  # (device view, host staging buffer or None)
+        ops = []
+        left_peer = _peer(group, rank - 1) if rank > 0 else (_peer(group, rank) if self_ring else None)
+        right_peer = _peer(group, rank + 1) if rank < world - 1 else (_peer(group, rank) if self_ring else None)
+        # receives first, then sends; within one direction a message pair matches in order, so
+        # with a ring of one (both peers = self) left <- seg[-hl:] and right <- seg[:hr] as intended
+        # On the wire every halo is raw bytes (a uint8 view): RCCL's process group refuses int16.
+        if left_peer is not None and hl:
+            self.left = torch.empty(hl, dtype=seg.dtype, device=buf_dev)
+            ops.append(dist.P2POp(dist.irecv, _wire(self.left), left_peer, group))
+        if right_peer is not None and hr:
+            self.right = torch.empty(hr, dtype=seg.dtype, device=buf_dev)
+            ops.append(dist.P2POp(dist.irecv, _wire(self.right), right_peer, group))
+        if right_peer is not None and hl:
+            ops.append(dist.P2POp(dist.isend, _wire(self._send_buf(seg[seg.numel() - hl:])), right_peer, group))
+        if left_peer is not None and hr:
+            ops.append(dist.P2POp(dist.isend, _wire(self._send_buf(seg[:hr])), left_peer, group))
+        self.ops = ops
+
+    def _send_buf(self, view: torch.Tensor) -> torch.Tensor:
+        if not self.staged:
+            return view
+        host = torch.empty(view.shape, dtype=view.dtype)
+        self._sends.append((view, host))
+        return host
+
+    def post(self):
+        """Post this step's exchange; returns the request handles (empty when staged)."""
+        if not self.ops:
+            return []
+        for view, host in self._sends:
+            host.copy_(view)
+        works = dist.batch_isend_irecv(self.ops)
+        if self.staged:
+            wait_all(works)
+            return []
+        return works
+
+    def halos(self):
+        """(left, right) on the segment's device, after the works have been waited on."""
+        if self.staged:
+            d = self.seg.device
+            return (None if self.left is None else self.left.to(d), None if self.right is None else self.right.to(d))
+        return self.left, self.right
+
+
+class XgmiHalo:
+    """Halos read straight from the neighbours' HBM over xGMI (the MI355X-native exchange).
+
+    Set up once, collectively: every rank exports the allocation holding its resident
+    segment (fir_hip.ipc_export), the handles are all-gathered over the process group, and
+    each rank maps its left and right neighbours' segments (fir_hip.ipc_import) at the
+    addresses of the HL / HR samples it needs.  A step then passes those addresses to the
+    edge kernel, which loads the 2 x (a few) bytes over xGMI itself: no message, no RCCL
+    kernel, no cross-stream event per step.  The mapping is checked once against the
+    samples the neighbour reports.  Valid while the neighbours' segments stay resident and
+    unchanged (a resident long vector filtered in place); ``close()`` unmaps."""
+
+    def __init__(self, seg: torch.Tensor, taps: int, channels: int = 1, group=None):
+        import fir_hip
+
+        seg = seg.reshape(-1)
+        if not seg.is_cuda or not seg.is_contiguous():
+            raise ValueError("XgmiHalo needs a contiguous device segment")
+        world = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        hl, hr = halo_sizes(taps, channels)
+        if seg.numel() < max(hl, hr):
+            raise ValueError("segment shorter than the filter halo")
+        handle, off = fir_hip.ipc_export(seg.data_ptr())
+        cpu = seg.cpu()
+        mine = {"handle": handle, "offset": off, "numel": seg.numel(), "elt": seg.element_size(),
+                "first": cpu[:hr].numpy().tobytes(), "last": cpu[seg.numel() - hl:].numpy().tobytes()}
+        infos = [None] * world
+        dist.all_gather_object(infos, mine, group=group)
+        dev = seg.device.index
+        self.left_ptr = self.right_ptr = None
+        self.left_host = self.right_host = None
+        self._mapped = []
+        try:
+            if rank > 0 and hl:
+                p = infos[rank - 1]
+                self.left_ptr = fir_hip.ipc_import(p["handle"], p["offset"] + (p["numel"] - hl) * p["elt"], dev)
+                self._mapped.append(self.left_ptr)
+                got = fir_hip.peek(self.left_ptr, hl * p["elt"])
+                if got != p["last"]:
+                    raise RuntimeError("left neighbour mapping reads the wrong samples")
+                self.left_host = np.frombuffer(got, dtype=cpu.numpy().dtype).copy()
+            if rank < world - 1 and hr:
+                p = infos[rank + 1]
+                self.right_ptr = fir_hip.ipc_import(p["handle"], p["offset"], dev)
+                self._mapped.append(self.right_ptr)
+                got = fir_hip.peek(self.right_ptr, hr * p["elt"])
+                if got != p["first"]:
+                    raise RuntimeError("right neighbour mapping reads the wrong samples")
+                self.right_host = np.frombuffer(got, dtype=cpu.numpy().dtype).copy()
+        except Exception:
+            self.close()
+            raise
+
+    def halos(self):
+        """(left, right) device addresses for the edge kernel (None at the global ends)."""
+        return self.left_ptr, self.right_ptr
+
+    def close(self) -> None:
+        import fir_hip
+
+        for p in self._mapped:
+            fir_hip.ipc_close(p)
+        self._mapped = []
+        self.left_ptr = self.right_ptr = None
+
+
+def make_halo_source(seg: torch.Tensor, taps: int, channels: int = 1, group=None, prefer: str = "xgmi"):
+    """The per-step halo source for a resident segment: XgmiHalo when every rank can map its
+    neighbours (decided collectively, so all ranks take the same path), else the RCCL
+    HaloExchange.  Returns (kind, source) with kind "xgmi" or "rccl"."""
+    ok, err = 0, None
+    src = None
+    if prefer == "xgmi":
+        try:
+            src = XgmiHalo(seg, taps, channels, group)
+            ok = 1
+        except Exception as e:  # noqa: BLE001 - any failure selects the RCCL path on every rank
+            err = e
+        flags = [None] * dist.get_world_size(group)
+        dist.all_gather_object(flags, ok, group=group)
+        if all(flags):
+            return "xgmi", src
+        if src is not None:
+            src.close()
+        if err is not None:
+            import sys
+
+            print(f"fir_hip.sharded: xGMI halo mapping unavailable ({err}); using RCCL", file=sys.stderr)
+    return "rccl", HaloExchange(seg, taps, channels, group)
+
+
 def post_halo_exchange(seg: torch.Tensor, taps: int, channels: int = 1, group=None):
     """Post the neighbour exchange for a 1-D segment.  Returns (left, right, works):
     `left` / `right` are the receive buffers (None at the global ends or when empty) and
-    `works` the request handles to wait on before the halos are read."""
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    hl, hr = halo_sizes(taps, channels)
-    if seg.numel() < max(hl, hr):
-        raise ValueError("segment shorter than the filter halo")
-    staged = seg.is_cuda and dist.get_backend(group) == "gloo"
-    # gloo has no device point-to-point: the few halo samples are staged through the host
-    # (only to rehearse the multi-rank flow on a single-GPU box; RCCL sends device buffers)
-    buf_dev = torch.device("cpu") if staged else seg.device
-
-    def _send(t):
-        return t.cpu() if staged else t.contiguous()
-
-    ops, left, right = [], None, None
-    if rank > 0:
-        if hl:
-            left = torch.empty(hl, dtype=seg.dtype, device=buf_dev)
-            ops.append(dist.P2POp(dist.irecv, left, _peer(group, rank - 1), group))
-        if hr:
-            ops.append(dist.P2POp(dist.isend, _send(seg[:hr]), _peer(group, rank - 1), group))
-    if rank < world - 1:
-        if hr:
-            right = torch.empty(hr, dtype=seg.dtype, device=buf_dev)
-            ops.append(dist.P2POp(dist.irecv, right, _peer(group, rank + 1), group))
-        if hl:
-            ops.append(dist.P2POp(dist.isend, _send(seg[seg.numel() - hl:]), _peer(group, rank + 1), group))
-    works = dist.batch_isend_irecv(ops) if ops else []
-    if staged:
-        wait_all(works)
-        return (None if left is None else left.to(seg.device), None if right is None else right.to(seg.device), [])
+    `works` the request handles to wait on before the halos are read.  One-shot form of
+    :class:`HaloExchange` (which a step loop should build once and post every step)."""
+    ex = HaloExchange(seg, taps, channels, group)
+    works = ex.post()
+    left, right = ex.halos()
     return left, right, works
+
+
+def _wire(t: torch.Tensor) -> torch.Tensor:
+    """The bytes of a contiguous tensor as uint8 (same storage)."""
+    return t.view(torch.uint8)
 
 
 def _peer(group, r: int) -> int:

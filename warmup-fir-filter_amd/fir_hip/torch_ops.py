@@ -92,26 +92,31 @@ def fir1d_fixed_rows_multi_dev(x: torch.Tensor, hq2, frac_bits: int = 12, acc_bi
     return out
 
 
-def fir1d_fixed_edges_dev(x: torch.Tensor, hq, out: torch.Tensor, halo_left: torch.Tensor | None,
-                          halo_right: torch.Tensor | None, frac_bits: int = 12, acc_bits: int = 32,
-                          out_stage: int = OUT_I32, channels: int = 1, stream=None) -> torch.Tensor:
-    """Recompute the halo-dependent edge outputs of a 1-D segment (see fir_hip.h)."""
+def fir1d_fixed_edges_dev(x: torch.Tensor, hq, out: torch.Tensor, halo_left, halo_right, frac_bits: int = 12,
+                          acc_bits: int = 32, out_stage: int = OUT_I32, channels: int = 1, stream=None) -> torch.Tensor:
+    """Recompute the halo-dependent edge outputs of a 1-D segment (see fir_hip.h).  A halo is a
+    device tensor of the segment's dtype, None (zeros), or an int device address holding the
+    halo samples (e.g. a neighbour's HBM mapped by fir_hip.ipc_import: read over xGMI)."""
     _check_dev(x, "x")
     _check_dev(out, "out")
     t = _taps(hq)
     L = t.n
     hl_n, hr_n = (L - 1 - L // 2) * channels, (L // 2) * channels
+    ptrs = []
     for h, n, name in ((halo_left, hl_n, "halo_left"), (halo_right, hr_n, "halo_right")):
-        if h is not None:
+        if h is None or not n:
+            ptrs.append(None)
+        elif isinstance(h, int):
+            ptrs.append(ctypes.c_void_p(h))
+        else:
             _check_dev(h, name)
             if h.dtype != x.dtype or h.numel() != n:
                 raise FirHipError(f"{name} must hold {n} samples of {x.dtype}")
+            ptrs.append(ctypes.c_void_p(h.data_ptr()))
     if x.numel() % channels:
         raise FirHipError("segment length must be a multiple of channels")
-    hlp = ctypes.c_void_p(halo_left.data_ptr()) if halo_left is not None and hl_n else None
-    hrp = ctypes.c_void_p(halo_right.data_ptr()) if halo_right is not None and hr_n else None
     _check(lib().fir1d_fixed_edges_dev(ctypes.c_void_p(x.data_ptr()), _IN[x.dtype], x.numel() // channels, channels,
-                                       t.ptr, t.n, int(frac_bits), int(acc_bits), int(out_stage), hlp, hrp,
+                                       t.ptr, t.n, int(frac_bits), int(acc_bits), int(out_stage), ptrs[0], ptrs[1],
                                        ctypes.c_void_p(out.data_ptr()), _stream_ptr(x, stream)),
            "fir1d_fixed_edges_dev")
     return out
