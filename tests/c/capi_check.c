@@ -37,6 +37,15 @@ int main(void) {
     expect(fir1d_fixed_rows_sharded(NULL, 0, 0, 16, 1, h3, 3, 12, 32, 0, NULL, devs, 3) == FIR_OK, "empty sharded");
     expect(fir_restore_u8_dev(NULL, 8, 9, NULL, NULL, NULL) == FIR_EINVAL, "bad policy");
     expect(fir2d_fixed_dev(NULL, 4, 4, h3, 0, 3, 12, 32, 0, NULL, NULL) == FIR_EINVAL, "2d zero rows");
+    {
+        char handle[FIR_IPC_HANDLE_BYTES];
+        int64_t off = 0;
+        void* p = NULL;
+        expect(fir_ipc_export(NULL, handle, &off) == FIR_EINVAL, "ipc export null");
+        expect(fir_ipc_import(handle, -1, 0, &p) == FIR_EINVAL, "ipc import offset");
+        expect(fir_ipc_close((void*)handle) == FIR_EINVAL, "ipc close unknown");
+        expect(fir_peek(NULL, NULL, 8) == FIR_EINVAL, "peek null");
+    }
     expect(strlen(fir_last_error()) > 0, "error text");
     if (!have) {
         uint8_t x[64] = {0}, y[64];

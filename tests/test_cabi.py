@@ -76,3 +76,16 @@ def test_sharded_and_restore_argument_checks_without_device(lib):
     assert lib.fir_restore_u8_dev(None, 0, 1, None, None, None) == 0
     assert lib.fir_restore_u8_dev(None, 8, 1, None, None, None) == 1
     assert lib.fir_restore_work_bytes() >= 256
+
+
+def test_ipc_argument_checks_without_device(lib):
+    off = ctypes.c_int64(0)
+    handle = ctypes.create_string_buffer(64)
+    p = ctypes.c_void_p(0)
+    assert lib.fir_ipc_export(None, handle, ctypes.byref(off)) == 1 and b"NULL" in lib.fir_last_error()
+    assert lib.fir_ipc_import(None, 0, 0, ctypes.byref(p)) == 1
+    assert lib.fir_ipc_import(handle, -1, 0, ctypes.byref(p)) == 1
+    assert lib.fir_ipc_close(ctypes.c_void_p(1234)) == 1 and b"fir_ipc_import" in lib.fir_last_error()
+    assert lib.fir_peek(None, None, 0) == 0  # empty no-op
+    assert lib.fir_peek(None, None, 8) == 1
+    assert lib.fir_peek(None, None, -1) == 1
