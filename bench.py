@@ -17,6 +17,10 @@ prints ONE JSON line.  Extra keys:
   parity        every rank's full output compared bit-exactly with the C oracle
   cpu_baseline_numpy  the vectorised NumPy restatement (oracle/fir_oracle.py, one core) on a
                 bounded leading slice of the same input (BASELINE.md's "NumPy CPU path")
+  cpu_baseline_numpy_threads  the same NumPy path over contiguous slices on a thread pool of
+                the host's cores (core count in `cores`)
+  host_issue_us_per_step  host time to enqueue one timed step (diagnostic: < ms_per_step
+                means the GPU, not Python, sets the pace)
 Other workloads: `cplx_i16` / `fir2d_u8` measure configs[2] / configs[4]; `fir1d_u8` the
 reference's own u8 -> sat-u8 golden path (a1/a4) at scale; `ideal_u8` (the f64
 ideal model), `bank_u8` (the fused 4-filter 3-tap bank, §8(f) 3) and
@@ -258,32 +262,72 @@ class Workload:
                                     halo_left=hl, halo_right=hr, nthreads=nthreads)
         return out
 
-    def numpy_oracle(self, max_units: int):
-        """The NumPy restatement on the leading ``max_units`` units; returns the units done."""
+    def numpy_oracle_threads(self, max_units: int, nthreads: int) -> int:
+        """The NumPy restatement over the leading ``max_units`` units split into ``nthreads``
+        contiguous slices on a thread pool (NumPy releases the GIL in its array loops); 1-D
+        int16 slices carry their true halos, row workloads split on row boundaries.
+        Returns the units done."""
+        from concurrent.futures import ThreadPoolExecutor
+
+        from oracle import fir_oracle as fo
+
+        if nthreads <= 1:
+            return self.numpy_oracle(max_units)
+        if self.name in ("fir1d_i16", "cplx_i16"):
+            n = min(self.units, max_units)
+            ch = self.channels
+            hl, hr = fo.halo_sizes(self.taps.n)
+            x = self.x_host
+
+            def job(i):
+                lo, hi = n * i // nthreads, n * (i + 1) // nthreads
+                a, b = lo * ch, hi * ch
+                fo.fir1d_i16_i32(x[a:b], self.taps.h, 12, 32, channels=ch,
+                                 halo_left=x[max(0, a - hl * ch):a] if a >= hl * ch else None,
+                                 halo_right=x[b:b + hr * ch] if b + hr * ch <= x.size else None)
+                return hi - lo
+        else:
+            unit_rows = self.w if self.name == "fir2d_u8" else (ROW_W if self.name in (
+                "ideal_u8", "bank_u8", "fir1d_u8", "restore_u8") else 1)
+            nrows = max(nthreads, min(self.units, max_units) // unit_rows)
+
+            def job(i):
+                r0, r1 = nrows * i // nthreads, nrows * (i + 1) // nthreads
+                return self.numpy_oracle((r1 - r0) * unit_rows, offset=r0 * unit_rows)
+        with ThreadPoolExecutor(nthreads) as pool:
+            return sum(pool.map(job, range(nthreads)))
+
+    def numpy_oracle(self, max_units: int, offset: int = 0):
+        """The NumPy restatement on ``max_units`` units from unit ``offset`` (row-aligned for
+        the row workloads); returns the units done."""
         from oracle import fir_oracle as fo
 
         if self.name == "fir2d_u8":
-            rows = max(1, min(self.h, max_units // self.w))
-            fo.fir2d_fixed(self.x_host[:rows], self.hq2, 12, 32, fo.OUT_U8_SAT)
+            r0 = offset // self.w
+            rows = max(1, min(self.h - r0, max_units // self.w))
+            fo.fir2d_fixed(self.x_host[r0:r0 + rows], self.hq2, 12, 32, fo.OUT_U8_SAT)
             return rows * self.w
         if self.name == "metrics_u8":
-            m = min(self.n, max_units)
-            fo.compute_metrics(self.x_host[:m], self.fixed_host[:m])
+            m = min(self.n - offset, max_units)
+            fo.compute_metrics(self.x_host[offset:offset + m], self.fixed_host[offset:offset + m])
             return m
         if self.name in ("ideal_u8", "bank_u8", "fir1d_u8", "restore_u8"):
-            rows = max(1, min(self.x_host.shape[0], max_units // ROW_W))
+            r0 = offset // ROW_W
+            rows = max(1, min(self.x_host.shape[0] - r0, max_units // ROW_W))
+            xs = self.x_host[r0:r0 + rows]
             if self.name == "restore_u8":
-                fo.to_u8_clip(self.x_host[:rows])
+                fo.to_u8_clip(xs)
             elif self.name == "fir1d_u8":
-                fo.fir1d_rows(self.x_host[:rows], self.taps.h, 12, 32, fo.OUT_U8_SAT)
+                fo.fir1d_rows(xs, self.taps.h, 12, 32, fo.OUT_U8_SAT)
             elif self.name == "ideal_u8":
-                fo.fir1d_ideal_rows(self.x_host[:rows], SHARPEN5_F64)
+                fo.fir1d_ideal_rows(xs, SHARPEN5_F64)
             else:
                 for h in BANK3:
-                    fo.fir1d_rows(self.x_host[:rows], h, 12, 32, fo.OUT_U8_SAT)
+                    fo.fir1d_rows(xs, h, 12, 32, fo.OUT_U8_SAT)
             return rows * ROW_W
-        n = min(self.units, max_units)
-        fo.fir1d_i16_i32(self.x_host[:n * self.channels], self.taps.h, 12, 32, channels=self.channels)
+        n = min(self.units - offset, max_units)
+        c = self.channels
+        fo.fir1d_i16_i32(self.x_host[offset * c:(offset + n) * c], self.taps.h, 12, 32, channels=c)
         return n
 
     def matches(self, ref) -> bool:
@@ -389,7 +433,7 @@ def main() -> int:
             ok = int(f.item()) == 0
         parity = "bit-exact vs oracle (full output, every rank)" if ok else "MISMATCH"
 
-    cpu = cpu_np = None
+    cpu = cpu_np = cpu_np_mt = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         nthr = _cpu_threads()
         wl.oracle(nthr)  # warm (page-in, thread pool)
@@ -412,6 +456,14 @@ def main() -> int:
         cpu_np = {"value": round(done / tn / 1e9, 5), "unit": wl.unit, "cores": 1, "kind": "port",
                   "sample": f"NumPy restatement (oracle/fir_oracle.py, int64 accumulation) on the first {done} "
                             f"units of the same input, {tn:.1f} s"}
+        # the same NumPy path on the host's cores (BASELINE.json: "NumPy CPU path timed on the host
+        # cores (core count stated)"): contiguous slices on a thread pool
+        tm0 = time.perf_counter()
+        done_m = wl.numpy_oracle_threads(1 << 26, nthr)
+        tm = time.perf_counter() - tm0
+        cpu_np_mt = {"value": round(done_m / tm / 1e9, 5), "unit": wl.unit, "cores": nthr, "kind": "port",
+                     "sample": f"NumPy restatement on the first {done_m} units, {nthr} slices on a thread pool, "
+                               f"{tm:.1f} s"}
 
     traffic = None
     pmc = ROOT / "profiles" / f"pmc_{args.workload}.json"
@@ -450,6 +502,7 @@ def main() -> int:
                      "timing": f"HIP events around {args.steps} back-to-back launches of the kernel"},
         "cpu_baseline": cpu,
         "cpu_baseline_numpy": cpu_np,
+        "cpu_baseline_numpy_threads": cpu_np_mt,
         "parity": parity,
         "host_issue_us_per_step": round(t_issue / args.steps * 1e6, 1),
     }
