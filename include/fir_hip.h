@@ -104,6 +104,16 @@ int fir1d_fixed_edges_dev(const void* x_dev, int in_dtype, int64_t n, int channe
                           const void* halo_left_dev, const void* halo_right_dev, void* y_dev,
                           void* stream);
 
+/* One shard of a longer single-row signal, halos given: the same outputs as
+ * fir1d_fixed_rows_dev followed by fir1d_fixed_edges_dev, in ONE register-kernel launch (the
+ * halos stand in for the zero padding) when n*channels is a whole number of 16-byte vectors
+ * and the buffers are 16-byte aligned; otherwise exactly those two launches.  The halos may
+ * live in another GPU's HBM mapped by fir_ipc_import (read over xGMI). */
+int fir1d_fixed_segment_dev(const void* x_dev, int in_dtype, int64_t n, int channels,
+                            const int32_t* hq, int taps, int frac_bits, int acc_bits, int out_stage,
+                            const void* halo_left_dev, const void* halo_right_dev, void* y_dev,
+                            void* stream);
+
 /* One-process multi-device form of fir1d_fixed_rows.  `devices`
  * lists ndev device ids (repeats allowed: a device then runs its shards in turn).
  * rows > 1: contiguous blocks of rows, no exchange (rows are independent).

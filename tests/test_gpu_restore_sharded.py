@@ -20,6 +20,8 @@ from conftest import GOLDEN
 from fir_hip import torch_ops
 from oracle import c_oracle, fir_oracle as fo
 
+DEV = torch.device("cuda", 0)
+
 
 def test_restore_reference_outputs_bit_exact():
     d = np.load(GOLDEN / "restore_u8.npz")
@@ -161,7 +163,7 @@ def _xgmi_worker(rank, world, port, taps, ch, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         dev = torch.device("cuda", 0)
-        n = 50_003
+        n = 50_003 if world != 2 else 65_536  # 2 ranks: whole vectors, the one-launch kernel path
         x = np.random.default_rng(7).integers(-32768, 32768, n * ch, dtype=np.int16)
         lo, hi = sharded.segment_bounds(n, world, rank)
         seg = torch.from_numpy(x[lo * ch:hi * ch].copy()).to(dev)
@@ -175,11 +177,18 @@ def _xgmi_worker(rank, world, port, taps, ch, q):
         torch.cuda.synchronize()
         parts = [None] * world
         dist.all_gather_object(parts, y.cpu().numpy())
+        # the one-launch form reads the same peer addresses inside the register kernel
+        y2 = torch.full(seg.shape, -7, dtype=torch.int32, device=dev)
+        to.fir1d_fixed_segment_dev(seg, taps, *src.halos(), 12, 32, fh.OUT_I32, ch, out=y2)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(y, y2))
+        flags = [None] * world
+        dist.all_gather_object(flags, same)
         dist.barrier()  # nobody unmaps / frees before every rank is done reading
         src.close()
         if rank == 0:
             full = co().fir1d_rows(x, taps, 12, 32, co().OUT_I32, channels=ch)
-            q.put((kind, bool(np.array_equal(np.concatenate(parts), full))))
+            q.put((kind, bool(np.array_equal(np.concatenate(parts), full)) and all(flags)))
     finally:
         dist.destroy_process_group()
 
@@ -207,3 +216,29 @@ def test_xgmi_peer_halos_across_processes(world, taps, ch):
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     kind, ok = q.get(timeout=5)
     assert kind == "xgmi" and ok
+
+
+@pytest.mark.parametrize("dtype,ch,stage", [(np.int16, 1, 1), (np.int16, 2, 1), (np.int16, 1, 0), (np.uint8, 1, 0),
+                                            (np.uint8, 1, 1)])
+@pytest.mark.parametrize("n", [8, 16, 4096, 4099, 1 << 20, (1 << 20) + 16, 3])
+def test_segment_with_halos_matches_oracle(dtype, ch, stage, n):
+    """fir1d_fixed_segment_dev: the register kernel with the halos in place of the zero padding
+    (n*ch a whole number of vectors) or rows + edge kernels (otherwise), every tap count 1..9
+    and a 12-tap generic case, one-sided and absent halos."""
+    rng = np.random.default_rng(n + ch)
+    lo, hi = (0, 256) if dtype == np.uint8 else (-32768, 32768)
+    x = rng.integers(lo, hi, n * ch, dtype=dtype)
+    xd = torch.from_numpy(x).to(DEV)
+    for L in list(range(1, 10)) + [12]:
+        hq = rng.integers(-3000, 3000, L) if dtype == np.int16 else rng.integers(-300, 900, L)
+        hl_n, hr_n = (L - 1 - L // 2) * ch, (L // 2) * ch
+        hlv = rng.integers(lo, hi, hl_n, dtype=dtype)
+        hrv = rng.integers(lo, hi, hr_n, dtype=dtype)
+        for use_l, use_r in ((True, True), (False, True), (True, False), (False, False)):
+            left = torch.from_numpy(hlv).to(DEV) if use_l and hl_n else None
+            right = torch.from_numpy(hrv).to(DEV) if use_r and hr_n else None
+            y = torch_ops.fir1d_fixed_segment_dev(xd, hq, left, right, 12, 32, stage, ch)
+            want = c_oracle().fir1d_rows(x, hq, 12, 32, stage, channels=ch,
+                                         halo_left=hlv if left is not None else None,
+                                         halo_right=hrv if right is not None else None)
+            assert np.array_equal(y.cpu().numpy(), want), (L, use_l, use_r)

@@ -327,6 +327,19 @@ int fir1d_fixed_edges_dev(const void* x_dev, int in_dtype, int64_t n, int channe
     }
 }
 
+int fir1d_fixed_segment_dev(const void* x_dev, int in_dtype, int64_t n, int channels, const int32_t* hq, int taps,
+                            int frac_bits, int acc_bits, int out_stage, const void* halo_left_dev,
+                            const void* halo_right_dev, void* y_dev, void* stream) {
+    try {
+        std::string err;
+        int rc = fir::launch_fir1d_segment(x_dev, in_dtype, n, channels, hq, taps, frac_bits, acc_bits, out_stage,
+                                           halo_left_dev, halo_right_dev, y_dev, (hipStream_t)stream, &err);
+        return rc ? fail(rc, err) : FIR_OK;
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
 int fir2d_fixed(const uint8_t* x, int64_t height, int64_t width, const int32_t* hq, int tap_rows, int tap_cols,
                 int frac_bits, int acc_bits, int out_stage, void* y, int device) {
     try {

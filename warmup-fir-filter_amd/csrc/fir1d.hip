@@ -259,6 +259,41 @@ int launch_fir1d_rows_multi(const void* x, int in_dtype, int64_t rows, int64_t w
     return FIR_OK;
 }
 
+// One shard of a longer single-row signal with its halos (fir1d_fixed_segment_dev): ONE launch
+// of the register kernel with the halos standing in for the zero padding when the segment is
+// a whole number of wave tiles (512 int16 / 4096 u8 samples), else the bulk pass then the edge
+// kernel.
+int launch_fir1d_segment(const void* x, int in_dtype, int64_t n, int ch, const int32_t* hq, int L, int frac,
+                         int acc_bits, int stage, const void* hl, const void* hr, void* y, hipStream_t stream,
+                         std::string* err) {
+    int rc = check_common(in_dtype, 1, n, ch, hq, L, frac, acc_bits, stage, err);
+    if (rc) return rc;
+    const int64_t total = n * ch;
+    if (total == 0) return FIR_OK;
+    if (!x || !y) return *err = "x and y must not be NULL", FIR_EINVAL;
+    if (total % reg_tile_samples(in_dtype == FIR_IN_U8) == 0 &&
+        reg_path_ok(x, y, in_dtype, 1, total, total, ch, hq, L, L, frac, acc_bits)) {
+        hipError_t e;
+        if (in_dtype == FIR_IN_U8)
+            e = stage == FIR_OUT_U8_SAT
+                    ? launch_reg_taps<uint8_t, FIR_OUT_U8_SAT, 1, 1>(L, x, y, 1, total, total, hq, frac, acc_bits, stream, hl, hr)
+                    : launch_reg_taps<uint8_t, FIR_OUT_I32, 1, 1>(L, x, y, 1, total, total, hq, frac, acc_bits, stream, hl, hr);
+        else if (ch == 1)
+            e = stage == FIR_OUT_U8_SAT
+                    ? launch_reg_taps<int16_t, FIR_OUT_U8_SAT, 1, 1>(L, x, y, 1, total, total, hq, frac, acc_bits, stream, hl, hr)
+                    : launch_reg_taps<int16_t, FIR_OUT_I32, 1, 1>(L, x, y, 1, total, total, hq, frac, acc_bits, stream, hl, hr);
+        else
+            e = stage == FIR_OUT_U8_SAT
+                    ? launch_reg_taps<int16_t, FIR_OUT_U8_SAT, 2, 1>(L, x, y, 1, total, total, hq, frac, acc_bits, stream, hl, hr)
+                    : launch_reg_taps<int16_t, FIR_OUT_I32, 2, 1>(L, x, y, 1, total, total, hq, frac, acc_bits, stream, hl, hr);
+        if (e != hipSuccess) return *err = std::string("fir1d segment launch failed: ") + hipGetErrorString(e), FIR_EHIP;
+        return FIR_OK;
+    }
+    rc = launch_fir1d_rows(x, in_dtype, 1, n, ch, hq, L, frac, acc_bits, stage, y, stream, err);
+    if (rc) return rc;
+    return launch_fir1d_edges(x, in_dtype, n, ch, hq, L, frac, acc_bits, stage, hl, hr, y, stream, err);
+}
+
 int launch_fir1d_edges(const void* x, int in_dtype, int64_t n, int ch, const int32_t* hq, int L, int frac,
                        int acc_bits, int stage, const void* hl, const void* hr, void* y, hipStream_t stream,
                        std::string* err) {

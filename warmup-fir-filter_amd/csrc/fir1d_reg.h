@@ -132,7 +132,28 @@ struct RowGeom {
     uint32_t rowlen32;  // width * channels, valid when multi_row
     int multi_row;      // rows > 1 (then total < 2^32 is guaranteed by the host)
     int aligned;        // one row, or rows a whole number of vectors: no vector straddles a row
+    // One row that is a shard of a longer signal, a whole number of TILES (64*U vectors), so
+    // vectors -1 and nvec are exactly the edge vectors lanes 0 / 63 load: the samples just
+    // before / after the row (HL / HR of them, device memory, e.g. a neighbour's HBM mapped
+    // over xGMI) stand in for the zero padding there, and the edge outputs come out final.
+    const void* halo_l;
+    const void* halo_r;
 };
+
+// The vector before the row (v = -1: its last `hl` samples = halo[0..hl)) or after it
+// (v = nvec: its first `hr` samples = halo[0..hr)), zeros elsewhere.
+template <typename InT>
+__device__ __forceinline__ void load_halo_vec(const void* halo, bool left, int nh, uint32_t (&d)[4]) {
+    constexpr int EPD = InTraits<InT>::kPerDword;
+    constexpr int VEC = 4 * EPD;
+    const InT* h = static_cast<const InT*>(halo);
+    d[0] = d[1] = d[2] = d[3] = 0;
+    for (int j = 0; j < nh; ++j) {
+        const int pos = left ? VEC - nh + j : j;
+        const uint32_t e = (uint32_t)h[j] & (EPD == 4 ? 0xFFu : 0xFFFFu);
+        d[pos / EPD] |= e << ((32 / EPD) * (pos % EPD));
+    }
+}
 
 // Load vector `v` (VEC samples) into 4 dwords: one 16-byte load when wholly in range,
 // element-wise with zero fill at the ragged end, zeros past the end / before 0.
@@ -432,9 +453,19 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
         const int64_t vb = tile * (kWave * U);
         uint32_t hv[4] = {0, 0, 0, 0};
         if (lane == 0) {
-            if (NDL > 0) load_vec<InT, false>(x, vb - 1, nvec, total, hv);
+            if (NDL > 0) {
+                if (vb == 0 && g.halo_l != nullptr)
+                    load_halo_vec<InT>(g.halo_l, true, HLE, hv);
+                else
+                    load_vec<InT, false>(x, vb - 1, nvec, total, hv);
+            }
         } else if (lane == kWave - 1) {
-            if (NDR > 0) load_vec<InT, false>(x, vb + kWave * U, nvec, total, hv);
+            if (NDR > 0) {
+                if (vb + kWave * U == nvec && g.halo_r != nullptr)
+                    load_halo_vec<InT>(g.halo_r, false, HRE, hv);
+                else
+                    load_vec<InT, false>(x, vb + kWave * U, nvec, total, hv);
+            }
         }
         uint32_t nxt[U][4];
         if constexpr (PERSIST) {  // next tile's loads go out before this tile's math and stores

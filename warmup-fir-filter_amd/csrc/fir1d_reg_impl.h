@@ -11,7 +11,8 @@
 
 namespace fir {
 
-// Hot-kernel shape chosen by the A/B microbenchmark (tools/microbench; profiles/r01/micro_*.txt):
+// Hot-kernel shape chosen by the A/B microbenchmark (tools/microbench; profiles/r01/micro_*.txt;
+// the chunk counts kRegU live in fir1d_reg_launch.h):
 // one 64-vector chunk per wave, default-policy loads and stores (non-temporal stores cost
 // 25-45 % on this 1:2 read:write stream; more chunks per wave or a persistent grid 3-15 %),
 // int32 outputs staged through LDS into whole 1 KiB store instructions (272 -> 257 us).
@@ -19,20 +20,21 @@ namespace fir {
 // over 4 KiB; 104.6 -> 94.0 us at 2^28, profiles/r01/micro_u8_chunks.txt); a fused bank
 // (F > 1) runs best at 2 chunks with its packed-16 filters (4-filter 3-tap bank: 259 us at 1
 // chunk on v_dot2, 229 us at 2 chunks with packed-16; profiles/r01/micro_u8_pk16.txt).
-template <typename InT, int F>
-constexpr int kRegU = sizeof(InT) == 1 ? (F == 1 ? 4 : 2) : 1;
 constexpr int kRegFlags = kCoal;
 constexpr int kPersistBlocks = 2048;
 
 template <typename InT, int STAGE, int L, int CH, int F, int FL>
 static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
-                                   const int32_t* hq, int frac, int acc_bits, hipStream_t stream) {
+                                   const int32_t* hq, int frac, int acc_bits, hipStream_t stream, const void* hl,
+                                   const void* hr) {
     using OutT = typename OutTraits<STAGE>::T;
     RowGeom g;
     g.total = total;
     g.rowlen32 = (uint32_t)(rows > 1 ? rowlen : 0);
     g.multi_row = rows > 1;
     g.aligned = rows == 1 || rowlen % (4 * InTraits<InT>::kPerDword) == 0;
+    g.halo_l = hl;
+    g.halo_r = hr;
     TapsN<L, F> t;
     for (int f = 0; f < F; ++f)
         for (int k = 0; k < L; ++k) t.h[f][k] = hq[f * L + k];
@@ -51,7 +53,8 @@ static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t
 // no accumulator can wrap: 255 * sum|h| + 2^(f-1) < 2^(acc_bits-1) for every filter.
 template <typename InT, int STAGE, int L, int CH, int F>
 static hipError_t launch_reg(const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
-                             const int32_t* hq, int frac, int acc_bits, hipStream_t stream) {
+                             const int32_t* hq, int frac, int acc_bits, hipStream_t stream, const void* hl,
+                             const void* hr) {
     bool taps16 = true;
     for (int k = 0; k < F * L; ++k) taps16 &= hq[k] >= -32768 && hq[k] <= 32767;
     const bool acc32 = acc_bits == 32;
@@ -68,33 +71,33 @@ static hipError_t launch_reg(const void* x, void* y, int64_t rows, int64_t total
             for (int k = 0; k < F * L; ++k) probe.h[k / L][k % L] = hq[k];
             if (taps16 && nowrap && (plan_u8_pk16(probe, frac) & kU8Pk16))
                 return launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kU8Dot2 | kU8Pk16>(x, y, rows, total, rowlen, hq,
-                                                                                          frac, acc_bits, stream);
+                                                                                          frac, acc_bits, stream, hl, hr);
         }
         if (taps16 && nowrap)
-            return launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kU8Dot2>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
+            return launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kU8Dot2>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream, hl, hr);
     }
     if constexpr (sizeof(InT) == 2 && CH == 1) {
         if (taps16)
-            return acc32 ? launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kDot2 | kAcc32>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream)
-                         : launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kDot2>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
+            return acc32 ? launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kDot2 | kAcc32>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream, hl, hr)
+                         : launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kDot2>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream, hl, hr);
     }
-    return acc32 ? launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kAcc32>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream)
-                 : launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
+    return acc32 ? launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kAcc32>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream, hl, hr)
+                 : launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream, hl, hr);
 }
 
 template <typename InT, int STAGE, int CH, int F>
 hipError_t launch_reg_taps(int L, const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
-                                  const int32_t* hq, int frac, int acc_bits, hipStream_t s) {
+                           const int32_t* hq, int frac, int acc_bits, hipStream_t s, const void* hl, const void* hr) {
     switch (L) {
-        case 1: return launch_reg<InT, STAGE, 1, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 2: return launch_reg<InT, STAGE, 2, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 3: return launch_reg<InT, STAGE, 3, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 4: return launch_reg<InT, STAGE, 4, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 5: return launch_reg<InT, STAGE, 5, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 6: return launch_reg<InT, STAGE, 6, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 7: return launch_reg<InT, STAGE, 7, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 8: return launch_reg<InT, STAGE, 8, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
-        case 9: return launch_reg<InT, STAGE, 9, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s);
+        case 1: return launch_reg<InT, STAGE, 1, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr);
+        case 2: return launch_reg<InT, STAGE, 2, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr);
+        case 3: return launch_reg<InT, STAGE, 3, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr);
+        case 4: return launch_reg<InT, STAGE, 4, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr);
+        case 5: return launch_reg<InT, STAGE, 5, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr);
+        case 6: return launch_reg<InT, STAGE, 6, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr);
+        case 7: return launch_reg<InT, STAGE, 7, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr);
+        case 8: return launch_reg<InT, STAGE, 8, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr);
+        case 9: return launch_reg<InT, STAGE, 9, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr);
         default: return hipErrorInvalidValue;
     }
 }

@@ -9,8 +9,19 @@ namespace fir {
 
 // Launch fir1d_reg_kernel for L taps (1..9) of F filters over rows x rowlen samples of
 // InT with CH interleaved channels; picks the dot2 / acc32 / u8 no-wrap variant.
+// halo_l / halo_r (rows == 1, total a multiple of reg_tile_samples): device samples around
+// the row that replace its zero padding (RowGeom::halo_l / halo_r).
 template <typename InT, int STAGE, int CH, int F>
 hipError_t launch_reg_taps(int L, const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
-                           const int32_t* hq, int frac, int acc_bits, hipStream_t s);
+                           const int32_t* hq, int frac, int acc_bits, hipStream_t s, const void* halo_l = nullptr,
+                           const void* halo_r = nullptr);
+
+// Chunks of 64 vectors per wave (the tile), by sample type and filter count (rationale and
+// measurements: fir1d_reg_impl.h).
+template <typename InT, int F>
+constexpr int kRegU = sizeof(InT) == 1 ? (F == 1 ? 4 : 2) : 1;
+
+// Samples per wave tile of the single-filter register kernel (64 lanes x U chunks x 16 bytes).
+inline int64_t reg_tile_samples(bool u8) { return u8 ? 64 * kRegU<uint8_t, 1> * 16 : 64 * kRegU<int16_t, 1> * 8; }
 
 }  // namespace fir

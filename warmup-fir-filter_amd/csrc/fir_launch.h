@@ -22,6 +22,11 @@ int launch_fir1d_edges(const void* x, int in_dtype, int64_t n, int ch, const int
                        int acc_bits, int stage, const void* halo_left, const void* halo_right, void* y,
                        hipStream_t stream, std::string* err);
 
+// A single-row shard with its halos: bulk + edges in one register-kernel launch when possible.
+int launch_fir1d_segment(const void* x, int in_dtype, int64_t n, int ch, const int32_t* hq, int L, int frac,
+                         int acc_bits, int stage, const void* halo_left, const void* halo_right, void* y,
+                         hipStream_t stream, std::string* err);
+
 // 2-D fixed FIR over a uint8 frame.
 int launch_fir2d(const uint8_t* x, int64_t height, int64_t width, const int32_t* hq, int tap_rows, int tap_cols,
                  int frac, int acc_bits, int stage, void* y, hipStream_t stream, std::string* err);

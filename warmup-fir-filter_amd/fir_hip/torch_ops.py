@@ -92,15 +92,8 @@ def fir1d_fixed_rows_multi_dev(x: torch.Tensor, hq2, frac_bits: int = 12, acc_bi
     return out
 
 
-def fir1d_fixed_edges_dev(x: torch.Tensor, hq, out: torch.Tensor, halo_left, halo_right, frac_bits: int = 12,
-                          acc_bits: int = 32, out_stage: int = OUT_I32, channels: int = 1, stream=None) -> torch.Tensor:
-    """Recompute the halo-dependent edge outputs of a 1-D segment (see fir_hip.h).  A halo is a
-    device tensor of the segment's dtype, None (zeros), or an int device address holding the
-    halo samples (e.g. a neighbour's HBM mapped by fir_hip.ipc_import: read over xGMI)."""
-    _check_dev(x, "x")
-    _check_dev(out, "out")
-    t = _taps(hq)
-    L = t.n
+def _halo_ptrs(x: torch.Tensor, L: int, channels: int, halo_left, halo_right):
+    """ctypes pointers of the two halos (a device tensor of x's dtype, None, or an int address)."""
     hl_n, hr_n = (L - 1 - L // 2) * channels, (L // 2) * channels
     ptrs = []
     for h, n, name in ((halo_left, hl_n, "halo_left"), (halo_right, hr_n, "halo_right")):
@@ -113,12 +106,49 @@ def fir1d_fixed_edges_dev(x: torch.Tensor, hq, out: torch.Tensor, halo_left, hal
             if h.dtype != x.dtype or h.numel() != n:
                 raise FirHipError(f"{name} must hold {n} samples of {x.dtype}")
             ptrs.append(ctypes.c_void_p(h.data_ptr()))
+    return ptrs
+
+
+def fir1d_fixed_edges_dev(x: torch.Tensor, hq, out: torch.Tensor, halo_left, halo_right, frac_bits: int = 12,
+                          acc_bits: int = 32, out_stage: int = OUT_I32, channels: int = 1, stream=None) -> torch.Tensor:
+    """Recompute the halo-dependent edge outputs of a 1-D segment (see fir_hip.h).  A halo is a
+    device tensor of the segment's dtype, None (zeros), or an int device address holding the
+    halo samples (e.g. a neighbour's HBM mapped by fir_hip.ipc_import: read over xGMI)."""
+    _check_dev(x, "x")
+    _check_dev(out, "out")
+    t = _taps(hq)
+    L = t.n
+    ptrs = _halo_ptrs(x, L, channels, halo_left, halo_right)
     if x.numel() % channels:
         raise FirHipError("segment length must be a multiple of channels")
     _check(lib().fir1d_fixed_edges_dev(ctypes.c_void_p(x.data_ptr()), _IN[x.dtype], x.numel() // channels, channels,
                                        t.ptr, t.n, int(frac_bits), int(acc_bits), int(out_stage), ptrs[0], ptrs[1],
                                        ctypes.c_void_p(out.data_ptr()), _stream_ptr(x, stream)),
            "fir1d_fixed_edges_dev")
+    return out
+
+
+def fir1d_fixed_segment_dev(x: torch.Tensor, hq, halo_left, halo_right, frac_bits: int = 12, acc_bits: int = 32,
+                            out_stage: int = OUT_I32, channels: int = 1, out: torch.Tensor | None = None,
+                            stream=None) -> torch.Tensor:
+    """One shard of a longer single-row signal with its halos (tensor, None = zeros, or an int
+    device address such as a neighbour's mapped HBM): bulk + edges, one launch when possible."""
+    _check_dev(x, "x")
+    if x.dtype not in _IN:
+        raise FirHipError(f"x dtype must be uint8 or int16, got {x.dtype}")
+    t = _taps(hq)
+    if out is None:
+        out = torch.empty(x.shape, dtype=_OUT_DTYPE[out_stage], device=x.device)
+    _check_dev(out, "out")
+    if out.shape != x.shape or out.dtype != _OUT_DTYPE[out_stage]:
+        raise FirHipError("out must match x's shape and the out_stage dtype")
+    if x.numel() % channels:
+        raise FirHipError("segment length must be a multiple of channels")
+    hl, hr = _halo_ptrs(x, t.n, channels, halo_left, halo_right)
+    _check(lib().fir1d_fixed_segment_dev(ctypes.c_void_p(x.data_ptr()), _IN[x.dtype], x.numel() // channels,
+                                         channels, t.ptr, t.n, int(frac_bits), int(acc_bits), int(out_stage), hl, hr,
+                                         ctypes.c_void_p(out.data_ptr()), _stream_ptr(x, stream)),
+           "fir1d_fixed_segment_dev")
     return out
 
 
