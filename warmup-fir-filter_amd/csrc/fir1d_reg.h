@@ -40,6 +40,9 @@ enum RegFlags : int {
     // clamp(V >> (f-s), 0, 255).  The other filters keep the byte-pair v_dot2 form.
     kU8Pk16 = 256,
     kU8PkHi8 = 1024,  // every filter unsigned with f - s == 8: the output byte is V's high byte
+    kHalo = 2048,     // a shard with halos (RowGeom::halo_l / halo_r) instead of zero padding; a
+                      // separate instantiation: the extra edge-load branches cost the plain
+                      // kernel 1.5 % (256.9 -> 260.8 us, tools/lib_ab.py)
 };
 
 constexpr int kNumXcd = 8;
@@ -428,6 +431,7 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
     constexpr bool ACC32 = FLAGS & kAcc32;
     constexpr bool U8DOT2 = (FLAGS & kU8Dot2) && sizeof(InT) == 1 && CH == 1;
     constexpr bool U8PK = U8DOT2 && (FLAGS & kU8Pk16) && STAGE == FIR_OUT_U8_SAT;
+    constexpr bool HALO = (FLAGS & kHalo) != 0;
     constexpr bool COAL = (FLAGS & kCoal) && STAGE == FIR_OUT_I32;
     constexpr int WPB = kBlock / kWave;
     uint32_t bias = 0;
@@ -454,14 +458,14 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
         uint32_t hv[4] = {0, 0, 0, 0};
         if (lane == 0) {
             if (NDL > 0) {
-                if (vb == 0 && g.halo_l != nullptr)
+                if (HALO && vb == 0 && g.halo_l != nullptr)
                     load_halo_vec<InT>(g.halo_l, true, HLE, hv);
                 else
                     load_vec<InT, false>(x, vb - 1, nvec, total, hv);
             }
         } else if (lane == kWave - 1) {
             if (NDR > 0) {
-                if (vb + kWave * U == nvec && g.halo_r != nullptr)
+                if (HALO && vb + kWave * U == nvec && g.halo_r != nullptr)
                     load_halo_vec<InT>(g.halo_r, false, HRE, hv);
                 else
                     load_vec<InT, false>(x, vb + kWave * U, nvec, total, hv);

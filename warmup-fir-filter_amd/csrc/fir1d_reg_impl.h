@@ -43,6 +43,15 @@ static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t
         if (!(plan_u8_pk16(t, frac) & kU8Pk16)) return hipErrorInvalidValue;  // caller checked
     int64_t ntiles = 0, blocks = 0;
     reg_launch_geometry<InT, kRegU<InT, F>, FL>(total, kPersistBlocks, &ntiles, &blocks);
+    if constexpr (F == 1) {
+        if (hl != nullptr || hr != nullptr) {
+            hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, kRegU<InT, F>, FL | kHalo, F>), dim3((unsigned)blocks),
+                               dim3(kBlock), 0, stream, (const InT*)x, (OutT*)y, g, t, 32 - acc_bits, frac, ntiles);
+            return hipGetLastError();
+        }
+    } else if (hl != nullptr || hr != nullptr) {
+        return hipErrorInvalidValue;  // shards with halos are single-filter calls
+    }
     hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, kRegU<InT, F>, FL, F>), dim3((unsigned)blocks), dim3(kBlock), 0,
                        stream, (const InT*)x, (OutT*)y, g, t, 32 - acc_bits, frac, ntiles);
     return hipGetLastError();
