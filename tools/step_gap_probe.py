@@ -3,6 +3,7 @@ steps of several compositions around the 2^28-sample int16 bulk kernel (HIP even
 compute stream, clocks warmed first):
 
   bulk          the bulk kernel alone
+  segment       one launch of the FIR kernel that reads the halos itself (the xGMI step)
   bulk+edge     + the one-block edge kernel (halos from a resident tensor)
   bulk+wait+edge  + a stream wait on an event recorded (once) on another stream
   bulk+xchg+edge  + the RCCL ring-of-one exchange posted every step (fir_hip.sharded)
@@ -88,13 +89,16 @@ def main():
             torch_ops.fir1d_fixed_edges_dev(x, taps, y, *ex.halos(), 12, 32, fir_hip.OUT_I32, stream=side)
         bulk()
 
+    def v_segment():  # the xGMI step's launch: halos read by the FIR kernel itself (local tensors here)
+        torch_ops.fir1d_fixed_segment_dev(x, taps, hl, hr, 12, 32, fir_hip.OUT_I32, out=y)
+
     def v_xchg_first():  # exchange first, its wait before the bulk, then bulk + edge back to back
         works = ex.post()
         sharded.wait_all(works)
         bulk()
         edge(*ex.halos())
 
-    variants = [("xchg-first", v_xchg_first), ("side-edge", v_side_edge), ("bulk", v_bulk), ("bulk+edge", v_edge), ("bulk+wait+edge", v_wait), ("bulk+xchg+edge", v_xchg),
+    variants = [("segment", v_segment), ("xchg-first", v_xchg_first), ("side-edge", v_side_edge), ("bulk", v_bulk), ("bulk+edge", v_edge), ("bulk+wait+edge", v_wait), ("bulk+xchg+edge", v_xchg),
                 ("xchg-side", v_side)]
     if len(sys.argv) > 2:  # a subset, e.g. for a trace
         variants = [v for v in variants if v[0] in sys.argv[2].split(",")]
