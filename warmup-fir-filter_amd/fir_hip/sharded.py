@@ -1,17 +1,20 @@
-"""Long-vector sharding across ranks with an (L-1)-sample halo exchange.
+"""Long-vector sharding across ranks with an (L-1)-sample halo.
 
-One process per GPU (``torch.distributed``; backend "nccl" is RCCL over xGMI on ROCm,
-"gloo" for the CPU tests).  A signal of N samples is cut into contiguous segments, one
-per rank.  An L-tap centre-aligned filter makes every segment need the last
-``HL = L-1-L//2`` samples of its left neighbour and the first ``HR = L//2`` samples of
-its right neighbour (times ``channels`` for interleaved complex samples); the global
-ends are zero padded.  That exchange is the only communication: two point-to-point
-messages of a few bytes per neighbour pair, posted as one ``batch_isend_irecv`` group.
+One process per GPU (``torch.distributed``; backend "nccl" is RCCL on ROCm, "gloo" for the
+CPU tests).  A signal of N samples is cut into contiguous segments, one per rank.  An L-tap
+centre-aligned filter makes every segment need the last ``HL = L-1-L//2`` samples of its
+left neighbour and the first ``HR = L//2`` samples of its right neighbour (times
+``channels`` for interleaved complex samples); the global ends are zero padded.  That halo is
+the only data that crosses GPUs.  Two sources:
 
-``sharded_fir1d_step`` overlaps the exchange with the bulk of the work: the full
-segment kernel runs first (its zero-padded edge outputs are provisional), the halo
-messages are in flight meanwhile, and a one-block edge kernel rewrites the HL + HR
-edge outputs once the halos have arrived (same stream, so it is ordered after both).
+* :class:`XgmiHalo` (default, :func:`make_halo_source`): each rank maps its neighbours'
+  resident segments once (HIP IPC through the C ABI); every pass is then one launch of the
+  FIR kernel whose edge lanes read the halo from the neighbours' HBM over xGMI
+  (``torch_ops.fir1d_fixed_segment_dev``).
+* :class:`HaloExchange` (fallback, ``FIR_HALO=rccl``): two point-to-point messages of a few
+  bytes per neighbour pair every pass, one ``batch_isend_irecv`` group, overlapped with the
+  bulk kernel; a one-block edge kernel then rewrites the HL + HR edge outputs
+  (``sharded_fir1d_step`` is the one-shot form).
 """
 from __future__ import annotations
 
@@ -127,9 +130,9 @@ class XgmiHalo:
         if seg.numel() < max(hl, hr):
             raise ValueError("segment shorter than the filter halo")
         handle, off = fir_hip.ipc_export(seg.data_ptr())
-        cpu = seg.cpu()
+        np_dtype = seg[:1].cpu().numpy().dtype
         mine = {"handle": handle, "offset": off, "numel": seg.numel(), "elt": seg.element_size(),
-                "first": cpu[:hr].numpy().tobytes(), "last": cpu[seg.numel() - hl:].numpy().tobytes()}
+                "first": seg[:hr].cpu().numpy().tobytes(), "last": seg[seg.numel() - hl:].cpu().numpy().tobytes()}
         infos = [None] * world
         dist.all_gather_object(infos, mine, group=group)
         dev = seg.device.index
@@ -144,7 +147,7 @@ class XgmiHalo:
                 got = fir_hip.peek(self.left_ptr, hl * p["elt"])
                 if got != p["last"]:
                     raise RuntimeError("left neighbour mapping reads the wrong samples")
-                self.left_host = np.frombuffer(got, dtype=cpu.numpy().dtype).copy()
+                self.left_host = np.frombuffer(got, dtype=np_dtype).copy()
             if rank < world - 1 and hr:
                 p = infos[rank + 1]
                 self.right_ptr = fir_hip.ipc_import(p["handle"], p["offset"], dev)
@@ -152,7 +155,7 @@ class XgmiHalo:
                 got = fir_hip.peek(self.right_ptr, hr * p["elt"])
                 if got != p["first"]:
                     raise RuntimeError("right neighbour mapping reads the wrong samples")
-                self.right_host = np.frombuffer(got, dtype=cpu.numpy().dtype).copy()
+                self.right_host = np.frombuffer(got, dtype=np_dtype).copy()
         except Exception:
             self.close()
             raise
