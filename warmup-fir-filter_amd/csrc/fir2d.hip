@@ -26,6 +26,10 @@ constexpr int kStrip2dGen = 16;  // VGPRs (4 waves/SIMD): 45.8 vs 48.5 us for 16
 // packed-16 25.7 -> 23.9 us at 3, general dot2 45.5 -> 43.9 us at 2; profiles/r01/micro2d_pk16.txt)
 constexpr int kPdSep = 3;
 constexpr int kPdGen = 2;
+// packed-16 form: 32-row strips, rows 4 ahead (23.5 vs 24.3 us for 16 rows / 3 ahead; a
+// memory-only twin of the same loop takes 21.1 us, profiles/r01/micro2d_copy.txt)
+constexpr int kStrip2dPk = 32;
+constexpr int kPdPk = 4;
 
 // Generic: one output per thread, exact int64 sum, global loads (L1/L2 absorb the reuse).
 struct Taps2G {
@@ -134,19 +138,20 @@ static hipError_t launch2d_reg(const uint8_t* x, void* y, int64_t H, int64_t W, 
         // packed 16-bit pixel pairs when the whole sum provably fits 16 bits (u8 stage only)
         if constexpr (STAGE == FIR_OUT_U8_SAT) {
             const int pk = nowrap ? plan_pk16(t, t.col, rowt, frac) : 0;
+            const dim3 gpk = fir2d_reg_grid<kVec2d, kStrip2dPk>(H, W);
             if (pk == (kMode2dPk16 | kMode2dPkHi8)) {
-                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, SNW | kMode2dPk16 | kMode2dPkHi8, 1, kPdSep>),
-                                   grid, dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
+                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dPk, SNW | kMode2dPk16 | kMode2dPkHi8, 1, kPdPk>),
+                                   gpk, dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
                 return hipGetLastError();
             }
             if (pk == kMode2dPk16) {
-                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, SNW | kMode2dPk16, 1, kPdSep>), grid,
+                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dPk, SNW | kMode2dPk16, 1, kPdPk>), gpk,
                                    dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
                 return hipGetLastError();
             }
             if (pk == (kMode2dPk16 | kMode2dPkSigned)) {
-                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, SNW | kMode2dPk16 | kMode2dPkSigned, 1, kPdSep>),
-                                   grid, dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
+                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dPk, SNW | kMode2dPk16 | kMode2dPkSigned, 1, kPdPk>),
+                                   gpk, dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
                 return hipGetLastError();
             }
         }
