@@ -20,6 +20,8 @@ prints ONE JSON line.  Extra keys:
                 bounded leading slice of the same input (BASELINE.md's "NumPy CPU path")
   cpu_baseline_numpy_threads  the same NumPy path over contiguous slices on a thread pool of
                 the host's cores (core count in `cores`)
+  cpu_baseline_python_loop  the reference's own per-sample Python loop (restated in
+                oracle.fir1d_loop) on 2^16 samples: what its CPU path costs (1-D workloads)
   host_issue_us_per_step  host time to enqueue one timed step (diagnostic: < ms_per_step
                 means the GPU, not Python, sets the pace)
 Other workloads: `cplx_i16` / `fir2d_u8` measure configs[2] / configs[4]; `fir1d_u8` the
@@ -203,6 +205,15 @@ class Workload:
             torch_ops.compare_metrics_dev(self.x, self.fixed, out=self.y, work=self.work)
         else:
             torch_ops.fir1d_fixed_rows_dev(self.x, self.taps, 12, 32, fir_hip.OUT_I32, self.channels, out=self.y)
+
+    def dominant(self):
+        """The step's dominant kernel alone (roofline timing): the halo-reading launch of an
+        xGMI-sharded step, else the bulk kernel."""
+        if self.sharded_1d and self.halo_kind == "xgmi":
+            torch_ops.fir1d_fixed_segment_dev(self.x, self.taps, *self.halo_src.halos(), 12, 32, fir_hip.OUT_I32,
+                                              self.channels, out=self.y)
+        else:
+            self.bulk()
 
     def step(self):
         """One pass of the hot path (for N > 1: bulk kernel, then the halo-dependent edges)."""
@@ -408,14 +419,14 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # Roofline: the dominant (bulk) kernel alone, `steps` back-to-back launches on the stream it
+    # Roofline: the dominant kernel alone (wl.dominant), `steps` back-to-back launches on the stream it
     # runs on, bracketed by two HIP events (events between launches would perturb the stream:
     # each record adds a ~11 us gap).  Average duration = event time / launches.
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     ev0.record()
     for _ in range(args.steps):
-        wl.bulk()
+        wl.dominant()
     ev1.record()
     ev1.synchronize()
     kern_avg_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
@@ -434,7 +445,7 @@ def main() -> int:
             ok = int(f.item()) == 0
         parity = "bit-exact vs oracle (full output, every rank)" if ok else "MISMATCH"
 
-    cpu = cpu_np = cpu_np_mt = None
+    cpu = cpu_np = cpu_np_mt = cpu_loop = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         nthr = _cpu_threads()
         wl.oracle(nthr)  # warm (page-in, thread pool)
@@ -465,6 +476,17 @@ def main() -> int:
         cpu_np_mt = {"value": round(done_m / tm / 1e9, 5), "unit": wl.unit, "cores": nthr, "kind": "port",
                      "sample": f"NumPy restatement on the first {done_m} units, {nthr} slices on a thread pool, "
                                f"{tm:.1f} s"}
+        if args.workload in ("fir1d_i16", "fir1d_u8"):  # the reference's own per-sample Python loop
+            from oracle import fir_oracle as fo
+
+            m = 1 << 16
+            tl0 = time.perf_counter()
+            fo.fir1d_loop(wl.x_host.reshape(-1)[:m], wl.taps.h, 12, 32,
+                          fo.OUT_I32 if args.workload == "fir1d_i16" else fo.OUT_U8_SAT)
+            tl = time.perf_counter() - tl0
+            cpu_loop = {"value": round(m / tl / 1e9, 7), "unit": wl.unit, "cores": 1, "kind": "port",
+                        "sample": f"the reference's per-sample x per-tap Python loop (oracle.fir1d_loop, "
+                                  f"fir_1d_fixed_ref.py:94-128) on the first {m} samples, {tl:.2f} s"}
 
     traffic = None
     pmc = ROOT / "profiles" / f"pmc_{args.workload}.json"
@@ -504,6 +526,7 @@ def main() -> int:
         "cpu_baseline": cpu,
         "cpu_baseline_numpy": cpu_np,
         "cpu_baseline_numpy_threads": cpu_np_mt,
+        "cpu_baseline_python_loop": cpu_loop,
         "parity": parity,
         "host_issue_us_per_step": round(t_issue / args.steps * 1e6, 1),
     }

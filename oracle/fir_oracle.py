@@ -15,6 +15,8 @@ Reference lines restated (paths relative to the reference root):
                   fir_1d/model/python/fir_1d_fixed_ref.py:75     (cast to uint8)
   wrap_round      fir_1d/model/python/fir_1d_fixed_ref.py:94,110-120 (mask to acc_bits,
                   sign-extend, + 2^(f-1), arithmetic >> f)
+  fir1d_loop      fir_1d/model/python/fir_1d_fixed_ref.py:94-128 as its per-sample Python loop
+                  (the reference's CPU cost, timed by bench.py on a small sample)
   fir1d_rows      fir_1d/model/python/fir_1d_fixed_ref.py:95-128 (same-mode, centre-aligned,
                   zero-padded MAC, saturate :123-126) applied per row as in
                   fir_1d/sim/vector/gen_fixed_output.py:34-60
@@ -135,6 +137,31 @@ def fir1d_rows(x, hq, frac_bits: int = 12, acc_bits: int = 32, out_stage: int = 
     y = _stage(q, out_stage)
     y = y.reshape(rows, channels, w).transpose(0, 2, 1).reshape(shape)
     return np.ascontiguousarray(y)
+
+
+def fir1d_loop(x, hq, frac_bits: int = 12, acc_bits: int = 32, out_stage: int = OUT_U8_SAT) -> list:
+    """The reference's own per-sample x per-tap Python loop (fir_1d_fixed_ref.py:94-128) over
+    one row, as plain Python ints: bounds-checked zero padding, mask to acc_bits, sign
+    restore, + 2^(f-1), >> f, then saturation (OUT_U8_SAT) or none (OUT_I32, variant a6).
+    Only for small inputs: bench.py times it to show what the reference's CPU path costs."""
+    xs = [int(v) for v in x]
+    hs = [int(v) for v in hq]
+    n_x, n_h, c = len(xs), len(hs), len(hs) // 2
+    mask, sign, bias = (1 << acc_bits) - 1, 1 << (acc_bits - 1), 1 << (frac_bits - 1)
+    out = []
+    for n in range(n_x):
+        acc = 0
+        for k in range(n_h):
+            i = n - k + c
+            acc += (xs[i] if 0 <= i < n_x else 0) * hs[k]
+        acc &= mask
+        if acc & sign:
+            acc -= 1 << acc_bits
+        v = (acc + bias) >> frac_bits
+        if out_stage == OUT_U8_SAT:
+            v = 0 if v < 0 else (255 if v > 255 else v)
+        out.append(v)
+    return out
 
 
 def fir_1d_fixed_golden(x, h, frac_bits: int = 12, acc_bits: int = 32, coeff_bits: int = 16) -> np.ndarray:
