@@ -70,7 +70,7 @@ static void launch_memcpy2d(const uint8_t* x, uint8_t* y, int64_t H, int64_t W, 
     CK(hipMemcpyAsync(y, x, H * W, hipMemcpyDeviceToDevice, s));
 }
 
-template <int VEC, int STRIP, int MODE, int MINW = 1, int PD = 1>
+template <int VEC, int STRIP, int MODE, int MINW = 1, int PD = 1, bool NTL = false>
 static void launch(const uint8_t* x, uint8_t* y, int64_t H, int64_t W, hipStream_t s) {
     Taps2<5, 5> t = {};
     for (int m = 0; m < 5; ++m)
@@ -86,7 +86,7 @@ static void launch(const uint8_t* x, uint8_t* y, int64_t H, int64_t W, hipStream
         exit(1);
     }
     const dim3 grid = fir2d_reg_grid<VEC, STRIP>(H, W);
-    hipLaunchKernelGGL((fir2d_reg_kernel<5, 5, FIR_OUT_U8_SAT, VEC, STRIP, MODE, MINW, PD>), grid, dim3(kBlock), 0, s, x, y, H,
+    hipLaunchKernelGGL((fir2d_reg_kernel<5, 5, FIR_OUT_U8_SAT, VEC, STRIP, MODE, MINW, PD, NTL>), grid, dim3(kBlock), 0, s, x, y, H,
                        W, t, 0, 12);
 }
 
@@ -124,6 +124,8 @@ int main(int argc, char** argv) {
         {"pk16hi8 v16 s16 pd3 w6", true, launch<16, 16, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 6, 3>, {}},
         {"pk16hi8 v16 s32 pd3", true, launch<16, 32, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 3>, {}},
         {"pk16hi8 v16 s32 pd4", true, launch<16, 32, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 4>, {}},
+        {"pk16hi8 v16 s32 pd4 ntld", true, launch<16, 32, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 4, true>, {}},
+        {"pk16hi8 v16 s16 pd3 ntld", true, launch<16, 16, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 3, true>, {}},
         {"pk16hi8 v8 s16 pd4", true, launch<8, 16, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 4>, {}},
         {"copy2d v16 s16 pd3", false, launch_copy2d<16, 16, 3, true>, {}},
         {"copy2d v16 s16 pd3 nohalo", false, launch_copy2d<16, 16, 3, false>, {}},

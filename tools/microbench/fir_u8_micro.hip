@@ -127,6 +127,14 @@ int main(int argc, char** argv) {
                          {"pk16 U1", 1, launch_fir<1, PK>, {}},
                          {"pk16 U2", 1, launch_fir<2, PK>, {}},
                          {"pk16 U4", 1, launch_fir<4, PK>, {}},
+                         {"fir U4 ntld", 1, launch_fir<4, kU8Dot2 | kNtLoad>, {}},
+                         {"fir U2 ntld", 1, launch_fir<2, kU8Dot2 | kNtLoad>, {}},
+                         {"fir U4 xcd", 1, launch_fir<4, kU8Dot2 | kXcd>, {}},
+                         {"fir U8", 1, launch_fir<8, kU8Dot2>, {}},
+                         {"fir U1 ntld", 1, launch_fir<1, kU8Dot2 | kNtLoad>, {}},
+                         {"bank pk16 U2 ntld", 2, launch_bank<2, PK | kNtLoad>, {}},
+                         {"bank pk16 U4 ntld", 2, launch_bank<4, PK | kNtLoad>, {}},
+                         {"bank pk16 U1 ntld", 2, launch_bank<1, PK | kNtLoad>, {}},
                          {"bank dot2 U1", 2, launch_bank<1, kU8Dot2>, {}},
                          {"bank dot2 U2", 2, launch_bank<2, kU8Dot2>, {}},
                          {"bank pk16 U1", 2, launch_bank<1, PK>, {}},

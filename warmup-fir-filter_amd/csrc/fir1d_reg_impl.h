@@ -23,6 +23,12 @@ namespace fir {
 constexpr int kRegFlags = kCoal;
 constexpr int kPersistBlocks = 2048;
 
+// One u8 filter streams its input with non-temporal loads (4 chunks per wave: 95.5 -> 88.8 us
+// at 2^28, profiles/r01/micro_u8_nt.txt); the fused bank, the int16 path, the ideal and the
+// 2-D kernels measured slower or equal with them (241 vs 234, 283 vs 272, 393 vs 394, 26.0 vs 23.8 us).
+template <int F>
+constexpr int kU8NtLoad = F == 1 ? kNtLoad : 0;
+
 template <typename InT, int STAGE, int L, int CH, int F, int FL>
 static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
                                    const int32_t* hq, int frac, int acc_bits, hipStream_t stream, const void* hl,
@@ -83,7 +89,8 @@ static hipError_t launch_reg(const void* x, void* y, int64_t rows, int64_t total
                                                                                           frac, acc_bits, stream, hl, hr);
         }
         if (taps16 && nowrap)
-            return launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kU8Dot2>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream, hl, hr);
+            return launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kU8Dot2 | kU8NtLoad<F>>(x, y, rows, total, rowlen, hq, frac,
+                                                                                           acc_bits, stream, hl, hr);
     }
     if constexpr (sizeof(InT) == 2 && CH == 1) {
         if (taps16)

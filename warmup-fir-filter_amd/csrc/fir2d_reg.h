@@ -134,15 +134,16 @@ __device__ __forceinline__ uint32_t clamp_u8_acc(uint32_t acc, int32_t sat_hi) {
 // Branch-free row load: the address is always in bounds (the caller clamps it) and the
 // value is zeroed by a select when the row/column is outside the frame, so the compiler can
 // count outstanding loads exactly (a load inside a branch makes it wait for all of them).
-template <int ND>
+template <int ND, bool NT = false>
 __device__ __forceinline__ void load_row_px(const uint8_t* __restrict__ p, bool ok, uint32_t (&d)[ND]) {
     typedef uint32_t vN __attribute__((ext_vector_type(ND)));
-    const vN q = *reinterpret_cast<const vN*>(p);
+    const vN* a = reinterpret_cast<const vN*>(p);
+    const vN q = NT ? __builtin_nontemporal_load(a) : *a;
 #pragma unroll
     for (int i = 0; i < ND; ++i) d[i] = ok ? q[i] : 0u;
 }
 
-template <int R, int C, int STAGE, int VEC, int STRIP, int MODE, int MINW = 1, int PD = 1>
+template <int R, int C, int STAGE, int VEC, int STRIP, int MODE, int MINW = 1, int PD = 1, bool NTL = false>
 __global__ __launch_bounds__(kBlock, MINW) void fir2d_reg_kernel(const uint8_t* __restrict__ x,
                                                            typename OutTraits<STAGE>::T* __restrict__ y, int64_t H,
                                                            int64_t W, Taps2<R, C> taps, int shl, int frac) {
@@ -192,7 +193,7 @@ __global__ __launch_bounds__(kBlock, MINW) void fir2d_reg_kernel(const uint8_t* 
         const int64_t row = r0 - TOP + t;
         const bool rok = row >= 0 && row < H;
         const uint8_t* rp = row_ptr(row);
-        load_row_px<ND>(rp + colc, rok && active, rows[t]);
+        load_row_px<ND, NTL>(rp + colc, rok && active, rows[t]);
         const uint32_t hv = *reinterpret_cast<const uint32_t*>(rp + hcol);
         hrows[t] = (hok && rok) ? hv : 0u;
     };

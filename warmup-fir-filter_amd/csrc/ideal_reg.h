@@ -21,7 +21,7 @@ struct TapsIdeal {
 };
 
 // NV dwords of u8 samples starting at dword index di (zero fill outside [0, total)).
-template <int NV>
+template <int NV, bool NT = false>
 __device__ __forceinline__ void load_u8_dwords(const uint8_t* __restrict__ x, int64_t di, int64_t total,
                                                uint32_t (&d)[NV]) {
     const int64_t b0 = di * 4;
@@ -30,7 +30,8 @@ __device__ __forceinline__ void load_u8_dwords(const uint8_t* __restrict__ x, in
         if constexpr (NV == 1) {
             d[0] = *reinterpret_cast<const uint32_t*>(x + b0);
         } else {
-            const vN q = *reinterpret_cast<const vN*>(x + b0);
+            const vN* p = reinterpret_cast<const vN*>(x + b0);
+            const vN q = NT ? __builtin_nontemporal_load(p) : *p;
 #pragma unroll
             for (int i = 0; i < NV; ++i) d[i] = q[i];
         }
@@ -59,7 +60,7 @@ __device__ __forceinline__ void ideal_outputs(const double (&s)[NS], const TapsI
 
 // COAL: a full wave stages its outputs in LDS and writes them back as whole contiguous
 // 1 KiB rows per store instruction (instead of 16 B per lane at a 16*NV-byte stride).
-template <int L, int NV, bool COAL = false>
+template <int L, int NV, bool COAL = false, bool NTL = false>
 __global__ __launch_bounds__(kBlock) void fir1d_ideal_reg_kernel(const uint8_t* __restrict__ x,
                                                                  double* __restrict__ y, int64_t total,
                                                                  uint32_t rowlen32, int multi_row, int aligned,
@@ -72,7 +73,7 @@ __global__ __launch_bounds__(kBlock) void fir1d_ideal_reg_kernel(const uint8_t* 
     const int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // this lane's vector
     const int64_t wave_v0 = v - lane;
     uint32_t own[NV];
-    load_u8_dwords<NV>(x, v * NV, total, own);
+    load_u8_dwords<NV, NTL>(x, v * NV, total, own);
     uint32_t seam = 0;
     if (lane == 0) {
         load_u8_dwords<1>(x, wave_v0 * NV - 1, total, *reinterpret_cast<uint32_t(*)[1]>(&seam));
