@@ -220,16 +220,12 @@ int main(int argc, char** argv) {
     CK(hipStreamCreate(&st));
 
     std::vector<Variant> vs = {
-        {"fir U1 mad (r01f)", true, launch_fir_old<1, 0>, 0, {}},
-        {"fir U1 mad", true, launch_fir<1, 0>, 0, {}},
-        {"fir U1 mad acc32", true, launch_fir<1, kAcc32>, 0, {}},
-        {"fir U1 dot2 acc32", true, launch_fir<1, kDot2 | kAcc32>, 0, {}},
         {"fir U1 dot2 acc32 coal", true, launch_fir<1, kDot2 | kAcc32 | kCoal>, 0, {}},
-        {"fir U1 dot2 acc32 coal xcd", true, launch_fir<1, kDot2 | kAcc32 | kCoal | kXcd>, 0, {}},
+        {"fir U1 coal ntld", true, launch_fir<1, kDot2 | kAcc32 | kCoal | kNtLoad>, 0, {}},
+        {"fir U2 coal ntld", true, launch_fir<2, kDot2 | kAcc32 | kCoal | kNtLoad>, 0, {}},
+        {"fir U4 coal ntld", true, launch_fir<4, kDot2 | kAcc32 | kCoal | kNtLoad>, 0, {}},
         {"fir U2 dot2 acc32 coal", true, launch_fir<2, kDot2 | kAcc32 | kCoal>, 0, {}},
-        {"fir U1 dot2", true, launch_fir<1, kDot2>, 0, {}},
-        {"fir U2 dot2 acc32", true, launch_fir<2, kDot2 | kAcc32>, 0, {}},
-        {"fir U1 dot2 acc32 nt-ld", true, launch_fir<1, kDot2 | kAcc32 | kNtLoad>, 0, {}},
+        {"fir U4 dot2 acc32 coal", true, launch_fir<4, kDot2 | kAcc32 | kCoal>, 0, {}},
         {"copy U1 plain", false, launch_copy<1, 0>, 0, {}},
         {"copy U1 coal (LDS)", false, launch_copy_coal, 0, {}},
         {"copy split U1", false, launch_copy_split<1>, 0, {}},
