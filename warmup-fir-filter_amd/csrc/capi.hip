@@ -65,6 +65,18 @@ int ensure(DeviceBuf& b, size_t bytes) {
     return FIR_OK;
 }
 
+// Puts the calling thread's current device back on scope exit: a host entry that runs on
+// `device` must not move the caller's (e.g. PyTorch's) current device.
+struct DeviceRestore {
+    int prev = -1;
+    DeviceRestore() {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    }
+    ~DeviceRestore() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
 // Validates `device`, makes it current, and returns its state (locked by the caller).
 int device_state(int device, DeviceState** out) {
     int n = 0;
@@ -106,6 +118,7 @@ size_t out_size(int stage) { return stage == FIR_OUT_I32 ? 4 : 1; }
 template <typename F>
 int run_host(int device, const void* x, size_t in_bytes, void* y, size_t out_bytes, F launch, size_t out_skip = 0,
              size_t in_cap = 0, size_t out_cap = 0) {
+    DeviceRestore restore;
     DeviceState* st = nullptr;
     int rc = device_state(device, &st);
     if (rc) return rc;
@@ -409,6 +422,7 @@ int64_t fir_metrics_work_bytes(void) { return (int64_t)fir::metrics_work_bytes()
 int fir_compare_metrics(const double* ideal, const uint8_t* fixed, int64_t n, double* out, int device) {
     try {
         if (n < 0 || !out || (n > 0 && (!ideal || !fixed))) return fail(FIR_EINVAL, "invalid arguments");
+        DeviceRestore restore;
         DeviceState* st = nullptr;
         int rc = device_state(device, &st);
         if (rc) return rc;
@@ -509,6 +523,7 @@ int fir_ipc_import(const void* handle, int64_t offset, int device, void** dev_pt
     try {
         if (!handle || !dev_ptr_out || offset < 0) return fail(FIR_EINVAL, "invalid argument");
         *dev_ptr_out = nullptr;
+        DeviceRestore restore;
         hipError_t e = hipSetDevice(device);
         if (e != hipSuccess) return fail(FIR_ENODEV, std::string("hipSetDevice: ") + hipGetErrorString(e));
         hipIpcMemHandle_t h;
