@@ -221,6 +221,9 @@ int main(int argc, char** argv) {
 
     std::vector<Variant> vs = {
         {"fir U1 dot2 acc32 coal", true, launch_fir<1, kDot2 | kAcc32 | kCoal>, 0, {}},
+        {"fir U1 coal ntst", true, launch_fir<1, kDot2 | kAcc32 | kCoal | kNtStore>, 0, {}},
+        {"fir U2 coal ntst", true, launch_fir<2, kDot2 | kAcc32 | kCoal | kNtStore>, 0, {}},
+        {"fir U1 coal ntld+st", true, launch_fir<1, kDot2 | kAcc32 | kCoal | kNtLoad | kNtStore>, 0, {}},
         {"fir U1 coal ntld", true, launch_fir<1, kDot2 | kAcc32 | kCoal | kNtLoad>, 0, {}},
         {"fir U2 coal ntld", true, launch_fir<2, kDot2 | kAcc32 | kCoal | kNtLoad>, 0, {}},
         {"fir U4 coal ntld", true, launch_fir<4, kDot2 | kAcc32 | kCoal | kNtLoad>, 0, {}},

@@ -131,7 +131,10 @@ int main(int argc, char** argv) {
                          {"fir U2 ntld", 1, launch_fir<2, kU8Dot2 | kNtLoad>, {}},
                          {"fir U4 xcd", 1, launch_fir<4, kU8Dot2 | kXcd>, {}},
                          {"fir U8", 1, launch_fir<8, kU8Dot2>, {}},
-                         {"fir U1 ntld", 1, launch_fir<1, kU8Dot2 | kNtLoad>, {}},
+                         {"fir U4 ntld+st", 1, launch_fir<4, kU8Dot2 | kNtLoad | kNtStore>, {}},
+                         {"fir U4 ntst", 1, launch_fir<4, kU8Dot2 | kNtStore>, {}},
+                         {"bank pk16 U2 ntst", 2, launch_bank<2, PK | kNtStore>, {}},
+                         {"bank pk16 U1 ntst", 2, launch_bank<1, PK | kNtStore>, {}},
                          {"bank pk16 U2 ntld", 2, launch_bank<2, PK | kNtLoad>, {}},
                          {"bank pk16 U4 ntld", 2, launch_bank<4, PK | kNtLoad>, {}},
                          {"bank pk16 U1 ntld", 2, launch_bank<1, PK | kNtLoad>, {}},

@@ -27,12 +27,12 @@ using namespace fir;
 static const double kH[5] = {-1.0 / 16, -4.0 / 16, 26.0 / 16, -4.0 / 16, -1.0 / 16};
 static const int64_t kW = 4096;
 
-template <int NV, bool COAL, bool NTL = false>
+template <int NV, bool COAL, bool NTL = false, bool NTS = false>
 static void launch(const uint8_t* x, double* y, int64_t total, hipStream_t s) {
     TapsIdeal<5> t;
     for (int k = 0; k < 5; ++k) t.h[k] = kH[k];
     const int64_t vecs = (total + 4 * NV - 1) / (4 * NV);
-    hipLaunchKernelGGL((fir1d_ideal_reg_kernel<5, NV, COAL, NTL>), dim3((unsigned)((vecs + kBlock - 1) / kBlock)),
+    hipLaunchKernelGGL((fir1d_ideal_reg_kernel<5, NV, COAL, NTL, NTS>), dim3((unsigned)((vecs + kBlock - 1) / kBlock)),
                        dim3(kBlock), 0, s, x, y, total, (uint32_t)kW, 1, 1, t);
 }
 
@@ -93,8 +93,9 @@ int main(int argc, char** argv) {
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     std::vector<V> vs = {{"NV1", launch<1, false>, {}}, {"NV1 coal", launch<1, true>, {}},
                          {"NV2 coal", launch<2, true>, {}}, {"NV4 coal", launch<4, true>, {}},
-                         {"NV2 strided", launch<2, false>, {}}, {"NV4 strided", launch<4, false>, {}},
-                         {"NV4 strided ntld", launch<4, false, true>, {}},
+                         {"NV2 coal ntst", launch<2, true, false, true>, {}},
+                         {"NV4 coal ntst", launch<4, true, false, true>, {}},
+                         {"NV2 coal ntld+st", launch<2, true, true, true>, {}},
                          {"store-only strided", launch_store<false>, {}},
                          {"store-only coal", launch_store<true>, {}}};
     const size_t nchecked = 4;

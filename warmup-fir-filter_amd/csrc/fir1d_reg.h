@@ -573,7 +573,12 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
                             asm volatile("" ::: "memory");
                             u32x4* yw = reinterpret_cast<u32x4*>(y + f * total + (vb + u * kWave) * VEC);
 #pragma unroll
-                            for (int i = 0; i < VEC / 4; ++i) yw[i * kWave + lane] = wb[i * kWave + lane];
+                            for (int i = 0; i < VEC / 4; ++i) {
+                                if constexpr (NTS)
+                                    __builtin_nontemporal_store(wb[i * kWave + lane], &yw[i * kWave + lane]);
+                                else
+                                    yw[i * kWave + lane] = wb[i * kWave + lane];
+                            }
                             asm volatile("" ::: "memory");
                             continue;
                         }

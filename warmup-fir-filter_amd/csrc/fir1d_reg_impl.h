@@ -12,22 +12,17 @@
 namespace fir {
 
 // Hot-kernel shape chosen by the A/B microbenchmark (tools/microbench; profiles/r01/micro_*.txt;
-// the chunk counts kRegU live in fir1d_reg_launch.h):
-// one 64-vector chunk per wave, default-policy loads and stores (non-temporal stores cost
-// 25-45 % on this 1:2 read:write stream; more chunks per wave or a persistent grid 3-15 %),
-// int32 outputs staged through LDS into whole 1 KiB store instructions (272 -> 257 us).
-// One u8 filter: 4 chunks per wave (the per-wave edge loads and row arithmetic amortised
-// over 4 KiB; 104.6 -> 94.0 us at 2^28, profiles/r01/micro_u8_chunks.txt); a fused bank
-// (F > 1) runs best at 2 chunks with its packed-16 filters (4-filter 3-tap bank: 259 us at 1
-// chunk on v_dot2, 229 us at 2 chunks with packed-16; profiles/r01/micro_u8_pk16.txt).
-constexpr int kRegFlags = kCoal;
+// the chunk counts kRegU live in fir1d_reg_launch.h): one 64-vector chunk per wave
+// (more chunks per wave or a persistent grid cost 3-15 %), int32 outputs staged through LDS
+// into whole 1 KiB store instructions (272 -> 257 us), and those whole-row stores
+// NON-TEMPORAL (257.9 -> 250.9 us, 80 % of HBM peak, micro_i16_nts.txt; non-temporal stores
+// of the lane-strided layout had cost 25-45 %, non-temporal loads cost 4 %).
+// One u8 filter: 4 chunks per wave (the per-wave edge loads and row arithmetic amortised over
+// 4 KiB; 104.6 -> 94.0 us at 2^28, micro_u8_chunks.txt), non-temporal stores 94.7 -> 82.2 us
+// (micro_u8_nts.txt).  A fused u8 bank: 1 chunk per wave with non-temporal stores (222.6 us vs
+// 229.3 at 2 chunks with plain stores).
+constexpr int kRegFlags = kCoal | kNtStore;
 constexpr int kPersistBlocks = 2048;
-
-// One u8 filter streams its input with non-temporal loads (4 chunks per wave: 95.5 -> 88.8 us
-// at 2^28, profiles/r01/micro_u8_nt.txt); the fused bank, the int16 path, the ideal and the
-// 2-D kernels measured slower or equal with them (241 vs 234, 283 vs 272, 393 vs 394, 26.0 vs 23.8 us).
-template <int F>
-constexpr int kU8NtLoad = F == 1 ? kNtLoad : 0;
 
 template <typename InT, int STAGE, int L, int CH, int F, int FL>
 static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
@@ -89,8 +84,8 @@ static hipError_t launch_reg(const void* x, void* y, int64_t rows, int64_t total
                                                                                           frac, acc_bits, stream, hl, hr);
         }
         if (taps16 && nowrap)
-            return launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kU8Dot2 | kU8NtLoad<F>>(x, y, rows, total, rowlen, hq, frac,
-                                                                                           acc_bits, stream, hl, hr);
+            return launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kU8Dot2>(x, y, rows, total, rowlen, hq, frac, acc_bits,
+                                                                               stream, hl, hr);
     }
     if constexpr (sizeof(InT) == 2 && CH == 1) {
         if (taps16)

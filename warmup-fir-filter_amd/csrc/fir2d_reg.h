@@ -345,7 +345,7 @@ __global__ __launch_bounds__(kBlock, MINW) void fir2d_reg_kernel(const uint8_t* 
                                 val[i] = o4;
                             }
                         }
-                        *reinterpret_cast<vN*>(dst) = val;
+                        *reinterpret_cast<vN*>(dst) = val;  // non-temporal: 24.6 vs 24.05 us, within noise
                     } else {
                         typedef uint32_t v4 __attribute__((ext_vector_type(4)));
 #pragma unroll

@@ -60,7 +60,7 @@ __device__ __forceinline__ void ideal_outputs(const double (&s)[NS], const TapsI
 
 // COAL: a full wave stages its outputs in LDS and writes them back as whole contiguous
 // 1 KiB rows per store instruction (instead of 16 B per lane at a 16*NV-byte stride).
-template <int L, int NV, bool COAL = false, bool NTL = false>
+template <int L, int NV, bool COAL = false, bool NTL = false, bool NTS = false>
 __global__ __launch_bounds__(kBlock) void fir1d_ideal_reg_kernel(const uint8_t* __restrict__ x,
                                                                  double* __restrict__ y, int64_t total,
                                                                  uint32_t rowlen32, int multi_row, int aligned,
@@ -132,7 +132,12 @@ __global__ __launch_bounds__(kBlock) void fir1d_ideal_reg_kernel(const uint8_t* 
             asm volatile("" ::: "memory");
             d2* yw = reinterpret_cast<d2*>(y + wave_v0 * VEC);
 #pragma unroll
-            for (int i = 0; i < VEC / 2; ++i) yw[i * kWave + lane] = wb[i * kWave + lane];
+            for (int i = 0; i < VEC / 2; ++i) {
+                if constexpr (NTS)
+                    __builtin_nontemporal_store(wb[i * kWave + lane], &yw[i * kWave + lane]);
+                else
+                    yw[i * kWave + lane] = wb[i * kWave + lane];
+            }
             return;
         }
     }

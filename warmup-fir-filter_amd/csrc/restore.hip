@@ -70,7 +70,7 @@ __global__ __launch_bounds__(kBlock) void restore_map_kernel(const double* __res
         __builtin_amdgcn_wave_barrier();  // one wave's LDS ops complete in order
         asm volatile("" ::: "memory");
 #pragma unroll
-        for (int i = 0; i < K / 8; ++i)
+        for (int i = 0; i < K / 8; ++i)  // plain stores: non-temporal ones measured 394 -> 415 us
             reinterpret_cast<u32x4*>(out + base)[i * kWave + lane] = reinterpret_cast<const u32x4*>(wb)[i * kWave + lane];
     } else {
         for (int64_t e = base + lane; e < n; e += kWave) out[e] = (uint8_t)conv(a[e], NORM, p);
