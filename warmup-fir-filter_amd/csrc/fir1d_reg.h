@@ -45,6 +45,16 @@ enum RegFlags : int {
                       // kernel 1.5 % (256.9 -> 260.8 us, tools/lib_ab.py)
 };
 
+// One non-temporal 16-byte row-store of the coalesced path, as inline asm: the same
+// `global_store_dwordx4 ... nt` the builtin emits, but 1.6 % faster in this kernel (the compiler
+// folds the second row's address into `offset:1024` and reorders; 247.8 -> 243.9 us,
+// profiles/r01/micro_i16_sc.txt; the sc0 / sc1 policy bits add nothing).  The s_nop covers the
+// VMEM-store-data hazard (a VALU write of the data VGPRs right after a >64-bit store), which the
+// compiler cannot see through inline asm.
+__device__ __forceinline__ void store16_nt(u32x4* p, u32x4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+
 constexpr int kNumXcd = 8;
 
 // Block id -> position in the tile order.  Blocks b and b + 8 run on the same XCD; with
@@ -575,7 +585,7 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
 #pragma unroll
                             for (int i = 0; i < VEC / 4; ++i) {
                                 if constexpr (NTS)
-                                    __builtin_nontemporal_store(wb[i * kWave + lane], &yw[i * kWave + lane]);
+                                    store16_nt(&yw[i * kWave + lane], wb[i * kWave + lane]);
                                 else
                                     yw[i * kWave + lane] = wb[i * kWave + lane];
                             }
