@@ -216,7 +216,10 @@ __device__ __forceinline__ void store_vec(typename OutTraits<STAGE>::T* __restri
             if constexpr (VEC == 16) {
                 const u32x4 val = {o[0], o[1], o[2], o[3]};
                 u32x4* p = reinterpret_cast<u32x4*>(y + g0);
-                if (NT) __builtin_nontemporal_store(val, p); else *p = val;
+                if constexpr (NT)
+                    store16_nt(p, val);  // u8 path: 79.2 -> 78.0 us vs the builtin (micro_u8_asm.txt)
+                else
+                    *p = val;
             } else {
                 const u32x2 val = {o[0], o[1]};
                 u32x2* p = reinterpret_cast<u32x2*>(y + g0);
@@ -247,7 +250,10 @@ __device__ __forceinline__ void store_u8_dwords(uint8_t* __restrict__ y, int64_t
         if constexpr (VEC == 16) {
             const u32x4 val = {o[0], o[1], o[2], o[3]};
             u32x4* p = reinterpret_cast<u32x4*>(y + g0);
-            if (NT) __builtin_nontemporal_store(val, p); else *p = val;
+            if constexpr (NT)
+                store16_nt(p, val);
+            else
+                *p = val;
         } else {
             const u32x2 val = {o[0], o[1]};
             u32x2* p = reinterpret_cast<u32x2*>(y + g0);
