@@ -94,6 +94,43 @@ def test_fir2d_separable_variants_vs_oracle(k, shape):
                                   co.fir2d(x, hq, frac, acc, stage)), (frac, acc, stage)
 
 
+GEN_PK_KERNELS = [  # non-separable kernels reaching the general packed-16 forms at frac 12
+    [[16, 32, 16], [32, 48, 32], [16, 32, 16]],                       # unsigned, f - s = 8: high byte
+    [[1, 2, 3], [4, 5, 6], [7, 8, 10]],                               # unsigned, shift 12
+    [[-1, 3, -1], [3, -8, 3], [-1, 3, -1]],                           # signed sum
+    [[0, -512, 0], [-512, 3072, -512], [0, -512, 0]],                 # Laplacian sharpen, s = 9
+    [[1, -2, 5, -2, 1]],                                              # 1 x 5 (never rank-1 split)
+    [[2], [-1], [7], [-1], [2]],                                      # 5 x 1
+    np.random.default_rng(55).integers(-4, 5, (5, 5)).tolist(),       # general 5x5, signed
+    np.random.default_rng(56).integers(0, 5, (3, 5)).tolist(),        # 3x5, unsigned
+]
+# At frac 8 the same kernels take the clamped shift (s <= f - 1); at frac 16 most exceed
+# 16-bit shifts (f - s > 15) or the range and fall back to v_dot2; acc 24 keeps the no-wrap proof.
+
+
+@pytest.mark.parametrize("k", range(len(GEN_PK_KERNELS)))
+@pytest.mark.parametrize("shape", [(1, 16), (29, 64), (64, 1280), (300, 4096 + 16)])
+def test_fir2d_general_packed16_vs_oracle(k, shape):
+    hq = np.array(GEN_PK_KERNELS[k], np.int64)
+    rng = np.random.default_rng(k * 11 + shape[0])
+    x = rng.integers(0, 256, shape, dtype=np.uint8)
+    x[0, : min(16, shape[1])] = 255  # saturating corners
+    co = c_oracle()
+    for frac, acc in ((12, 32), (8, 24), (16, 32), (10, 32)):
+        for stage in (fir_hip.OUT_U8_SAT, fir_hip.OUT_I32):
+            assert np.array_equal(fir_hip.fir2d_fixed(x, hq, frac, acc, stage),
+                                  co.fir2d(x, hq, frac, acc, stage)), (frac, acc, stage)
+
+
+def test_fir2d_full_frame_8192_general():
+    """configs[4] frame with a non-separable 5x5 kernel (general packed-16 form)."""
+    x = np.random.default_rng(20260228).integers(0, 256, (8192, 8192), dtype=np.uint8)
+    hq = np.array(GEN_PK_KERNELS[6], np.int64)
+    y = torch_ops.fir2d_fixed_dev(torch.from_numpy(x).to(DEV), hq)
+    torch.cuda.synchronize()
+    assert np.array_equal(y.cpu().numpy(), c_oracle().fir2d(x, hq))
+
+
 def test_fir2d_full_frame_8192():
     """BASELINE configs[4]: 8192 x 8192 u8 frame, 5x5 unity-gain kernel."""
     x = np.random.default_rng(20260227).integers(0, 256, (8192, 8192), dtype=np.uint8)

@@ -1,0 +1,61 @@
+"""Dev A/B for the 2-D kernel: fir2d_fixed_dev on an 8192 x 8192 u8 frame from two builds of
+libfir_hip.so in one process, interleaved batches of back-to-back launches timed by HIP events.
+Usage: python tools/lib_ab2d.py <lib A> <lib B> [<lib C> ...]   (AB_ROUNDS=10)
+Kernels: the bench's separable low-pass, a non-separable 5x5 and a 3x3 sharpen."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+KERNELS = {
+    "sep5x5_lp": np.outer([256, 1024, 1536, 1024, 256], [256, 1024, 1536, 1024, 256]) // 4096,
+    "gen5x5": np.random.default_rng(55).integers(-4, 5, (5, 5)),
+    "sharpen3x3": np.array([[0, -512, 0], [-512, 3072, -512], [0, -512, 0]]),
+}
+
+
+def main():
+    paths = sys.argv[1:]
+    libs = [ctypes.CDLL(p) for p in paths]
+    rounds = int(os.environ.get("AB_ROUNDS", "10"))
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(s)
+    H = W = 8192
+    x = torch.from_numpy(np.random.default_rng(1).integers(0, 256, (H, W), dtype=np.uint8)).to(dev)
+    vp = ctypes.c_void_p
+    for lib in libs:
+        lib.fir2d_fixed_dev.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, vp, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp]
+    for kname, k in KERNELS.items():
+        R, C = k.shape
+        h = (ctypes.c_int32 * (R * C))(*[int(v) for v in k.reshape(-1)])
+        ys = [torch.empty_like(x) for _ in libs]
+
+        def run(i, n):
+            for _ in range(n):
+                rc = libs[i].fir2d_fixed_dev(vp(x.data_ptr()), H, W, h, R, C, 12, 32, 0, vp(ys[i].data_ptr()),
+                                             vp(s.cuda_stream))
+                assert rc == 0
+        for i in range(len(libs)):
+            run(i, 50)
+        torch.cuda.synchronize()
+        assert all(torch.equal(ys[0], y) for y in ys[1:]), kname
+        t = [[] for _ in libs]
+        for _ in range(rounds):
+            for i in range(len(libs)):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                run(i, 100)
+                b.record()
+                b.synchronize()
+                t[i].append(a.elapsed_time(b) / 100 * 1e3)
+        for i, p in enumerate(paths):
+            v = sorted(t[i])
+            print(f"{kname:12s} {p}: median {v[len(v) // 2]:.1f} us  min {v[0]:.1f} us", flush=True)
+
+
+if __name__ == "__main__":
+    main()

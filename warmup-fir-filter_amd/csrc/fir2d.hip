@@ -30,6 +30,16 @@ constexpr int kPdGen = 2;
 // memory-only twin of the same loop takes 21.1 us, profiles/r01/micro2d_copy.txt)
 constexpr int kStrip2dPk = 32;
 constexpr int kPdPk = 4;
+// general packed-16 form: 16-row strips (a 32-row strip's R*C MACs per row exceed the forced
+// unroll budget: the loop stays rolled and its ring spills to scratch)
+#ifndef FIR2D_PKG_VEC  // overridable for the A/B builds (tools/lib_ab2d.py)
+#define FIR2D_PKG_VEC 16
+#define FIR2D_PKG_STRIP 16
+#define FIR2D_PKG_PD 3
+#endif
+constexpr int kVec2dPkGen = FIR2D_PKG_VEC;
+constexpr int kStrip2dPkGen = FIR2D_PKG_STRIP;
+constexpr int kPdPkGen = FIR2D_PKG_PD;
 
 // Generic: one output per thread, exact int64 sum, global loads (L1/L2 absorb the reuse).
 struct Taps2G {
@@ -168,6 +178,27 @@ static hipError_t launch2d_reg(const uint8_t* x, void* y, int64_t H, int64_t W, 
             hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, kMode2dSep, 1, kPdSep>), grid, dim3(kBlock), 0, s,
                                x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
     } else {
+        // packed 16-bit pixel pairs when the whole sum provably fits 16 bits (u8 stage only)
+        if constexpr (STAGE == FIR_OUT_U8_SAT) {
+            constexpr int GNW = kMode2dDot2 | kMode2dNoWrap | kMode2dPk16, ST = kStrip2dPkGen, PD = kPdPkGen;
+            const int pk = nowrap ? plan_pk16_gen(t, hq, frac) : 0;
+            const dim3 gpk = fir2d_reg_grid<kVec2dPkGen, ST>(H, W);
+            if (pk == (kMode2dPk16 | kMode2dPkHi8)) {
+                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dPkGen, ST, GNW | kMode2dPkHi8, 1, PD>), gpk,
+                                   dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
+                return hipGetLastError();
+            }
+            if (pk == kMode2dPk16) {
+                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dPkGen, ST, GNW, 1, PD>), gpk, dim3(kBlock), 0, s, x,
+                                   (OutT*)y, H, W, t, 32 - acc_bits, frac);
+                return hipGetLastError();
+            }
+            if (pk == (kMode2dPk16 | kMode2dPkSigned)) {
+                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dPkGen, ST, GNW | kMode2dPkSigned, 1, PD>), gpk,
+                                   dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
+                return hipGetLastError();
+            }
+        }
         const dim3 grid = fir2d_reg_grid<kVec2dGen, kStrip2dGen>(H, W);
         if (nowrap)
             hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dGen, kStrip2dGen, kMode2dDot2 | kMode2dNoWrap, 4, kPdGen>),

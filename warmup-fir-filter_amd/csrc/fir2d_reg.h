@@ -32,6 +32,9 @@ struct Taps2 {
     uint32_t rowb[C];
     uint32_t colb[R];
     uint32_t pkbias, pkshift, pkmax;
+    // PK16 general form (any kernel, kMode2dDot2 | kMode2dPk16): pkh[m][i] = hq[m][C-1-i] / 2^s
+    // replicated into both halves (multiplies window pixel j+i of output j)
+    uint32_t pkh[R][C];
 };
 
 // 2-D kernel arithmetic: general 5x5 on v_mad_i32_i24 / packed v_dot2, or rank-1 separable
@@ -48,6 +51,8 @@ struct Taps2 {
 // pixel PAIRS, exact mod 2^16 (so intermediate row sums may wrap), and the u8 stage is
 // (V >> (f-s)) clamped to [0, 255] = sat((2^s V_true + 2^(f-1)) >> f), the reference's value.
 // kMode2dPkHi8: unsigned with f-s == 8, the output byte is V's high byte (one v_perm per 4 px).
+// kMode2dPk16 with kMode2dDot2 (any kernel, not only rank-1): the same 16-bit argument over the
+// full R x C taps, R*C v_pk_mad_u16 per pixel PAIR (12.5 per pixel for 5x5 instead of 15 v_dot2).
 enum Fir2dMode : int {
     kMode2dMad = 0,
     kMode2dDot2 = 1,
@@ -106,6 +111,42 @@ inline int plan_pk16(Taps2<R, C>& t, const int32_t* col, const int32_t* row, int
     auto rep = [](int64_t v) { return ((uint32_t)v & 0xFFFFu) * 0x10001u; };
     for (int i = 0; i < C; ++i) t.rowb[i] = rep(rq[C - 1 - i]);
     for (int m = 0; m < R; ++m) t.colb[m] = rep(cq[m]);
+    t.pkbias = rep((int64_t)1 << (frac - 1 - s));
+    t.pkshift = rep(frac - s);
+    t.pkmax = rep(255);
+    return mode;
+}
+
+// PK16 planning for a general (not necessarily rank-1) kernel: the same power-of-two
+// factoring and 16-bit range proof over all R*C taps.  Returns the extra mode bits or 0.
+template <int R, int C>
+inline int plan_pk16_gen(Taps2<R, C>& t, const int32_t* hq, int frac) {
+    if (frac < 1 || frac > 22) return 0;
+    int z = 40;
+    for (int k = 0; k < R * C; ++k) {
+        int64_t v = hq[k];
+        int zk = 0;
+        while (v != 0 && (v & 1) == 0 && zk < 40) v >>= 1, ++zk;
+        if (v != 0 && zk < z) z = zk;
+    }
+    if (z >= 40) return 0;  // all-zero kernel: the other paths handle it
+    const int s = z < frac - 1 ? z : frac - 1;
+    if (frac - s > 15) return 0;  // 16-bit shifts take the amount mod 16
+    int64_t vmax = (int64_t)1 << (frac - 1 - s), vmin = vmax;
+    for (int k = 0; k < R * C; ++k) {
+        const int64_t p = (int64_t)hq[k] >> s;
+        (p > 0 ? vmax : vmin) += 255 * p;
+    }
+    int mode;
+    if (vmin >= 0 && vmax <= 65535)
+        mode = kMode2dPk16 | (frac - s == 8 ? kMode2dPkHi8 : 0);
+    else if (vmin >= -32768 && vmax <= 32767)
+        mode = kMode2dPk16 | kMode2dPkSigned;
+    else
+        return 0;
+    auto rep = [](int64_t v) { return ((uint32_t)v & 0xFFFFu) * 0x10001u; };
+    for (int m = 0; m < R; ++m)
+        for (int i = 0; i < C; ++i) t.pkh[m][i] = rep((int64_t)hq[m * C + C - 1 - i] >> s);
     t.pkbias = rep((int64_t)1 << (frac - 1 - s));
     t.pkshift = rep(frac - s);
     t.pkmax = rep(255);
@@ -182,8 +223,10 @@ __global__ __launch_bounds__(kBlock, MINW) void fir2d_reg_kernel(const uint8_t* 
         for (int j = 0; j < VEC; ++j) acc[s][j] = acc0;
     uint32_t qr[R][VEC] = {}, rsprev[VEC] = {};  // SEP16: packed (rs_t, rs_t-1) ring and rs_t-1
     constexpr bool PK16 = (MODE & 3) == kMode2dSep && (MODE & kMode2dPk16);
-    static_assert(!PK16 || STAGE == FIR_OUT_U8_SAT, "PK16 is a u8-stage form");
+    constexpr bool PKG = (MODE & 3) == kMode2dDot2 && (MODE & kMode2dPk16);  // general packed-16
+    static_assert(!(PK16 || PKG) || STAGE == FIR_OUT_U8_SAT, "PK16 is a u8-stage form");
     uint32_t rs2[R][VEC / 2] = {}, pko[VEC / 2] = {};  // PK16: row-sum pair ring, output pairs
+    uint32_t ag[R][VEC / 2] = {};                      // PKG: output-pair ring
 
     auto row_ptr = [&](int64_t row) { return x + (row < 0 ? 0 : (row >= H ? H - 1 : row)) * W; };
     // input rows of the strip: row t is loaded PD steps before it is consumed (the unrolled
@@ -219,7 +262,22 @@ __global__ __launch_bounds__(kBlock, MINW) void fir2d_reg_kernel(const uint8_t* 
                 uint32_t Pr[NP + 4 - HLE];
                 PairBuilder<4 - HLE, NP>::run(sb, Pr);
                 const uint32_t* P = Pr + (4 - HLE);
-                if constexpr ((MODE & 3) == kMode2dDot2) {
+                if constexpr (PKG) {  // input row t feeds R output rows, C pair MACs each
+#pragma unroll
+                    for (int m = 0; m < R; ++m) {
+                        const int slot = (s + 1 + m) % R;
+#pragma unroll
+                        for (int q = 0; q < VEC / 2; ++q)  // m = R-1 opens the row from the bias
+                            ag[slot][q] = pk_mad16(P[2 * q], taps.pkh[m][0], m == R - 1 ? taps.pkbias : ag[slot][q]);
+#pragma unroll
+                        for (int i = 1; i < C; ++i)
+#pragma unroll
+                            for (int q = 0; q < VEC / 2; ++q) ag[slot][q] = pk_mad16(P[2 * q + i], taps.pkh[m][i], ag[slot][q]);
+                    }
+                    // the completed row (m = 0) stays here, interleaved (see the PK16 pin below)
+#pragma unroll
+                    for (int q = 0; q < VEC / 2; ++q) asm volatile("" : "+v"(ag[(s + 1) % R][q]));
+                } else if constexpr ((MODE & 3) == kMode2dDot2) {
 #pragma unroll
                     for (int m = 0; m < R; ++m) {
                         const int slot = (s + 1 + m) % R;
@@ -322,15 +380,19 @@ __global__ __launch_bounds__(kBlock, MINW) void fir2d_reg_kernel(const uint8_t* 
                     if constexpr (STAGE == FIR_OUT_U8_SAT) {
                         typedef uint32_t vN __attribute__((ext_vector_type(ND)));
                         vN val;
+                        auto po = [&](int k) -> uint32_t {
+                            if constexpr (PKG) return ag[slot][k];
+                            else return pko[k];
+                        };
 #pragma unroll
                         for (int i = 0; i < ND; ++i) {
-                            if constexpr (PK16) {  // pairs (4i, 4i+1), (4i+2, 4i+3) -> 4 bytes
+                            if constexpr (PK16 || PKG) {  // pairs (4i, 4i+1), (4i+2, 4i+3) -> 4 bytes
                                 if constexpr ((MODE & kMode2dPkHi8) != 0) {
-                                    val[i] = __builtin_amdgcn_perm(pko[2 * i + 1], pko[2 * i], 0x07050301u);
+                                    val[i] = __builtin_amdgcn_perm(po(2 * i + 1), po(2 * i), 0x07050301u);
                                 } else {
                                     constexpr bool SG = (MODE & kMode2dPkSigned) != 0;
-                                    const uint32_t lo = pk_stage_u8<SG>(pko[2 * i], taps.pkshift, taps.pkmax);
-                                    const uint32_t hi = pk_stage_u8<SG>(pko[2 * i + 1], taps.pkshift, taps.pkmax);
+                                    const uint32_t lo = pk_stage_u8<SG>(po(2 * i), taps.pkshift, taps.pkmax);
+                                    const uint32_t hi = pk_stage_u8<SG>(po(2 * i + 1), taps.pkshift, taps.pkmax);
                                     val[i] = __builtin_amdgcn_perm(hi, lo, 0x06040200u);
                                 }
                             } else if constexpr (NOWRAP) {
