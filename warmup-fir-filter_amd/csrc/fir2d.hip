@@ -35,11 +35,15 @@ constexpr int kPdPk = 4;
 #ifndef FIR2D_PKG_VEC  // overridable for the A/B builds (tools/lib_ab2d.py)
 #define FIR2D_PKG_VEC 16
 #define FIR2D_PKG_STRIP 16
-#define FIR2D_PKG_PD 3
+#define FIR2D_PKG_PD 0
 #endif
 constexpr int kVec2dPkGen = FIR2D_PKG_VEC;
 constexpr int kStrip2dPkGen = FIR2D_PKG_STRIP;
-constexpr int kPdPkGen = FIR2D_PKG_PD;
+// prefetch depth (0 = by tap count): rows 2 ahead for 5x5-size kernels (0.5-3 % faster than
+// depth 3 over two A/B runs), 3 ahead for smaller ones (3x3: 21.9 vs 22.3 us at depth 2;
+// profiles/r01/ab2d_pk16_general.txt)
+template <int R, int C>
+constexpr int pd_pk_gen() { return FIR2D_PKG_PD ? FIR2D_PKG_PD : (R * C >= 20 ? 2 : 3); }
 
 // Generic: one output per thread, exact int64 sum, global loads (L1/L2 absorb the reuse).
 struct Taps2G {
@@ -180,7 +184,7 @@ static hipError_t launch2d_reg(const uint8_t* x, void* y, int64_t H, int64_t W, 
     } else {
         // packed 16-bit pixel pairs when the whole sum provably fits 16 bits (u8 stage only)
         if constexpr (STAGE == FIR_OUT_U8_SAT) {
-            constexpr int GNW = kMode2dDot2 | kMode2dNoWrap | kMode2dPk16, ST = kStrip2dPkGen, PD = kPdPkGen;
+            constexpr int GNW = kMode2dDot2 | kMode2dNoWrap | kMode2dPk16, ST = kStrip2dPkGen, PD = pd_pk_gen<R, C>();
             const int pk = nowrap ? plan_pk16_gen(t, hq, frac) : 0;
             const dim3 gpk = fir2d_reg_grid<kVec2dPkGen, ST>(H, W);
             if (pk == (kMode2dPk16 | kMode2dPkHi8)) {
