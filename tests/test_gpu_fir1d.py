@@ -10,6 +10,7 @@ full 2^28-sample benchmark size.
 """
 from __future__ import annotations
 
+import ctypes
 import hashlib
 from pathlib import Path
 
@@ -280,6 +281,24 @@ def test_full_size_complex_2_27():
     y = torch_ops.fir1d_fixed_rows_dev(torch.from_numpy(x).to(DEV), TAPS["lp3"], 12, 32, fir_hip.OUT_I32, 2)
     torch.cuda.synchronize()
     assert np.array_equal(y.cpu().numpy(), _co().fir1d_rows(x, TAPS["lp3"], 12, 32, 1, channels=2))
+
+
+def test_host_entry_large_prefaulted_output():
+    """The NumPy entry at 2^26 int16 -> int32 (a fresh 256 MiB output, pre-faulted by the host
+    threads of run_host) and the C entry writing u8 output over its own u8 input (aliased:
+    no pre-fault writes may touch the input)."""
+    x = np.random.default_rng(20260301).integers(-32768, 32768, 1 << 26, dtype=np.int16)
+    y = fir_hip.fir1d_fixed_rows(x, TAPS["wrap5"], 12, 32, fir_hip.OUT_I32)
+    assert np.array_equal(y, _co().fir1d_rows(x, TAPS["wrap5"], 12, 32, 1))
+    xu = np.random.default_rng(20260302).integers(0, 256, 1 << 26, dtype=np.uint8)
+    ref = _co().fir1d_rows(xu, TAPS["sharpen5"], 12, 32, 0)
+    h = np.asarray(TAPS["sharpen5"], np.int32)
+    buf = xu.copy()
+    vp = ctypes.c_void_p
+    rc = fir_hip.lib().fir1d_fixed_rows(vp(buf.ctypes.data), fir_hip.IN_U8, 1, buf.size, 1, vp(h.ctypes.data),
+                                        h.size, 12, 32, fir_hip.OUT_U8_SAT, vp(buf.ctypes.data), 0)
+    assert rc == 0
+    assert np.array_equal(buf, ref)
 
 
 def test_repeat_launch_deterministic():
