@@ -90,6 +90,7 @@ class Workload:
 
     def __init__(self, name: str, rank: int, world: int, dev: torch.device, log2n: int):
         self.name, self.rank, self.world, self.dev = name, rank, world, dev
+        self.gen2d = False
         rng = np.random.default_rng(SEED + rank)
         if name == "fir1d_i16":
             self.n = 1 << log2n
@@ -118,12 +119,17 @@ class Workload:
             self.h = self.w = 8192
             h1 = np.array(SIMPLE_LP5, dtype=np.int64)
             self.hq2 = (np.outer(h1, h1) // 4096).astype(np.int64)  # unity-gain 5x5 Q4.12
+            # FIR2D_TAPS=gen5x5: a non-separable signed 5x5 (the general packed-16 form) instead
+            self.gen2d = os.environ.get("FIR2D_TAPS") == "gen5x5"
+            if self.gen2d:
+                self.hq2 = np.random.default_rng(55).integers(-4, 5, (5, 5)).astype(np.int64)
             self.x_host = rng.integers(0, 256, (self.h, self.w), dtype=np.uint8)
             self.bytes_per_unit = 1 + 1
             self.units = self.h * self.w
             self.unit = "Gpixels/s"
             self.dtype = "int32 (u8 in, int32 wrap-around acc, u8 saturated out)"
-            self.config = {"workload": "fir2d_u8_5x5_simple_lp_outer_q4.12", "frame": [self.h, self.w],
+            self.config = {"workload": "fir2d_u8_5x5_" + ("nonseparable_signed_seed55" if self.gen2d else
+                                                          "simple_lp_outer_q4.12"), "frame": [self.h, self.w],
                            "parallelism": "single GPU (replicas when N > 1)"}
         elif name in ("ideal_u8", "bank_u8", "fir1d_u8"):
             self.n = 1 << log2n
@@ -489,7 +495,7 @@ def main() -> int:
                                   f"fir_1d_fixed_ref.py:94-128) on the first {m} samples, {tl:.2f} s"}
 
     traffic = None
-    pmc = ROOT / "profiles" / f"pmc_{args.workload}.json"
+    pmc = ROOT / "profiles" / f"pmc_{args.workload}{'_gen5x5' if wl.gen2d else ''}.json"
     if pmc.exists():
         try:
             summary = json.loads(pmc.read_text())
@@ -519,8 +525,9 @@ def main() -> int:
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": KERNELS[args.workload],
-                     "limiter": "VALU (~8.8 VALU instructions/pixel on packed 16-bit pixel pairs, DESIGN.md §5)" if args.workload == "fir2d_u8"
-                     else "HBM",
+                     "limiter": ("VALU (12.5 v_pk_mad_u16/pixel: general packed-16 form, DESIGN.md §5)" if wl.gen2d else
+                                 "VALU (~8.8 VALU instructions/pixel on packed 16-bit pixel pairs, DESIGN.md §5)")
+                     if args.workload == "fir2d_u8" else "HBM",
                      "kernel_avg_us": round(kern_avg_s * 1e6, 2), "algorithmic_bytes_per_launch": alg_bytes,
                      "timing": f"HIP events around {args.steps} back-to-back launches of the kernel"},
         "cpu_baseline": cpu,
