@@ -7,6 +7,7 @@ import ctypes
 import re
 from pathlib import Path
 
+import numpy as np
 import pytest
 
 import fir_hip
@@ -89,3 +90,26 @@ def test_ipc_argument_checks_without_device(lib):
     assert lib.fir_peek(None, None, 0) == 0  # empty no-op
     assert lib.fir_peek(None, None, 8) == 1
     assert lib.fir_peek(None, None, -1) == 1
+
+
+def test_out_argument_is_checked_before_any_call():
+    """``out=`` (reused host output): wrong dtype/shape/layout or an overlap with
+    the input is refused in the host layer, before the library is called."""
+    x = np.zeros((4, 64), np.uint8)
+    h = [1, 2, 1]
+    bad = [np.zeros((4, 64), np.int32), np.zeros((4, 63), np.uint8), np.zeros((64, 4), np.uint8).T,
+           [[0] * 64] * 4]
+    ro = np.zeros((4, 64), np.uint8)
+    ro.flags.writeable = False
+    for out in bad + [ro]:
+        with pytest.raises(fir_hip.FirHipError):
+            fir_hip.fir1d_fixed_rows(x, h, out=out)
+    with pytest.raises(fir_hip.FirHipError, match="overlap"):
+        fir_hip.fir2d_fixed(x, [[0, 1, 0]], out=x)
+    with pytest.raises(fir_hip.FirHipError, match="overlap"):
+        fir_hip.fir1d_fixed_rows_multi(x, [h], out=x[None])
+    with pytest.raises(fir_hip.FirHipError, match="overlap"):
+        fir_hip.fir1d_fixed_rows_sharded(x, h, out=x)
+    x16 = np.zeros(128, np.int16)
+    with pytest.raises(fir_hip.FirHipError, match="overlap"):  # partial overlap via a view
+        fir_hip.fir1d_fixed_rows(x16[:64].view(np.uint8), h, out=x16.view(np.uint8)[64:192])

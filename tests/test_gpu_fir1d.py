@@ -375,3 +375,27 @@ def test_generator_over_golden_images_uses_fused_path(tmp_path, images, image_ou
     for o in image_outputs["outputs"]:
         p = out / f"fixed_{o['tap']}" / f"{o['case_stem']}__{o['coeff_name']}_fixed_{o['tap']}_y_u8.npy"
         assert _sha(np.load(p)) == o["fixed_u8_sha256"], p.name
+
+
+@pytest.mark.gpu
+def test_out_argument_reuses_the_buffer():
+    """``out=`` returns the caller's array filled with the same bits as a fresh call, for the
+    single, multi-filter and 2-D entries, and in place over a u8 input."""
+    rng = np.random.default_rng(20261016)
+    x = rng.integers(0, 256, (37, 1001), dtype=np.uint8)
+    h = TAPS["sharpen5"]
+    ref = _co().fir1d_rows(x, h, 12, 32, 0)
+    out = np.full_like(x, 7)
+    assert fir_hip.fir1d_fixed_rows(x, h, out=out) is out and np.array_equal(out, ref)
+    buf = x.copy()
+    assert fir_hip.fir1d_fixed_rows(buf, h, out=buf) is buf and np.array_equal(buf, ref)
+    o32 = np.zeros(x.shape, np.int32)
+    fir_hip.fir1d_fixed_rows(x, h, out_stage=fir_hip.OUT_I32, out=o32)
+    assert np.array_equal(o32, fir_hip.fir1d_fixed_rows(x, h, out_stage=fir_hip.OUT_I32))
+    hq = np.stack([np.asarray(TAPS["lp3"] + [0, 0]), np.asarray(h)])
+    om = np.zeros((2,) + x.shape, np.uint8)
+    assert fir_hip.fir1d_fixed_rows_multi(x, hq, out=om) is om
+    assert np.array_equal(om, fir_hip.fir1d_fixed_rows_multi(x, hq))
+    k = [[1, 2, 1], [2, 4, 2], [1, 2, 1]]
+    o2 = np.zeros(x.shape, np.uint8)
+    assert fir_hip.fir2d_fixed(x, k, out=o2) is o2 and np.array_equal(o2, fir_hip.fir2d_fixed(x, k))

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Where a host-pointer call's time goes (2^28 int16 -> int32): the whole NumPy entry, a
-fresh 1 GiB output's first-touch cost alone, and the C entry into an already-touched output."""
+fresh 1 GiB output's first-touch cost alone, the C entry into an already-touched output, and
+the NumPy entry given that output as ``out=``."""
 import ctypes
 import json
 import sys
@@ -41,6 +42,7 @@ def main():
         "numpy_entry_ms": best(lambda: fir_hip.fir1d_fixed_rows(x, hq, 12, 32, fir_hip.OUT_I32)),
         "fresh_1GiB_output_first_touch_ms": best(lambda: np.empty(x.size, np.int32).fill(0)),
         "c_entry_touched_output_ms": best(direct),
+        "numpy_entry_reused_out_ms": best(lambda: fir_hip.fir1d_fixed_rows(x, hq, 12, 32, fir_hip.OUT_I32, out=y)),
     }
     out["pcie_bytes"] = 6 * x.size
     print(json.dumps(out))

@@ -134,8 +134,31 @@ def _taps_i32(hq) -> np.ndarray:
     return h.astype(np.int32)
 
 
+def _out_buf(out, shape, dtype, x, same_ok: bool = False) -> np.ndarray:
+    """The output array: a fresh one, or the caller's ``out`` (reused buffers skip the
+    first-touch page faults a fresh host array pays).  ``out`` must match
+    exactly and must not overlap the input ``x``, except that ``same_ok`` lets it BE the input
+    buffer (u8 in place: fir1d_fixed_rows' C entry stages the input on the device before any
+    write to the output, tested aliased)."""
+    if out is None:
+        return np.empty(shape, dtype=dtype)
+    if not isinstance(out, np.ndarray):
+        raise FirHipError("out must be a numpy array")
+    if out.dtype != np.dtype(dtype) or out.shape != tuple(shape):
+        raise FirHipError(f"out must be {np.dtype(dtype)} of shape {tuple(shape)}, "
+                          f"got {out.dtype} of shape {out.shape}")
+    if not out.flags.c_contiguous or not out.flags.writeable:
+        raise FirHipError("out must be C-contiguous and writeable")
+    if same_ok and out.ctypes.data == x.ctypes.data and out.nbytes == x.nbytes:
+        return out
+    if np.shares_memory(out, x):
+        raise FirHipError("out must not overlap the input")
+    return out
+
+
 def fir1d_fixed_rows(x: np.ndarray, hq, frac_bits: int = 12, acc_bits: int = 32,
-                     out_stage: int = OUT_U8_SAT, channels: int = 1, device: int = 0) -> np.ndarray:
+                     out_stage: int = OUT_U8_SAT, channels: int = 1, device: int = 0,
+                     out: np.ndarray | None = None) -> np.ndarray:
     """Row-wise same-mode fixed FIR of a uint8/int16 array (last axis = row of
     width*channels interleaved samples).  Returns uint8 (OUT_U8_SAT) or int32 (OUT_I32)."""
     x = np.ascontiguousarray(x)
@@ -152,7 +175,7 @@ def fir1d_fixed_rows(x: np.ndarray, hq, frac_bits: int = 12, acc_bits: int = 32,
     rows = x.size // rowlen if rowlen else 0
     if rowlen % channels:
         raise FirHipError("row length must be a multiple of channels")
-    y = np.empty(x.shape, dtype=np.uint8 if out_stage == OUT_U8_SAT else np.int32)
+    y = _out_buf(out, x.shape, np.uint8 if out_stage == OUT_U8_SAT else np.int32, x, same_ok=True)
     _check(lib().fir1d_fixed_rows(_ptr(x), in_dtype, rows, rowlen // channels, channels, _ptr(h), h.size,
                                   int(frac_bits), int(acc_bits), int(out_stage), _ptr(y), int(device)),
            "fir1d_fixed_rows")
@@ -160,7 +183,8 @@ def fir1d_fixed_rows(x: np.ndarray, hq, frac_bits: int = 12, acc_bits: int = 32,
 
 
 def fir1d_fixed_rows_sharded(x: np.ndarray, hq, frac_bits: int = 12, acc_bits: int = 32,
-                             out_stage: int = OUT_U8_SAT, channels: int = 1, devices=(0,)) -> np.ndarray:
+                             out_stage: int = OUT_U8_SAT, channels: int = 1, devices=(0,),
+                             out: np.ndarray | None = None) -> np.ndarray:
     """fir1d_fixed_rows spread over several devices of this process (``devices`` may repeat
     an id): row blocks for images, halo-widened segments for one long row."""
     x = np.ascontiguousarray(x)
@@ -180,7 +204,7 @@ def fir1d_fixed_rows_sharded(x: np.ndarray, hq, frac_bits: int = 12, acc_bits: i
     rows = x.size // rowlen if rowlen else 0
     if rowlen % channels:
         raise FirHipError("row length must be a multiple of channels")
-    y = np.empty(x.shape, dtype=np.uint8 if out_stage == OUT_U8_SAT else np.int32)
+    y = _out_buf(out, x.shape, np.uint8 if out_stage == OUT_U8_SAT else np.int32, x)
     _check(lib().fir1d_fixed_rows_sharded(_ptr(x), in_dtype, rows, rowlen // channels, channels, _ptr(h), h.size,
                                           int(frac_bits), int(acc_bits), int(out_stage), _ptr(y), _ptr(devs),
                                           devs.size), "fir1d_fixed_rows_sharded")
@@ -188,7 +212,8 @@ def fir1d_fixed_rows_sharded(x: np.ndarray, hq, frac_bits: int = 12, acc_bits: i
 
 
 def fir1d_fixed_rows_multi(x: np.ndarray, hq2, frac_bits: int = 12, acc_bits: int = 32,
-                           out_stage: int = OUT_U8_SAT, channels: int = 1, device: int = 0) -> np.ndarray:
+                           out_stage: int = OUT_U8_SAT, channels: int = 1, device: int = 0,
+                           out: np.ndarray | None = None) -> np.ndarray:
     """F filters (rows of the F x L array hq2) over the same x in one call; returns an
     array of shape (F, *x.shape).  u8 input is read once per 4 filters on the GPU."""
     x = np.ascontiguousarray(x)
@@ -211,7 +236,7 @@ def fir1d_fixed_rows_multi(x: np.ndarray, hq2, frac_bits: int = 12, acc_bits: in
     rows = x.size // rowlen if rowlen else 0
     if rowlen % channels:
         raise FirHipError("row length must be a multiple of channels")
-    y = np.empty((nf,) + x.shape, dtype=np.uint8 if out_stage == OUT_U8_SAT else np.int32)
+    y = _out_buf(out, (nf,) + x.shape, np.uint8 if out_stage == OUT_U8_SAT else np.int32, x)
     _check(lib().fir1d_fixed_rows_multi(_ptr(x), in_dtype, rows, rowlen // channels, channels, _ptr(h), L, nf,
                                         int(frac_bits), int(acc_bits), int(out_stage), _ptr(y), int(device)),
            "fir1d_fixed_rows_multi")
@@ -219,7 +244,7 @@ def fir1d_fixed_rows_multi(x: np.ndarray, hq2, frac_bits: int = 12, acc_bits: in
 
 
 def fir2d_fixed(x: np.ndarray, hq2, frac_bits: int = 12, acc_bits: int = 32, out_stage: int = OUT_U8_SAT,
-                device: int = 0) -> np.ndarray:
+                device: int = 0, out: np.ndarray | None = None) -> np.ndarray:
     """2-D same-mode fixed FIR of a uint8 frame with a (R, C) quantized kernel."""
     x = np.ascontiguousarray(x, dtype=np.uint8)
     if x.ndim != 2:
@@ -229,7 +254,7 @@ def fir2d_fixed(x: np.ndarray, hq2, frac_bits: int = 12, acc_bits: int = 32, out
         raise FirHipError("hq2 must be 2-D")
     R, C = h2.shape
     h = _taps_i32(h2.reshape(-1))
-    y = np.empty(x.shape, dtype=np.uint8 if out_stage == OUT_U8_SAT else np.int32)
+    y = _out_buf(out, x.shape, np.uint8 if out_stage == OUT_U8_SAT else np.int32, x)
     _check(lib().fir2d_fixed(_ptr(x), x.shape[0], x.shape[1], _ptr(h), R, C, int(frac_bits), int(acc_bits),
                              int(out_stage), _ptr(y), int(device)), "fir2d_fixed")
     return y
