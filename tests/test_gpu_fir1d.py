@@ -399,3 +399,25 @@ def test_out_argument_reuses_the_buffer():
     k = [[1, 2, 1], [2, 4, 2], [1, 2, 1]]
     o2 = np.zeros(x.shape, np.uint8)
     assert fir_hip.fir2d_fixed(x, k, out=o2) is o2 and np.array_equal(o2, fir_hip.fir2d_fixed(x, k))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,dtype,channels,taps", [
+    ((1, 2 * ((1 << 25) + 37)), np.int16, 2, 63),    # one long row: 8 halo-reading segments
+    ((1, (1 << 26) + 13), np.uint8, 1, 4),            # ragged last segment, even taps
+    ((4099, 16411), np.uint8, 1, 5),                  # row blocks
+])
+def test_host_entry_chunked_overlap(shape, dtype, channels, taps):
+    """Host calls of >= 64 MiB run in 8 chunks with the H2D and D2H copies overlapped
+    (capi.hip run_host_chunked); same bits as the oracle, also in place for u8."""
+    rng = np.random.default_rng(20261017)
+    info = np.iinfo(dtype)
+    x = rng.integers(info.min, info.max + 1, shape, dtype=dtype)
+    hq = rng.integers(-3000, 3000, taps).tolist()
+    stage = fir_hip.OUT_I32 if dtype == np.int16 else fir_hip.OUT_U8_SAT
+    ref = _co().fir1d_rows(x, hq, 12, 32, 1 if stage == fir_hip.OUT_I32 else 0, channels=channels)
+    assert np.array_equal(fir_hip.fir1d_fixed_rows(x, hq, out_stage=stage, channels=channels), ref)
+    if dtype == np.uint8:
+        buf = x.copy()
+        fir_hip.fir1d_fixed_rows(buf, hq, out=buf)
+        assert np.array_equal(buf, ref)

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -44,6 +46,7 @@ struct DeviceState {
     std::mutex mu;
     bool init = false;
     hipStream_t stream = nullptr;
+    hipStream_t stream_d2h = nullptr;  // the chunked host path's device-to-host copies
     DeviceBuf in, out;
 };
 
@@ -105,6 +108,7 @@ int init_locked(DeviceState* st, int device) {
         return fail(FIR_ENODEV, std::string("device ") + std::to_string(device) + " is " + p.gcnArchName +
                                     "; libfir_hip is built for gfx950 (MI355X) only");
     HIP_TRY(hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&st->stream_d2h, hipStreamNonBlocking));
     st->init = true;
     return FIR_OK;
 }
@@ -136,6 +140,102 @@ int run_host(int device, const void* x, size_t in_bytes, void* y, size_t out_byt
     }
     HIP_TRY(hipMemcpyAsync(y, (char*)st->out.ptr + out_skip, out_bytes, hipMemcpyDeviceToHost, st->stream));
     HIP_TRY(hipStreamSynchronize(st->stream));
+    return FIR_OK;
+}
+
+// Large fir1d_fixed_rows host calls in kChunks pieces so the two PCIe directions overlap: this
+// thread issues chunk i's H2D and then chunk i-1's kernel on `stream` (a single row's segment
+// reads its right halo from chunk i, already staged); a second host thread issues chunk i-1's
+// D2H on `stream_d2h` behind that kernel's event.  Row blocks for images (no halo), 64-sample
+// aligned segments through launch_fir1d_segment for one long row (halos inside the staged
+// input, zero at the signal ends).  A u8 in-place call stays correct: chunk i's output is
+// copied back only after chunk i+1's input left the host.  FIR_HOST_CHUNKED=0 turns it off.
+constexpr int kChunks = 8;
+constexpr size_t kChunkedMinBytes = size_t(64) << 20;
+
+bool use_chunked(int64_t rows, int64_t n, int in_dtype) {
+    static const bool on = [] {
+        const char* e = std::getenv("FIR_HOST_CHUNKED");
+        return !(e && e[0] == '0');
+    }();
+    return on && (rows == 1 || rows >= kChunks) && (size_t)n * in_size(in_dtype) >= kChunkedMinBytes;
+}
+
+int run_host_chunked(int device, const void* x, int in_dtype, int64_t rows, int64_t width, int ch,
+                     const int32_t* hq, int taps, int frac, int acc, int stage, void* y) {
+    DeviceRestore restore;
+    DeviceState* st = nullptr;
+    int rc = device_state(device, &st);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(st->mu);
+    if ((rc = init_locked(st, device))) return rc;
+    const size_t isz = in_size(in_dtype), osz = out_size(stage);
+    const int64_t n = rows * width * ch;
+    if ((rc = ensure(st->in, (size_t)n * isz)) || (rc = ensure(st->out, (size_t)n * osz))) return rc;
+    int64_t b[kChunks + 1];
+    for (int i = 0; i <= kChunks; ++i)
+        b[i] = rows > 1 ? rows * i / kChunks * width * ch : (i == kChunks ? n : n / kChunks * i / 64 * 64);
+    const int64_t hl = (int64_t)(taps - 1 - taps / 2) * ch, hr = (int64_t)(taps / 2) * ch;
+    if (rows == 1 && (b[1] < hl + hr || n - b[kChunks - 1] < hl + hr))
+        return run_host(device, x, (size_t)n * isz, y, (size_t)n * osz, [&](void* dx, void* dy, hipStream_t s, std::string* err) {
+            return fir::launch_fir1d_rows(dx, in_dtype, rows, width, ch, hq, taps, frac, acc, stage, dy, s, err);
+        });
+    char* dx = (char*)st->in.ptr;
+    char* dy = (char*)st->out.ptr;
+    hipEvent_t ev[kChunks];
+    for (int i = 0; i < kChunks; ++i) HIP_TRY(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+    std::atomic<int> ready{0};  // kernels whose event is recorded (kChunks + 1: abort)
+    hipError_t d2h_err = hipSuccess;
+    std::thread d2h([&] {
+        (void)hipSetDevice(device);
+        for (int i = 0; i < kChunks; ++i) {
+            int r;
+            while ((r = ready.load(std::memory_order_acquire)) <= i) std::this_thread::yield();
+            if (r > kChunks) return;
+            hipError_t e = hipStreamWaitEvent(st->stream_d2h, ev[i], 0);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync((char*)y + b[i] * osz, dy + b[i] * osz, (size_t)(b[i + 1] - b[i]) * osz,
+                                   hipMemcpyDeviceToHost, st->stream_d2h);
+            if (e != hipSuccess) {
+                d2h_err = e;
+                return;
+            }
+        }
+        d2h_err = hipStreamSynchronize(st->stream_d2h);
+    });
+    std::string err;
+    hipError_t e = hipSuccess;
+    auto kernel = [&](int i) -> int {
+        int r;
+        if (rows > 1)
+            r = fir::launch_fir1d_rows(dx + b[i] * isz, in_dtype, (b[i + 1] - b[i]) / (width * ch), width, ch, hq, taps,
+                                       frac, acc, stage, dy + b[i] * osz, st->stream, &err);
+        else
+            r = fir::launch_fir1d_segment(dx + b[i] * isz, in_dtype, (b[i + 1] - b[i]) / ch, ch, hq, taps, frac, acc,
+                                          stage, i ? dx + (b[i] - hl) * isz : nullptr,
+                                          i + 1 < kChunks ? dx + b[i + 1] * isz : nullptr, dy + b[i] * osz,
+                                          st->stream, &err);
+        if (r) return r;
+        e = hipEventRecord(ev[i], st->stream);
+        if (e != hipSuccess) return FIR_EHIP;
+        ready.store(i + 1, std::memory_order_release);
+        return FIR_OK;
+    };
+    for (int i = 0; i <= kChunks && !rc; ++i) {
+        if (i < kChunks) {
+            e = hipMemcpyAsync(dx + b[i] * isz, (const char*)x + b[i] * isz, (size_t)(b[i + 1] - b[i]) * isz,
+                               hipMemcpyHostToDevice, st->stream);
+            if (e != hipSuccess) rc = FIR_EHIP;
+        }
+        if (!rc && i > 0) rc = kernel(i - 1);
+    }
+    if (rc) ready.store(kChunks + 1, std::memory_order_release);
+    d2h.join();
+    (void)hipStreamSynchronize(st->stream);
+    for (int i = 0; i < kChunks; ++i) (void)hipEventDestroy(ev[i]);
+    if (rc == FIR_EHIP && err.empty()) return fail(rc, std::string("chunked host path: ") + hipGetErrorString(e));
+    if (rc) return fail(rc, err);
+    if (d2h_err != hipSuccess) return fail(FIR_EHIP, std::string("chunked host path D2H: ") + hipGetErrorString(d2h_err));
     return FIR_OK;
 }
 
@@ -178,6 +278,15 @@ int fir1d_fixed_rows(const void* x, int in_dtype, int64_t rows, int64_t width, i
             return rc ? fail(rc, err) : FIR_OK;
         }
         if (!x || !y) return fail(FIR_EINVAL, "x and y must not be NULL");
+        if (use_chunked(rows, n, in_dtype)) {
+            // scalar arguments validated by a zero-size launch first, as the unchunked path does
+            std::string err;
+            int rc = fir::launch_fir1d_rows(nullptr, in_dtype, 0, 0, channels, hq, taps, frac_bits, acc_bits,
+                                            out_stage, nullptr, nullptr, &err);
+            if (rc) return fail(rc, err);
+            return run_host_chunked(device, x, in_dtype, rows, width, channels, hq, taps, frac_bits, acc_bits,
+                                    out_stage, y);
+        }
         return run_host(device, x, (size_t)n * in_size(in_dtype), y, (size_t)n * out_size(out_stage),
                         [&](void* dx, void* dy, hipStream_t s, std::string* err) {
                             return fir::launch_fir1d_rows(dx, in_dtype, rows, width, channels, hq, taps, frac_bits,
