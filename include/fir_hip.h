@@ -173,8 +173,15 @@ int fir_restore_u8_dev(const double* a_dev, int64_t n, int policy, uint8_t* out_
  *   dev_ptr, and dev_ptr's byte offset inside that allocation.
  * fir_ipc_import: map a handle exported by ANOTHER process on this node for kernels on
  *   `device`; *dev_ptr_out = mapped base + offset.  Release with fir_ipc_close(*dev_ptr_out).
- * fir_peek: synchronous copy of `bytes` device bytes (own or imported) to host memory. */
+ * fir_peek: synchronous copy of `bytes` device bytes (own or imported) to host memory.
+ * fir_device_bus_id: the PCI bus id ("0000:05:00.0") of `device`, NUL-terminated in `out`.
+ * fir_peer_access: *can = 1 when kernels on `device` may read the HBM of the GPU with PCI bus
+ *   id `peer_bus_id` (the same GPU, or a peer visible to this process with peer access);
+ *   0 when that GPU is not visible here or has no peer path.  Checked before any kernel
+ *   reads a mapped neighbour (a mapping alone does not prove a kernel may read it). */
 #define FIR_IPC_HANDLE_BYTES 64
+int fir_device_bus_id(int device, char* out, int len);
+int fir_peer_access(int device, const char* peer_bus_id, int* can);
 int fir_ipc_export(const void* dev_ptr, void* handle_out, int64_t* offset_out);
 int fir_ipc_import(const void* handle, int64_t offset, int device, void** dev_ptr_out);
 int fir_ipc_close(void* dev_ptr);

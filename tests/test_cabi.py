@@ -90,6 +90,11 @@ def test_ipc_argument_checks_without_device(lib):
     assert lib.fir_peek(None, None, 0) == 0  # empty no-op
     assert lib.fir_peek(None, None, 8) == 1
     assert lib.fir_peek(None, None, -1) == 1
+    can = ctypes.c_int32(7)
+    assert lib.fir_device_bus_id(0, None, 64) == 1 and b"16 bytes" in lib.fir_last_error()
+    assert lib.fir_device_bus_id(0, ctypes.create_string_buffer(8), 8) == 1
+    assert lib.fir_peer_access(0, None, ctypes.byref(can)) == 1 and b"NULL" in lib.fir_last_error()
+    assert lib.fir_peer_access(0, b"0000:00:00.0", None) == 1
 
 
 def test_out_argument_is_checked_before_any_call():

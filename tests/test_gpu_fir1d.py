@@ -406,6 +406,11 @@ def test_out_argument_reuses_the_buffer():
     ((1, 2 * ((1 << 25) + 37)), np.int16, 2, 63),    # one long row: 8 halo-reading segments
     ((1, (1 << 26) + 13), np.uint8, 1, 4),            # ragged last segment, even taps
     ((4099, 16411), np.uint8, 1, 5),                  # row blocks
+    ((1, 3 * ((1 << 26) + 11)), np.uint8, 3, 5),      # frames of 3 channels: segments start on a frame
+    ((1, 3 * ((1 << 25) + 5)), np.int16, 3, 3),       # same, int16 (generic kernel per segment)
+    ((1, 5 * ((1 << 24) + 3)), np.int16, 5, 1),       # one tap: any channel count is legal
+    ((1, 1000003 * 70), np.uint8, 1000003, 1),        # frames longer than a chunk: unchunked
+    ((1031, 3 * 21701), np.int16, 3, 5),              # row blocks of 3-channel rows
 ])
 def test_host_entry_chunked_overlap(shape, dtype, channels, taps):
     """Host calls of >= 64 MiB run in 8 chunks with the H2D and D2H copies overlapped

@@ -218,6 +218,20 @@ def test_xgmi_peer_halos_across_processes(world, taps, ch):
     assert kind == "xgmi" and ok
 
 
+def test_peer_access_check():
+    """The guard XgmiHalo runs before any kernel reads a neighbour: this GPU can read itself,
+    and a bus id no visible GPU has is refused (that rank then takes the RCCL path)."""
+    import fir_hip as fh
+
+    bus = fh.device_bus_id(0)
+    assert len(bus) >= 7 and ":" in bus
+    assert fh.peer_access(0, bus)
+    assert not fh.peer_access(0, "0000:ff:1f.7")
+    for d in range(fh.device_count()):
+        other = fh.device_bus_id(d)
+        assert fh.peer_access(0, other) in (True, False)
+
+
 @pytest.mark.parametrize("dtype,ch,stage", [(np.int16, 1, 1), (np.int16, 2, 1), (np.int16, 1, 0), (np.uint8, 1, 0),
                                             (np.uint8, 1, 1)])
 @pytest.mark.parametrize("n", [8, 16, 4096, 4099, 1 << 20, (1 << 20) + 16, 3])

@@ -9,7 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <atomic>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -19,6 +19,7 @@
 #include <thread>
 #include <vector>
 
+#include "fir1d_reg_launch.h"
 #include "fir_hip.h"
 #include "fir_launch.h"
 
@@ -47,6 +48,8 @@ struct DeviceState {
     bool init = false;
     hipStream_t stream = nullptr;
     hipStream_t stream_d2h = nullptr;  // the chunked host path's device-to-host copies
+    static constexpr int kChunks = 8;
+    hipEvent_t chunk_ev[kChunks] = {};  // the chunked host path's per-chunk kernel events
     DeviceBuf in, out;
 };
 
@@ -107,8 +110,10 @@ int init_locked(DeviceState* st, int device) {
     if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0)
         return fail(FIR_ENODEV, std::string("device ") + std::to_string(device) + " is " + p.gcnArchName +
                                     "; libfir_hip is built for gfx950 (MI355X) only");
-    HIP_TRY(hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking));
-    HIP_TRY(hipStreamCreateWithFlags(&st->stream_d2h, hipStreamNonBlocking));
+    if (!st->stream) HIP_TRY(hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking));
+    if (!st->stream_d2h) HIP_TRY(hipStreamCreateWithFlags(&st->stream_d2h, hipStreamNonBlocking));
+    for (hipEvent_t& ev : st->chunk_ev)
+        if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     st->init = true;
     return FIR_OK;
 }
@@ -146,11 +151,14 @@ int run_host(int device, const void* x, size_t in_bytes, void* y, size_t out_byt
 // Large fir1d_fixed_rows host calls in kChunks pieces so the two PCIe directions overlap: this
 // thread issues chunk i's H2D and then chunk i-1's kernel on `stream` (a single row's segment
 // reads its right halo from chunk i, already staged); a second host thread issues chunk i-1's
-// D2H on `stream_d2h` behind that kernel's event.  Row blocks for images (no halo), 64-sample
-// aligned segments through launch_fir1d_segment for one long row (halos inside the staged
-// input, zero at the signal ends).  A u8 in-place call stays correct: chunk i's output is
-// copied back only after chunk i+1's input left the host.  FIR_HOST_CHUNKED=0 turns it off.
-constexpr int kChunks = 8;
+// D2H on `stream_d2h` behind that kernel's event (a pageable D2H blocks its issuing thread).
+// Chunk boundaries: row blocks for images (block starts kept 16-byte aligned so every chunk
+// stays on the register kernel), and for one long row whole frames (`ch` samples) rounded to
+// the register kernel's wave tile, so every interior segment is one halo-reading launch
+// (halos inside the staged input, zero at the signal ends).  A u8 in-place call stays
+// correct: chunk i's output is copied back only after chunk i+1's input left the host.
+// FIR_HOST_CHUNKED=0 turns it off.
+constexpr int kChunks = DeviceState::kChunks;
 constexpr size_t kChunkedMinBytes = size_t(64) << 20;
 
 bool use_chunked(int64_t rows, int64_t n, int in_dtype) {
@@ -161,37 +169,72 @@ bool use_chunked(int64_t rows, int64_t n, int in_dtype) {
     return on && (rows == 1 || rows >= kChunks) && (size_t)n * in_size(in_dtype) >= kChunkedMinBytes;
 }
 
+int64_t gcd64(int64_t a, int64_t b) {
+    while (b) {
+        const int64_t t = a % b;
+        a = b;
+        b = t;
+    }
+    return a;
+}
+
+// Chunk boundaries b[0..kChunks] in samples (see above); false when some chunk would be too
+// short to hold its halos (the caller then runs the call unchunked).
+bool chunk_bounds(int64_t rows, int64_t width, int ch, int in_dtype, int stage, int taps, int64_t b[kChunks + 1]) {
+    const int64_t rowlen = width * ch, n = rows * rowlen;
+    b[0] = 0;
+    b[kChunks] = n;
+    if (rows > 1) {
+        const int64_t minsz = (int64_t)std::min(in_size(in_dtype), out_size(stage));
+        const int64_t ra = 16 / gcd64(16, rowlen * minsz % 16);  // rows per 16-byte-aligned block start
+        const int64_t units = rows / ra;
+        if (units < kChunks) return false;
+        for (int i = 1; i < kChunks; ++i) b[i] = units * i / kChunks * ra * rowlen;
+        return true;
+    }
+    const int64_t tile = fir::reg_tile_samples(in_dtype == FIR_IN_U8);
+    const int64_t g = tile / gcd64(tile, ch) * ch;  // lcm(tile, ch) samples
+    const int64_t units = n / g;
+    if (units < kChunks) return false;
+    for (int i = 1; i < kChunks; ++i) b[i] = units * i / kChunks * g;
+    const int64_t halo = (int64_t)(taps - 1) * ch;
+    for (int i = 0; i < kChunks; ++i)
+        if (b[i + 1] - b[i] < halo) return false;
+    return true;
+}
+
 int run_host_chunked(int device, const void* x, int in_dtype, int64_t rows, int64_t width, int ch,
                      const int32_t* hq, int taps, int frac, int acc, int stage, void* y) {
+    const size_t isz = in_size(in_dtype), osz = out_size(stage);
+    const int64_t n = rows * width * ch;
+    int64_t b[kChunks + 1];
+    if (!chunk_bounds(rows, width, ch, in_dtype, stage, taps, b))
+        return run_host(device, x, (size_t)n * isz, y, (size_t)n * osz, [&](void* dx, void* dy, hipStream_t s, std::string* err) {
+            return fir::launch_fir1d_rows(dx, in_dtype, rows, width, ch, hq, taps, frac, acc, stage, dy, s, err);
+        });
     DeviceRestore restore;
     DeviceState* st = nullptr;
     int rc = device_state(device, &st);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(st->mu);
     if ((rc = init_locked(st, device))) return rc;
-    const size_t isz = in_size(in_dtype), osz = out_size(stage);
-    const int64_t n = rows * width * ch;
     if ((rc = ensure(st->in, (size_t)n * isz)) || (rc = ensure(st->out, (size_t)n * osz))) return rc;
-    int64_t b[kChunks + 1];
-    for (int i = 0; i <= kChunks; ++i)
-        b[i] = rows > 1 ? rows * i / kChunks * width * ch : (i == kChunks ? n : n / kChunks * i / 64 * 64);
-    const int64_t hl = (int64_t)(taps - 1 - taps / 2) * ch, hr = (int64_t)(taps / 2) * ch;
-    if (rows == 1 && (b[1] < hl + hr || n - b[kChunks - 1] < hl + hr))
-        return run_host(device, x, (size_t)n * isz, y, (size_t)n * osz, [&](void* dx, void* dy, hipStream_t s, std::string* err) {
-            return fir::launch_fir1d_rows(dx, in_dtype, rows, width, ch, hq, taps, frac, acc, stage, dy, s, err);
-        });
+    const int64_t hl = (int64_t)(taps - 1 - taps / 2) * ch;
     char* dx = (char*)st->in.ptr;
     char* dy = (char*)st->out.ptr;
-    hipEvent_t ev[kChunks];
-    for (int i = 0; i < kChunks; ++i) HIP_TRY(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
-    std::atomic<int> ready{0};  // kernels whose event is recorded (kChunks + 1: abort)
+    hipEvent_t* ev = st->chunk_ev;
+    std::mutex mu;
+    std::condition_variable cv;
+    int ready = 0;  // kernels whose event is recorded (kChunks + 1: abort)
     hipError_t d2h_err = hipSuccess;
     std::thread d2h([&] {
         (void)hipSetDevice(device);
         for (int i = 0; i < kChunks; ++i) {
-            int r;
-            while ((r = ready.load(std::memory_order_acquire)) <= i) std::this_thread::yield();
-            if (r > kChunks) return;
+            {
+                std::unique_lock<std::mutex> g(mu);
+                cv.wait(g, [&] { return ready > i; });
+                if (ready > kChunks) return;
+            }
             hipError_t e = hipStreamWaitEvent(st->stream_d2h, ev[i], 0);
             if (e == hipSuccess)
                 e = hipMemcpyAsync((char*)y + b[i] * osz, dy + b[i] * osz, (size_t)(b[i + 1] - b[i]) * osz,
@@ -201,8 +244,14 @@ int run_host_chunked(int device, const void* x, int in_dtype, int64_t rows, int6
                 return;
             }
         }
-        d2h_err = hipStreamSynchronize(st->stream_d2h);
     });
+    auto post = [&](int v) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            ready = v;
+        }
+        cv.notify_one();
+    };
     std::string err;
     hipError_t e = hipSuccess;
     auto kernel = [&](int i) -> int {
@@ -218,7 +267,7 @@ int run_host_chunked(int device, const void* x, int in_dtype, int64_t rows, int6
         if (r) return r;
         e = hipEventRecord(ev[i], st->stream);
         if (e != hipSuccess) return FIR_EHIP;
-        ready.store(i + 1, std::memory_order_release);
+        post(i + 1);
         return FIR_OK;
     };
     for (int i = 0; i <= kChunks && !rc; ++i) {
@@ -229,13 +278,16 @@ int run_host_chunked(int device, const void* x, int in_dtype, int64_t rows, int6
         }
         if (!rc && i > 0) rc = kernel(i - 1);
     }
-    if (rc) ready.store(kChunks + 1, std::memory_order_release);
+    if (rc) post(kChunks + 1);
     d2h.join();
+    // Every copy already queued must land before returning, on success or failure: the caller
+    // may free `y`, and the next call reuses st->out.
+    const hipError_t sync_d2h = hipStreamSynchronize(st->stream_d2h);
     (void)hipStreamSynchronize(st->stream);
-    for (int i = 0; i < kChunks; ++i) (void)hipEventDestroy(ev[i]);
     if (rc == FIR_EHIP && err.empty()) return fail(rc, std::string("chunked host path: ") + hipGetErrorString(e));
     if (rc) return fail(rc, err);
     if (d2h_err != hipSuccess) return fail(FIR_EHIP, std::string("chunked host path D2H: ") + hipGetErrorString(d2h_err));
+    if (sync_d2h != hipSuccess) return fail(FIR_EHIP, std::string("chunked host path D2H: ") + hipGetErrorString(sync_d2h));
     return FIR_OK;
 }
 
@@ -662,6 +714,41 @@ int fir_ipc_close(void* dev_ptr) {
         }
         hipError_t e = hipIpcCloseMemHandle(base);
         if (e != hipSuccess) return fail(FIR_EHIP, std::string("hipIpcCloseMemHandle: ") + hipGetErrorString(e));
+        return FIR_OK;
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int fir_device_bus_id(int device, char* out, int len) {
+    try {
+        if (!out || len < 16) return fail(FIR_EINVAL, "out must hold at least 16 bytes");
+        out[0] = 0;
+        hipError_t e = hipDeviceGetPCIBusId(out, len, device);
+        if (e != hipSuccess) return fail(FIR_ENODEV, std::string("hipDeviceGetPCIBusId: ") + hipGetErrorString(e));
+        return FIR_OK;
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int fir_peer_access(int device, const char* peer_bus_id, int* can) {
+    try {
+        if (!peer_bus_id || !can) return fail(FIR_EINVAL, "NULL argument");
+        *can = 0;
+        int peer = -1;
+        if (hipDeviceGetByPCIBusId(&peer, peer_bus_id) != hipSuccess || peer < 0) {
+            (void)hipGetLastError();  // not visible to this process: no kernel path to it
+            return FIR_OK;
+        }
+        if (peer == device) {
+            *can = 1;
+            return FIR_OK;
+        }
+        int ok = 0;
+        hipError_t e = hipDeviceCanAccessPeer(&ok, device, peer);
+        if (e != hipSuccess) return fail(FIR_EHIP, std::string("hipDeviceCanAccessPeer: ") + hipGetErrorString(e));
+        *can = ok ? 1 : 0;
         return FIR_OK;
     } catch (...) {
         return fail(FIR_EHIP, "internal error");

@@ -24,7 +24,7 @@ __all__ = [
     "FirHipError", "lib", "lib_path", "device_count", "fir1d_fixed_rows", "fir1d_fixed_rows_multi",
     "fir1d_fixed_rows_sharded", "fir2d_fixed", "fir1d_ideal_rows", "compare_metrics", "restore_u8", "IN_U8", "IN_I16",
     "OUT_U8_SAT", "OUT_I32", "RESTORE_CLIP", "RESTORE_NORMALIZE", "MAX_TAPS", "EXPORTS", "ipc_export", "ipc_import",
-    "ipc_close", "peek", "IPC_HANDLE_BYTES",
+    "ipc_close", "peek", "IPC_HANDLE_BYTES", "device_bus_id", "peer_access",
 ]
 
 IN_U8, IN_I16 = 0, 1
@@ -73,6 +73,8 @@ EXPORTS = {
     "fir_ipc_import": (_i32, [_vp, _i64, _i32, ctypes.POINTER(_vp)]),
     "fir_ipc_close": (_i32, [_vp]),
     "fir_peek": (_i32, [_vp, _vp, _i64]),
+    "fir_device_bus_id": (_i32, [_i32, ctypes.c_char_p, _i32]),
+    "fir_peer_access": (_i32, [_i32, ctypes.c_char_p, ctypes.POINTER(_i32)]),
 }
 
 _lib = None
@@ -329,6 +331,20 @@ def ipc_import(handle: bytes, offset: int, device: int) -> int:
 
 def ipc_close(dev_ptr: int) -> None:
     _check(lib().fir_ipc_close(ctypes.c_void_p(dev_ptr)), "fir_ipc_close")
+
+
+def device_bus_id(device: int) -> str:
+    """PCI bus id of ``device`` (names the GPU across processes with different device orders)."""
+    buf = ctypes.create_string_buffer(64)
+    _check(lib().fir_device_bus_id(int(device), buf, 64), "fir_device_bus_id")
+    return buf.value.decode()
+
+
+def peer_access(device: int, peer_bus_id: str) -> bool:
+    """Whether kernels on ``device`` may read the HBM of the GPU at ``peer_bus_id``."""
+    can = _i32(0)
+    _check(lib().fir_peer_access(int(device), peer_bus_id.encode(), ctypes.byref(can)), "fir_peer_access")
+    return bool(can.value)
 
 
 def peek(dev_ptr: int, nbytes: int) -> bytes:

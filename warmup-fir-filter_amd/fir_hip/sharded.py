@@ -129,16 +129,22 @@ class XgmiHalo:
         hl, hr = halo_sizes(taps, channels)
         if seg.numel() < max(hl, hr):
             raise ValueError("segment shorter than the filter halo")
+        dev = seg.device.index
         handle, off = fir_hip.ipc_export(seg.data_ptr())
         np_dtype = seg[:1].cpu().numpy().dtype
         mine = {"handle": handle, "offset": off, "numel": seg.numel(), "elt": seg.element_size(),
+                "bus": fir_hip.device_bus_id(dev),
                 "first": seg[:hr].cpu().numpy().tobytes(), "last": seg[seg.numel() - hl:].cpu().numpy().tobytes()}
         infos = [None] * world
         dist.all_gather_object(infos, mine, group=group)
-        dev = seg.device.index
         self.left_ptr = self.right_ptr = None
         self.left_host = self.right_host = None
         self._mapped = []
+        # a kernel on this GPU will load from the neighbours' HBM: refuse (-> RCCL on every rank)
+        # unless this process sees that GPU with a peer path, before mapping anything
+        for r in ((rank - 1,) if rank > 0 and hl else ()) + ((rank + 1,) if rank < world - 1 and hr else ()):
+            if not fir_hip.peer_access(dev, infos[r]["bus"]):
+                raise RuntimeError(f"no peer access from device {dev} to rank {r}'s GPU {infos[r]['bus']}")
         try:
             if rank > 0 and hl:
                 p = infos[rank - 1]
