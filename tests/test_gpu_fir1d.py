@@ -424,5 +424,5 @@ def test_host_entry_chunked_overlap(shape, dtype, channels, taps):
     assert np.array_equal(fir_hip.fir1d_fixed_rows(x, hq, out_stage=stage, channels=channels), ref)
     if dtype == np.uint8:
         buf = x.copy()
-        fir_hip.fir1d_fixed_rows(buf, hq, out=buf)
+        fir_hip.fir1d_fixed_rows(buf, hq, channels=channels, out=buf)
         assert np.array_equal(buf, ref)
