@@ -1,0 +1,327 @@
+// stream_micro.hip — HBM stream ceilings for the headline kernel's traffic (dev tool, not the
+// product): 2^28 int16 read, 2^28 int32 written (the 5-tap int16 -> int32 FIR's bytes), with
+// the read side as register loads or LDS-DMA (global_load_lds_dwordx4), default or
+// non-temporal policy, and the store side's shape and cache policy; plus read-only and write-only
+// ceilings of the same sizes.  Variants interleaved round-robin in one process; the widen
+// copies are checked against the CPU.
+//
+// Build: make -C tools/microbench     Run: tools/microbench/stream_micro [rounds]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#define CK(e)                                                                              \
+    do {                                                                                   \
+        hipError_t _e = (e);                                                               \
+        if (_e != hipSuccess) {                                                            \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #e, hipGetErrorString(_e)); \
+            exit(1);                                                                       \
+        }                                                                                  \
+    } while (0)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+constexpr int kAuxNt = 2;  // CPol NT on gfx94x/gfx950
+
+__device__ __forceinline__ void st_nt(u32x4* p, u32x4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+
+__device__ __forceinline__ void glds16(const void* g, void* lds_wave_base, bool nt) {
+    if (nt)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                         (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, kAuxNt);
+    else
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                         (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ u32x4 widen_lo(u32x2 d) {  // 4 int16 -> 4 int32
+    return u32x4{(uint32_t)(int32_t)(int16_t)d.x, (uint32_t)((int32_t)d.x >> 16), (uint32_t)(int32_t)(int16_t)d.y,
+                 (uint32_t)((int32_t)d.y >> 16)};
+}
+
+// ---- widen copies: K KiB of int16 per wave -> 2K KiB of int32 ---------------------------
+// Register path: lane loads 16 B per KiB, LDS transpose, 1 KiB nt row stores (the FIR's shape).
+template <int K, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void widen_reg(const int16_t* __restrict__ x, int32_t* __restrict__ y) {
+    __shared__ u32x4 sb[BLOCK / 64][K * 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t wave = (int64_t)blockIdx.x * (BLOCK / 64) + w;
+    const u32x4* src = reinterpret_cast<const u32x4*>(x) + wave * (64 * K);
+    u32x4 d[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) d[k] = __builtin_nontemporal_load(src + k * 64 + lane);
+#pragma unroll
+    for (int k = 0; k < K; ++k) sb[w][k * 64 + lane] = d[k];
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    const u32x2* s2 = reinterpret_cast<const u32x2*>(&sb[w][0]);
+    u32x4* dst = reinterpret_cast<u32x4*>(y) + wave * (128 * K);
+#pragma unroll
+    for (int r = 0; r < 2 * K; ++r) st_nt(dst + r * 64 + lane, widen_lo(s2[r * 64 + lane]));
+}
+
+// LDS-DMA path: K global_load_lds_dwordx4 (1 KiB each) per wave, vmcnt(0), then rows as above.
+template <int K, int BLOCK, bool NT>
+__global__ __launch_bounds__(BLOCK) void widen_glds(const int16_t* __restrict__ x, int32_t* __restrict__ y) {
+    __shared__ u32x4 sb[BLOCK / 64][K * 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t wave = (int64_t)blockIdx.x * (BLOCK / 64) + w;
+    const u32x4* src = reinterpret_cast<const u32x4*>(x) + wave * (64 * K);
+#pragma unroll
+    for (int k = 0; k < K; ++k) glds16(src + k * 64 + lane, &sb[w][k * 64], NT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const u32x2* s2 = reinterpret_cast<const u32x2*>(&sb[w][0]);
+    u32x4* dst = reinterpret_cast<u32x4*>(y) + wave * (128 * K);
+#pragma unroll
+    for (int r = 0; r < 2 * K; ++r) st_nt(dst + r * 64 + lane, widen_lo(s2[r * 64 + lane]));
+}
+
+// ---- read-only / write-only ceilings ---------------------------------------------------
+template <int K, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void read_reg(const int16_t* __restrict__ x, int32_t* __restrict__ sink) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
+    const u32x4* src = reinterpret_cast<const u32x4*>(x) + wave * (64 * K);
+    u32x4 d[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) d[k] = __builtin_nontemporal_load(src + k * 64 + lane);
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) s ^= d[k].x ^ d[k].y ^ d[k].z ^ d[k].w;
+    if (s == 0x9E3779B9u) sink[lane] = (int32_t)s;  // keeps the loads
+}
+
+template <int K, int BLOCK, bool NT>
+__global__ __launch_bounds__(BLOCK) void read_glds(const int16_t* __restrict__ x, int32_t* __restrict__ sink) {
+    __shared__ u32x4 sb[BLOCK / 64][K * 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t wave = (int64_t)blockIdx.x * (BLOCK / 64) + w;
+    const u32x4* src = reinterpret_cast<const u32x4*>(x) + wave * (64 * K);
+#pragma unroll
+    for (int k = 0; k < K; ++k) glds16(src + k * 64 + lane, &sb[w][k * 64], NT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const u32x4 v = sb[w][lane];
+    if ((v.x ^ v.w) == 0x9E3779B9u) sink[lane] = 1;
+}
+
+template <int K, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void write_nt(int32_t* __restrict__ y) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
+    u32x4* dst = reinterpret_cast<u32x4*>(y) + wave * (64 * K);
+#pragma unroll
+    for (int k = 0; k < K; ++k) st_nt(dst + k * 64 + lane, u32x4{(uint32_t)lane, (uint32_t)k, 0u, 1u});
+}
+
+// Store patterns, R KiB per wave: P=0 whole 1 KiB rows (lane i -> bytes 16i of each row),
+// P=1 each lane 32 contiguous bytes per 2 KiB (two adjacent dwordx4), P=2 64 contiguous bytes
+// per 4 KiB.  POL: 0 plain, 1 nt, 2 sc0 sc1, 3 sc1.
+template <int POL>
+__device__ __forceinline__ void st16(u32x4* p, u32x4 v) {
+    if constexpr (POL == 0) asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 1) asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+    else asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+// Widen copies with the store side varied: H=1 a wave loads 512 B (8 B per lane) and stores one
+// 1 KiB row; H=0 a wave loads 1 KiB and stores (P=0) two rows through LDS or (P=1) each lane's
+// own 32 output bytes straight from registers.  POL as st16.
+template <int H, int P, int POL, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void widen_pat(const int16_t* __restrict__ x, int32_t* __restrict__ y) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t wave = (int64_t)blockIdx.x * (BLOCK / 64) + w;
+    if constexpr (H == 1) {
+        const u32x2* src = reinterpret_cast<const u32x2*>(x) + wave * 64;
+        const u32x2 d = __builtin_nontemporal_load(src + lane);
+        st16<POL>(reinterpret_cast<u32x4*>(y) + wave * 64 + lane, widen_lo(d));
+    } else if constexpr (P == 1) {
+        const u32x4* src = reinterpret_cast<const u32x4*>(x) + wave * 64;
+        const u32x4 d = __builtin_nontemporal_load(src + lane);
+        u32x4* dst = reinterpret_cast<u32x4*>(y) + wave * 128 + 2 * lane;
+        st16<POL>(dst, widen_lo(u32x2{d.x, d.y}));
+        st16<POL>(dst + 1, widen_lo(u32x2{d.z, d.w}));
+    } else {
+        __shared__ u32x4 sb[BLOCK / 64][64];
+        const u32x4* src = reinterpret_cast<const u32x4*>(x) + wave * 64;
+        sb[w][lane] = __builtin_nontemporal_load(src + lane);
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        const u32x2* s2 = reinterpret_cast<const u32x2*>(&sb[w][0]);
+        u32x4* dst = reinterpret_cast<u32x4*>(y) + wave * 128;
+        st16<POL>(dst + lane, widen_lo(s2[lane]));
+        st16<POL>(dst + 64 + lane, widen_lo(s2[64 + lane]));
+    }
+}
+
+template <int P, int R, int POL, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void write_pat(int32_t* __restrict__ y) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
+    u32x4* dst = reinterpret_cast<u32x4*>(y) + wave * (64 * R);
+    constexpr int G = P == 0 ? 1 : (P == 1 ? 2 : 4);  // contiguous 16-B pieces per lane
+#pragma unroll
+    for (int k = 0; k < R / G; ++k)
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+            st16<POL>(dst + k * 64 * G + lane * G + g, u32x4{(uint32_t)lane, (uint32_t)k, (uint32_t)g, 1u});
+}
+
+// ---------------------------------------------------------------------------------------
+struct Bufs {
+    int16_t* x;
+    int32_t* y;
+    int64_t n;
+};
+
+struct V {
+    std::string name;
+    void (*fn)(const Bufs&, hipStream_t);
+    double bytes;   // per launch
+    bool widen;     // output checkable
+    std::vector<float> us;
+};
+
+template <int K, int BLOCK>
+void l_widen_reg(const Bufs& b, hipStream_t s) {
+    hipLaunchKernelGGL((widen_reg<K, BLOCK>), dim3((unsigned)(b.n / (512 * K) / (BLOCK / 64))), dim3(BLOCK), 0, s,
+                       b.x, b.y);
+}
+template <int K, int BLOCK, bool NT>
+void l_widen_glds(const Bufs& b, hipStream_t s) {
+    hipLaunchKernelGGL((widen_glds<K, BLOCK, NT>), dim3((unsigned)(b.n / (512 * K) / (BLOCK / 64))), dim3(BLOCK), 0,
+                       s, b.x, b.y);
+}
+template <int K, int BLOCK>
+void l_read_reg(const Bufs& b, hipStream_t s) {
+    hipLaunchKernelGGL((read_reg<K, BLOCK>), dim3((unsigned)(b.n / (512 * K) / (BLOCK / 64))), dim3(BLOCK), 0, s, b.x,
+                       b.y);
+}
+template <int K, int BLOCK, bool NT>
+void l_read_glds(const Bufs& b, hipStream_t s) {
+    hipLaunchKernelGGL((read_glds<K, BLOCK, NT>), dim3((unsigned)(b.n / (512 * K) / (BLOCK / 64))), dim3(BLOCK), 0,
+                       s, b.x, b.y);
+}
+template <int K, int BLOCK>
+void l_write(const Bufs& b, hipStream_t s) {
+    hipLaunchKernelGGL((write_nt<K, BLOCK>), dim3((unsigned)(b.n / (256 * K) / (BLOCK / 64))), dim3(BLOCK), 0, s,
+                       b.y);
+}
+
+template <int P, int R, int POL, int BLOCK>
+void l_wpat(const Bufs& b, hipStream_t s) {
+    hipLaunchKernelGGL((write_pat<P, R, POL, BLOCK>), dim3((unsigned)(b.n / (256 * R) / (BLOCK / 64))), dim3(BLOCK),
+                       0, s, b.y);
+}
+
+template <int H, int P, int POL, int BLOCK>
+void l_wdpat(const Bufs& b, hipStream_t s) {
+    hipLaunchKernelGGL((widen_pat<H, P, POL, BLOCK>), dim3((unsigned)(b.n / (H ? 256 : 512) / (BLOCK / 64))),
+                       dim3(BLOCK), 0, s, b.x, b.y);
+}
+
+int main(int argc, char** argv) {
+    const int rounds = argc > 1 ? atoi(argv[1]) : 15;
+    Bufs b;
+    b.n = (int64_t)1 << 28;
+    CK(hipMalloc(&b.x, b.n * 2));
+    CK(hipMalloc(&b.y, b.n * 4));
+    std::vector<int16_t> hx(b.n);
+    uint32_t r = 12345;
+    for (auto& v : hx) {
+        r = r * 1664525u + 1013904223u;
+        v = (int16_t)(r >> 16);
+    }
+    CK(hipMemcpy(b.x, hx.data(), b.n * 2, hipMemcpyHostToDevice));
+    hipStream_t st;
+    CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    const double rw = b.n * 6.0, rd = b.n * 2.0, wr = b.n * 4.0;
+    std::vector<V> vs = {
+        {"widen reg K1 b256", l_widen_reg<1, 256>, rw, true, {}},
+        {"widen reg K2 b256", l_widen_reg<2, 256>, rw, true, {}},
+        {"widen half row nt", l_wdpat<1, 0, 1, 256>, rw, true, {}},
+        {"widen half row plain", l_wdpat<1, 0, 0, 256>, rw, true, {}},
+        {"widen half row sc0sc1", l_wdpat<1, 0, 2, 256>, rw, true, {}},
+        {"widen lane32 plain", l_wdpat<0, 1, 0, 256>, rw, true, {}},
+        {"widen lane32 sc0sc1", l_wdpat<0, 1, 2, 256>, rw, true, {}},
+        {"widen rows nt", l_wdpat<0, 0, 1, 256>, rw, true, {}},
+        {"widen rows plain", l_wdpat<0, 0, 0, 256>, rw, true, {}},
+        {"widen rows sc0sc1", l_wdpat<0, 0, 2, 256>, rw, true, {}},
+        {"widen rows sc1", l_wdpat<0, 0, 3, 256>, rw, true, {}},
+        {"widen reg K1 b512", l_widen_reg<1, 512>, rw, true, {}},
+        {"widen glds K1 b256", l_widen_glds<1, 256, false>, rw, true, {}},
+        {"widen glds K1 b256 nt", l_widen_glds<1, 256, true>, rw, true, {}},
+
+        {"read reg K1 b256", l_read_reg<1, 256>, rd, false, {}},
+
+        {"read glds K1 b256", l_read_glds<1, 256, false>, rd, false, {}},
+        {"read glds K1 b256 nt", l_read_glds<1, 256, true>, rd, false, {}},
+
+        {"write nt K2 b256", l_write<2, 256>, wr, false, {}},
+        {"write nt K8 b256", l_write<8, 256>, wr, false, {}},
+        {"wpat rows R2 plain", l_wpat<0, 2, 0, 256>, wr, false, {}},
+        {"wpat rows R2 nt", l_wpat<0, 2, 1, 256>, wr, false, {}},
+        {"wpat rows R2 sc0sc1", l_wpat<0, 2, 2, 256>, wr, false, {}},
+        {"wpat rows R2 sc1", l_wpat<0, 2, 3, 256>, wr, false, {}},
+        {"wpat rows R4 plain", l_wpat<0, 4, 0, 256>, wr, false, {}},
+        {"wpat rows R1 nt", l_wpat<0, 1, 1, 256>, wr, false, {}},
+        {"wpat rows R2 nt b1024", l_wpat<0, 2, 1, 1024>, wr, false, {}},
+        {"wpat rows R2 nt b64", l_wpat<0, 2, 1, 64>, wr, false, {}},
+        {"wpat lane32 R2 plain", l_wpat<1, 2, 0, 256>, wr, false, {}},
+        {"wpat lane32 R2 nt", l_wpat<1, 2, 1, 256>, wr, false, {}},
+        {"wpat lane32 R4 plain", l_wpat<1, 4, 0, 256>, wr, false, {}},
+        {"wpat rows R1 plain", l_wpat<0, 1, 0, 256>, wr, false, {}},
+        {"wpat rows R1 sc0sc1", l_wpat<0, 1, 2, 256>, wr, false, {}},
+    };
+    // correctness of every widen variant (sampled)
+    std::vector<int32_t> hy(b.n);
+    for (auto& v : vs) {
+        if (!v.widen) continue;
+        CK(hipMemset(b.y, 0xA5, b.n * 4));
+        v.fn(b, st);
+        CK(hipStreamSynchronize(st));
+        CK(hipMemcpy(hy.data(), b.y, b.n * 4, hipMemcpyDeviceToHost));
+        int64_t nbad = 0, nunw = 0, first = -1;
+        for (int64_t i = 0; i < b.n; ++i)
+            if (hy[i] != (int32_t)hx[i]) {
+                if (first < 0) first = i;
+                ++nbad;
+                nunw += hy[i] == (int32_t)0xA5A5A5A5;
+            }
+        if (nbad) {
+            printf("MISMATCH %-24s %lld wrong (%lld never written), first at %lld (tile %lld): %d != %d\n",
+                   v.name.c_str(), (long long)nbad, (long long)nunw, (long long)first, (long long)(first / 512),
+                   hy[first], (int)hx[first]);
+            v.widen = false;
+            v.name += " [WRONG]";
+        }
+    }
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int w = 0; w < 100; ++w) vs[w % vs.size()].fn(b, st);
+    const int batch = 20;
+    for (int rr = 0; rr < rounds; ++rr)
+        for (auto& v : vs) {
+            CK(hipEventRecord(e0, st));
+            for (int i = 0; i < batch; ++i) v.fn(b, st);
+            CK(hipEventRecord(e1, st));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            v.us.push_back(ms * 1e3f / batch);
+        }
+    printf("%-26s %10s %10s %10s %8s\n", "variant", "median_us", "min_us", "GB/s", "%8TB/s");
+    for (auto& v : vs) {
+        std::sort(v.us.begin(), v.us.end());
+        const double med = v.us[v.us.size() / 2];
+        printf("%-26s %10.1f %10.1f %10.1f %8.1f\n", v.name.c_str(), med, v.us[0], v.bytes / med / 1e3,
+               v.bytes / med / 1e3 / 80.0);
+    }
+    return 0;
+}
