@@ -16,7 +16,18 @@
 
 namespace fir {
 
-constexpr int kMetricBlocks = 4096;
+// 2048 blocks (8192 waves, 32 per CU) over 4096: 359 -> 356 / 369 -> 362 us in two same-process
+// A/Bs; 1024 blocks, 8 or 4 loads per tile, the next tile's loads issued before the arithmetic
+// (+3-5 %), and the fixed bytes as whole rows through LDS gained nothing
+// (profiles/r02/ab_restore_metrics.txt).  FIR_METRIC_*: A/B builds only.
+#ifndef FIR_METRIC_BLOCKS
+#define FIR_METRIC_BLOCKS 2048
+#endif
+#ifndef FIR_METRIC_LOADS
+#define FIR_METRIC_LOADS 16
+#endif
+
+constexpr int kMetricBlocks = FIR_METRIC_BLOCKS;
 
 struct Part {
     double sabs, cabs, ssq, csq, sd, cd, mx;
@@ -73,7 +84,7 @@ __device__ __forceinline__ void metrics_term(double id, uint32_t fx, double& sab
 // a tile plainly and adds the tile partials into its Neumaier-compensated accumulators
 // (a compensated add per sample made the kernel latency-bound).  The ragged tail and
 // unaligned inputs take the per-sample grid-stride loop.
-constexpr int kMetricLoads = 16;
+constexpr int kMetricLoads = FIR_METRIC_LOADS;
 constexpr int kMetricTile = kMetricLoads * kWave * 2;
 
 template <bool VEC>
@@ -89,16 +100,16 @@ __global__ __launch_bounds__(kBlock) void metrics_pass1(const double* __restrict
         const int lane = threadIdx.x & (kWave - 1);
         const int64_t ntile = n / kMetricTile;
         const int64_t nwaves = (int64_t)gridDim.x * (kBlock / kWave);
-        for (int64_t t = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6); t < ntile; t += nwaves) {
+        auto load_tile = [&](int64_t t, d2 (&a)[kMetricLoads], uint32_t (&f)[kMetricLoads]) {
             const d2* pi = reinterpret_cast<const d2*>(ideal + t * kMetricTile);
             const uint16_t* pf = reinterpret_cast<const uint16_t*>(fixed + t * kMetricTile);
-            d2 a[kMetricLoads];
-            uint32_t f[kMetricLoads];
 #pragma unroll
             for (int i = 0; i < kMetricLoads; ++i) {
                 a[i] = __builtin_nontemporal_load(pi + i * kWave + lane);
                 f[i] = __builtin_nontemporal_load(pf + i * kWave + lane);
             }
+        };
+        auto tile_sums = [&](const d2 (&a)[kMetricLoads], const uint32_t (&f)[kMetricLoads]) {
             double sabs = 0.0, ssq = 0.0, sd = 0.0;
 #pragma unroll
             for (int i = 0; i < kMetricLoads; ++i) {
@@ -108,6 +119,12 @@ __global__ __launch_bounds__(kBlock) void metrics_pass1(const double* __restrict
             neu_add(p.sabs, p.cabs, sabs);
             neu_add(p.ssq, p.csq, ssq);
             neu_add(p.sd, p.cd, sd);
+        };
+        for (int64_t t = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6); t < ntile; t += nwaves) {
+            d2 a[kMetricLoads];
+            uint32_t f[kMetricLoads];
+            load_tile(t, a, f);
+            tile_sums(a, f);
         }
         start = ntile * kMetricTile;
     }

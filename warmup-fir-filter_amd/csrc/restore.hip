@@ -9,9 +9,9 @@
 // product are rounded separately as in NumPy (-ffp-contract=off); the scale 255/(hi-lo)
 // is formed once on the device.  NaN maps to 0 (NumPy's cast of NaN is unspecified).
 //
-// HBM layout: a wave converts 2048 consecutive doubles with whole-wave 1 KiB non-temporal
-// loads (lane-interleaved 16-byte pairs, 16 in flight per lane), then transposes its 2048
-// result bytes through LDS so every store instruction writes 1 KiB contiguous.  normalize adds a
+// HBM layout: a wave converts 128*K consecutive doubles with whole-wave 1 KiB non-temporal
+// loads (lane-interleaved 16-byte pairs, K = 2 per lane), then transposes its result bytes
+// through LDS so every store instruction writes one contiguous row.  normalize adds a
 // min/max pass (grid-stride, per-block tree, one final block) ahead of the same map.
 #include <algorithm>
 #include <string>
@@ -22,10 +22,19 @@
 namespace fir {
 
 constexpr int kRestoreBlocks = 1024;
-// 16 non-temporal 16-byte loads in flight per lane (2048 doubles per wave): the read-stream
-// A/B (tools/microbench/read_micro.hip) reads 2 GiB in 364 us this way vs 416 us with 8
-// default-policy loads.
-constexpr int kRestoreLoads = 16;
+// 2 non-temporal 16-byte loads per lane (256 doubles, 256 result bytes per wave): many short
+// waves keep more of the read stream in flight than few long ones.  Same-process A/B over
+// 2^28 doubles (profiles/r02/ab_restore_metrics.txt): 16 loads 372-397 us, 8: 366, 4: 361-376,
+// 2: 354-363, 1: 389; the 2 GiB read-only ceiling is 301 us at 1-2 loads per lane
+// (profiles/r02/read_ceiling_2gib.txt).  FIR_RESTORE_*: A/B builds only.
+#ifndef FIR_RESTORE_LOADS
+#define FIR_RESTORE_LOADS 2
+#endif
+#ifndef FIR_RESTORE_NTSTORE
+#define FIR_RESTORE_NTSTORE 0
+#endif
+constexpr int kRestoreLoads = FIR_RESTORE_LOADS;
+static_assert(kRestoreLoads <= 4 || kRestoreLoads % 8 == 0, "restore loads per lane");
 constexpr int kRestorePerWave = 2 * kWave * kRestoreLoads;
 
 struct RestoreParams {
@@ -69,9 +78,23 @@ __global__ __launch_bounds__(kBlock) void restore_map_kernel(const double* __res
             wb[i * kWave + lane] = (uint16_t)(conv(v[i].x, NORM, p) | (conv(v[i].y, NORM, p) << 8));
         __builtin_amdgcn_wave_barrier();  // one wave's LDS ops complete in order
         asm volatile("" ::: "memory");
+        // the wave's 128*K result bytes as whole rows: 16 (K >= 8), 8, 4 or 2 (K = 4, 2, 1) bytes per lane
+        if constexpr (K >= 8) {
 #pragma unroll
-        for (int i = 0; i < K / 8; ++i)  // plain stores: non-temporal ones measured 394 -> 415 us
-            reinterpret_cast<u32x4*>(out + base)[i * kWave + lane] = reinterpret_cast<const u32x4*>(wb)[i * kWave + lane];
+            for (int i = 0; i < K / 8; ++i) {  // plain stores: non-temporal ones measured 394 -> 415 us
+                u32x4* dst = reinterpret_cast<u32x4*>(out + base) + i * kWave + lane;
+                const u32x4 val = reinterpret_cast<const u32x4*>(wb)[i * kWave + lane];
+                if constexpr (FIR_RESTORE_NTSTORE) __builtin_nontemporal_store(val, dst); else *dst = val;
+            }
+        } else if constexpr (K == 4) {
+            typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+            reinterpret_cast<u32x2*>(out + base)[lane] = reinterpret_cast<const u32x2*>(wb)[lane];
+        } else if constexpr (K == 2) {
+            reinterpret_cast<uint32_t*>(out + base)[lane] = reinterpret_cast<const uint32_t*>(wb)[lane];
+        } else {
+            static_assert(K == 1, "restore loads per lane");
+            reinterpret_cast<uint16_t*>(out + base)[lane] = wb[lane];
+        }
     } else {
         for (int64_t e = base + lane; e < n; e += kWave) out[e] = (uint8_t)conv(a[e], NORM, p);
     }
