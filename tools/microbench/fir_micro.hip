@@ -147,6 +147,48 @@ static void launch_copy_policy(const int16_t* x, int32_t* y, int64_t n, hipStrea
                        x, y, nvec);
 }
 
+static const int32_t kTaps[5] = {-256, -1024, 6656, -1024, -256};
+
+// Lean single-row int16 -> int32 kernel (acc_bits 32, int16 taps on v_dot2): a lane owns 4
+// samples (8 B), a wave 256 samples, ONE 1 KiB store row per wave straight from registers; the
+// two edge dwords come from one branch-free 4-byte load (lane 0: the dword before the wave,
+// lane 63: the dword after it, other lanes re-read their own first dword, unused).  Needs
+// whole waves: nvec % 64 == 0.
+template <int L, bool NTS>
+__global__ __launch_bounds__(kBlock) void fir1d_i16_lean(const int16_t* __restrict__ x, int32_t* __restrict__ y,
+                                                         int64_t nvec, TapsN<L> taps, int frac) {
+    constexpr int HLE = L - 1 - L / 2, HRE = L / 2;
+    static_assert(HLE <= 2 && HRE <= 2, "halo of one dword per side");
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (v >= nvec) return;  // wave-uniform
+    const u32x2 d = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(x) + v);
+    const int64_t ei = lane == 0 ? 2 * v - 1 : (lane == kWave - 1 ? 2 * v + 2 : 2 * v);
+    const bool eok = ei >= 0 && ei < 2 * nvec;
+    const uint32_t ev = reinterpret_cast<const uint32_t*>(x)[eok ? ei : 2 * v];
+    const uint32_t e = eok ? ev : 0u;
+    uint32_t Wd[4];
+    Wd[0] = from_prev_lane(e, d.y);
+    Wd[1] = d.x;
+    Wd[2] = d.y;
+    Wd[3] = from_next_lane(e, d.x);
+    int32_t q[4];
+    Dot2Vec<1, 4, L, 0, 4, true>::run(Wd, taps.pk[0], 0, frac, q);
+    u32x4* dst = reinterpret_cast<u32x4*>(y) + v;
+    const u32x4 val = {(uint32_t)q[0], (uint32_t)q[1], (uint32_t)q[2], (uint32_t)q[3]};
+    if constexpr (NTS) store16_nt(dst, val); else *dst = val;
+}
+
+template <bool NTS>
+static void launch_lean(const int16_t* x, int32_t* y, int64_t n, hipStream_t s, int) {
+    TapsN<5> t;
+    for (int k = 0; k < 5; ++k) t.h[0][k] = kTaps[k];
+    pack_taps(t);
+    const int64_t nvec = n / 4;
+    hipLaunchKernelGGL((fir1d_i16_lean<5, NTS>), dim3((unsigned)((nvec + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, x,
+                       y, nvec, t, 12);
+}
+
 struct Variant {
     std::string name;
     bool is_fir;
@@ -154,8 +196,6 @@ struct Variant {
     int blocks_arg;
     std::vector<float> us;
 };
-
-static const int32_t kTaps[5] = {-256, -1024, 6656, -1024, -256};
 
 template <int U, int FLAGS>
 static void launch_fir(const int16_t* x, int32_t* y, int64_t n, hipStream_t s, int pblocks) {
@@ -220,18 +260,11 @@ int main(int argc, char** argv) {
     CK(hipStreamCreate(&st));
 
     std::vector<Variant> vs = {
-        {"fir U1 dot2 acc32 coal", true, launch_fir<1, kDot2 | kAcc32 | kCoal>, 0, {}},
-        {"fir U1 coal ntst", true, launch_fir<1, kDot2 | kAcc32 | kCoal | kNtStore>, 0, {}},
-        {"fir U2 coal ntst", true, launch_fir<2, kDot2 | kAcc32 | kCoal | kNtStore>, 0, {}},
-        {"fir U1 coal ntld+st", true, launch_fir<1, kDot2 | kAcc32 | kCoal | kNtLoad | kNtStore>, 0, {}},
-        {"fir U1 coal ntld", true, launch_fir<1, kDot2 | kAcc32 | kCoal | kNtLoad>, 0, {}},
-        {"fir U2 coal ntld", true, launch_fir<2, kDot2 | kAcc32 | kCoal | kNtLoad>, 0, {}},
-        {"fir U4 coal ntld", true, launch_fir<4, kDot2 | kAcc32 | kCoal | kNtLoad>, 0, {}},
-        {"fir U2 dot2 acc32 coal", true, launch_fir<2, kDot2 | kAcc32 | kCoal>, 0, {}},
-        {"fir U4 dot2 acc32 coal", true, launch_fir<4, kDot2 | kAcc32 | kCoal>, 0, {}},
-        {"copy U1 plain", false, launch_copy<1, 0>, 0, {}},
+        {"fir U1 coal ntst (lib)", true, launch_fir<1, kDot2 | kAcc32 | kCoal | kNtStore>, 0, {}},
+        {"lean ntst", true, launch_lean<true>, 0, {}},
+        {"lean plain st", true, launch_lean<false>, 0, {}},
+        {"fir U1 coal ntst (lib) b", true, launch_fir<1, kDot2 | kAcc32 | kCoal | kNtStore>, 0, {}},
         {"copy U1 coal (LDS)", false, launch_copy_coal, 0, {}},
-        {"copy split U1", false, launch_copy_split<1>, 0, {}},
     };
 
     // correctness (FIR variants): sampled positions + both ends
