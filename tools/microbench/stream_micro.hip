@@ -159,6 +159,47 @@ __global__ __launch_bounds__(BLOCK) void widen_pat(const int16_t* __restrict__ x
     }
 }
 
+// widen_pat H=1 plus what the FIR adds per wave: E=1 one more 4-byte load per lane (branch-free,
+// lanes 0/63 the dwords around the wave, the rest their own), E=2 that plus the two DPP moves,
+// E=3 the halo through LDS instead: each wave publishes its edge dwords, one block barrier,
+// lanes 0/63 read the neighbours' (block edges load from memory).
+template <int E>
+__global__ __launch_bounds__(256) void widen_half_edge(const int16_t* __restrict__ x, int32_t* __restrict__ y,
+                                                       int64_t nvec) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const u32x2 d = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(x) + v);
+    uint32_t e = 0;
+    if constexpr (E == 1 || E == 2) {
+        const int64_t ei = lane == 0 ? 2 * v - 1 : (lane == 63 ? 2 * v + 2 : 2 * v);
+        const bool ok = ei >= 0 && ei < 2 * nvec;
+        const uint32_t ev = reinterpret_cast<const uint32_t*>(x)[ok ? ei : 2 * v];
+        e = ok ? ev : 0u;
+    } else if constexpr (E == 3) {
+        __shared__ uint32_t edge[4][2];
+        if (lane == 0) edge[w][0] = d.x;
+        if (lane == 63) edge[w][1] = d.y;
+        uint32_t ev = 0;
+        const bool outer = (lane == 0 && w == 0) || (lane == 63 && w == 3);
+        if (outer) {
+            const int64_t ei = lane == 0 ? 2 * v - 1 : 2 * v + 2;
+            if (ei >= 0 && ei < 2 * nvec) ev = reinterpret_cast<const uint32_t*>(x)[ei];
+        }
+        __syncthreads();
+        if (!outer) ev = lane == 0 ? edge[w - 1][1] : (lane == 63 ? edge[w + 1][0] : 0u);
+        e = ev;
+    }
+    uint32_t a = d.x, b = d.y;
+    if constexpr (E >= 2) {
+        a ^= (uint32_t)__builtin_amdgcn_update_dpp((int)e, (int)d.y, 0x138, 0xF, 0xF, false) & 0x80000000u;
+        b ^= (uint32_t)__builtin_amdgcn_update_dpp((int)e, (int)d.x, 0x130, 0xF, 0xF, false) & 0x80000000u;
+    } else {
+        a ^= e & 0x80000000u & (uint32_t)(lane == 64);
+    }
+    (void)a;
+    st16<1>(reinterpret_cast<u32x4*>(y) + v, widen_lo(u32x2{E >= 2 ? a ^ (a & 0x80000000u) ^ (d.x & 0x80000000u) : d.x, E >= 2 ? b ^ (b & 0x80000000u) ^ (d.y & 0x80000000u) : d.y}));
+}
+
 template <int P, int R, int POL, int BLOCK>
 __global__ __launch_bounds__(BLOCK) void write_pat(int32_t* __restrict__ y) {
     const int lane = threadIdx.x & 63;
@@ -225,6 +266,11 @@ void l_wdpat(const Bufs& b, hipStream_t s) {
                        dim3(BLOCK), 0, s, b.x, b.y);
 }
 
+template <int E>
+void l_whe(const Bufs& b, hipStream_t s) {
+    hipLaunchKernelGGL((widen_half_edge<E>), dim3((unsigned)(b.n / 4 / 256)), dim3(256), 0, s, b.x, b.y, b.n / 4);
+}
+
 int main(int argc, char** argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 15;
     Bufs b;
@@ -243,40 +289,12 @@ int main(int argc, char** argv) {
     const double rw = b.n * 6.0, rd = b.n * 2.0, wr = b.n * 4.0;
     std::vector<V> vs = {
         {"widen reg K1 b256", l_widen_reg<1, 256>, rw, true, {}},
-        {"widen reg K2 b256", l_widen_reg<2, 256>, rw, true, {}},
         {"widen half row nt", l_wdpat<1, 0, 1, 256>, rw, true, {}},
-        {"widen half row plain", l_wdpat<1, 0, 0, 256>, rw, true, {}},
-        {"widen half row sc0sc1", l_wdpat<1, 0, 2, 256>, rw, true, {}},
-        {"widen lane32 plain", l_wdpat<0, 1, 0, 256>, rw, true, {}},
-        {"widen lane32 sc0sc1", l_wdpat<0, 1, 2, 256>, rw, true, {}},
+        {"half + edge load", l_whe<1>, rw, true, {}},
+        {"half + edge load + dpp", l_whe<2>, rw, true, {}},
+        {"half + LDS halo", l_whe<3>, rw, true, {}},
+        {"half + no edge", l_whe<0>, rw, true, {}},
         {"widen rows nt", l_wdpat<0, 0, 1, 256>, rw, true, {}},
-        {"widen rows plain", l_wdpat<0, 0, 0, 256>, rw, true, {}},
-        {"widen rows sc0sc1", l_wdpat<0, 0, 2, 256>, rw, true, {}},
-        {"widen rows sc1", l_wdpat<0, 0, 3, 256>, rw, true, {}},
-        {"widen reg K1 b512", l_widen_reg<1, 512>, rw, true, {}},
-        {"widen glds K1 b256", l_widen_glds<1, 256, false>, rw, true, {}},
-        {"widen glds K1 b256 nt", l_widen_glds<1, 256, true>, rw, true, {}},
-
-        {"read reg K1 b256", l_read_reg<1, 256>, rd, false, {}},
-
-        {"read glds K1 b256", l_read_glds<1, 256, false>, rd, false, {}},
-        {"read glds K1 b256 nt", l_read_glds<1, 256, true>, rd, false, {}},
-
-        {"write nt K2 b256", l_write<2, 256>, wr, false, {}},
-        {"write nt K8 b256", l_write<8, 256>, wr, false, {}},
-        {"wpat rows R2 plain", l_wpat<0, 2, 0, 256>, wr, false, {}},
-        {"wpat rows R2 nt", l_wpat<0, 2, 1, 256>, wr, false, {}},
-        {"wpat rows R2 sc0sc1", l_wpat<0, 2, 2, 256>, wr, false, {}},
-        {"wpat rows R2 sc1", l_wpat<0, 2, 3, 256>, wr, false, {}},
-        {"wpat rows R4 plain", l_wpat<0, 4, 0, 256>, wr, false, {}},
-        {"wpat rows R1 nt", l_wpat<0, 1, 1, 256>, wr, false, {}},
-        {"wpat rows R2 nt b1024", l_wpat<0, 2, 1, 1024>, wr, false, {}},
-        {"wpat rows R2 nt b64", l_wpat<0, 2, 1, 64>, wr, false, {}},
-        {"wpat lane32 R2 plain", l_wpat<1, 2, 0, 256>, wr, false, {}},
-        {"wpat lane32 R2 nt", l_wpat<1, 2, 1, 256>, wr, false, {}},
-        {"wpat lane32 R4 plain", l_wpat<1, 4, 0, 256>, wr, false, {}},
-        {"wpat rows R1 plain", l_wpat<0, 1, 0, 256>, wr, false, {}},
-        {"wpat rows R1 sc0sc1", l_wpat<0, 1, 2, 256>, wr, false, {}},
     };
     // correctness of every widen variant (sampled)
     std::vector<int32_t> hy(b.n);
