@@ -91,14 +91,14 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(dx, hx.data(), total, hipMemcpyHostToDevice));
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    std::vector<V> vs = {{"NV1", launch<1, false>, {}}, {"NV1 coal", launch<1, true>, {}},
-                         {"NV2 coal", launch<2, true>, {}}, {"NV4 coal", launch<4, true>, {}},
-                         {"NV2 coal ntst", launch<2, true, false, true>, {}},
-                         {"NV4 coal ntst", launch<4, true, false, true>, {}},
-                         {"NV2 coal ntld+st", launch<2, true, true, true>, {}},
+    std::vector<V> vs = {{"NV2 coal ntst (lib)", launch<2, true, false, true>, {}},
+                         {"NV1 coal ntst", launch<1, true, false, true>, {}},
+                         {"NV1 coal ntld+st", launch<1, true, true, true>, {}},
+                         {"NV1 coal", launch<1, true>, {}},
+                         {"NV2 coal ntst (lib) b", launch<2, true, false, true>, {}},
                          {"store-only strided", launch_store<false>, {}},
                          {"store-only coal", launch_store<true>, {}}};
-    const size_t nchecked = 4;
+    const size_t nchecked = 5;
     for (size_t vi = 0; vi < nchecked; ++vi) {
         auto& v = vs[vi];
         CK(hipMemset(dy, 0xFF, total * 8));

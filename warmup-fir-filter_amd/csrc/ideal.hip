@@ -55,8 +55,11 @@ __global__ __launch_bounds__(kBlock) void fir1d_ideal_kernel(const uint8_t* __re
     }
 }
 
-constexpr int kIdealNV = 2;  // dwords (x4 u8 samples) per lane; NV2 + LDS-coalesced stores won the A/B,
-                             // their whole-row stores non-temporal: 394.5 -> 352.5 us (micro_ideal_nts.txt)
+// dwords (x4 u8 samples) per lane, outputs through LDS as whole 1 KiB non-temporal rows
+// (394.5 -> 352.5 us, profiles/r01/micro_ideal_nts.txt).  One dword per lane (a wave: 256 B in,
+// 2 KiB out) beats two (512 B in, 4 KiB out): 347.6 -> 337.6 us (profiles/r02/micro_ideal_nv1.txt);
+// short waves keep more of the store stream in flight.
+constexpr int kIdealNV = 1;
 
 template <int L>
 static hipError_t launch_ideal_reg(const uint8_t* x, double* y, int64_t rows, int64_t width, const double* h,
