@@ -121,30 +121,14 @@ int main(int argc, char** argv) {
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     constexpr int PK = kU8Dot2 | kU8Pk16;
-    std::vector<V> vs = {{"fir U1", 1, launch_fir<1, kU8Dot2>, {}},
-                         {"fir U2", 1, launch_fir<2, kU8Dot2>, {}},
-                         {"fir U4", 1, launch_fir<4, kU8Dot2>, {}},
-                         {"pk16 U1", 1, launch_fir<1, PK>, {}},
-                         {"pk16 U2", 1, launch_fir<2, PK>, {}},
-                         {"pk16 U4", 1, launch_fir<4, PK>, {}},
-                         {"fir U4 ntld", 1, launch_fir<4, kU8Dot2 | kNtLoad>, {}},
-                         {"fir U2 ntld", 1, launch_fir<2, kU8Dot2 | kNtLoad>, {}},
-                         {"fir U4 xcd", 1, launch_fir<4, kU8Dot2 | kXcd>, {}},
-                         {"fir U8", 1, launch_fir<8, kU8Dot2>, {}},
-                         {"fir U4 ntld+st", 1, launch_fir<4, kU8Dot2 | kNtLoad | kNtStore>, {}},
-                         {"fir U4 ntst", 1, launch_fir<4, kU8Dot2 | kNtStore>, {}},
-                         {"bank pk16 U2 ntst", 2, launch_bank<2, PK | kNtStore>, {}},
-                         {"bank pk16 U1 ntst", 2, launch_bank<1, PK | kNtStore>, {}},
-                         {"bank pk16 U2 ntld", 2, launch_bank<2, PK | kNtLoad>, {}},
-                         {"bank pk16 U4 ntld", 2, launch_bank<4, PK | kNtLoad>, {}},
-                         {"bank pk16 U1 ntld", 2, launch_bank<1, PK | kNtLoad>, {}},
-                         {"bank dot2 U1", 2, launch_bank<1, kU8Dot2>, {}},
-                         {"bank dot2 U2", 2, launch_bank<2, kU8Dot2>, {}},
-                         {"bank pk16 U1", 2, launch_bank<1, PK>, {}},
-                         {"bank pk16 U2", 2, launch_bank<2, PK>, {}},
+    std::vector<V> vs = {{"fir U4 ntst (lib)", 1, launch_fir<4, kU8Dot2 | kNtStore>, {}},
+                         {"fir U1 ntst", 1, launch_fir<1, kU8Dot2 | kNtStore>, {}},
+                         {"fir U2 ntst", 1, launch_fir<2, kU8Dot2 | kNtStore>, {}},
+                         {"fir U1 ntld+st", 1, launch_fir<1, kU8Dot2 | kNtLoad | kNtStore>, {}},
+                         {"fir U4 ntst (lib) b", 1, launch_fir<4, kU8Dot2 | kNtStore>, {}},
+                         {"bank pk16 U1 ntst (lib)", 2, launch_bank<1, PK | kNtStore>, {}},
+                         {"bank pk16 U1 ntld+st", 2, launch_bank<1, PK | kNtLoad | kNtStore>, {}},
                          {"copy16 U1", 0, launch_copy<1>, {}},
-                         {"copy16 U2", 0, launch_copy<2>, {}},
-                         {"copy16 U4", 0, launch_copy<4>, {}},
                          {"hipMemcpy D2D", 0, launch_memcpy, {}}};
     for (auto& v : vs) {
         if (v.kind == 0) continue;
