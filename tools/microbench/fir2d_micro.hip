@@ -120,13 +120,15 @@ int main(int argc, char** argv) {
     hipStream_t st;
     CK(hipStreamCreate(&st));
     std::vector<V> vs = {
-        {"pk16hi8 v16 s16 pd3", true, launch<16, 16, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 3>, {}},
-        {"pk16hi8 v16 s16 pd3 w6", true, launch<16, 16, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 6, 3>, {}},
-        {"pk16hi8 v16 s32 pd3", true, launch<16, 32, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 3>, {}},
-        {"pk16hi8 v16 s32 pd4", true, launch<16, 32, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 4>, {}},
-        {"pk16hi8 v16 s32 pd4 ntld", true, launch<16, 32, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 4, true>, {}},
-        {"pk16hi8 v16 s16 pd3 ntld", true, launch<16, 16, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 3, true>, {}},
-        {"pk16hi8 v8 s16 pd4", true, launch<8, 16, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 4>, {}},
+        {"pk16hi8 v16 s32 pd4 (lib)", true, launch<16, 32, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 4>, {}},
+        {"pk16hi8 v16 s32 pd6", true, launch<16, 32, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 6>, {}},
+        {"pk16hi8 v16 s32 pd8", true, launch<16, 32, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 8>, {}},
+        {"pk16hi8 v16 s32 pd12", true, launch<16, 32, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 12>, {}},
+        {"pk16hi8 v16 s16 pd6", true, launch<16, 16, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 6>, {}},
+        {"pk16hi8 v16 s16 pd8", true, launch<16, 16, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 8>, {}},
+        {"pk16hi8 v8 s32 pd8", true, launch<8, 32, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 8>, {}},
+        {"pk16hi8 v8 s16 pd8", true, launch<8, 16, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 8>, {}},
+        {"pk16hi8 v16 s32 pd4 (lib) b", true, launch<16, 32, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 4>, {}},
         {"copy2d v16 s16 pd3", false, launch_copy2d<16, 16, 3, true>, {}},
         {"copy2d v16 s16 pd3 nohalo", false, launch_copy2d<16, 16, 3, false>, {}},
         {"copy2d v16 s32 pd3", false, launch_copy2d<16, 32, 3, true>, {}},
