@@ -123,14 +123,22 @@ class Workload:
             self.gen2d = os.environ.get("FIR2D_TAPS") == "gen5x5"
             if self.gen2d:
                 self.hq2 = np.random.default_rng(55).integers(-4, 5, (5, 5)).astype(np.int64)
-            self.x_host = rng.integers(0, 256, (self.h, self.w), dtype=np.uint8)
+            # A step filters a batch of FIR2D_FRAMES distinct 8192x8192 frames in one launch
+            # (fir2d_fixed_frames_dev).  One frame (64 MiB in + 64 MiB out) fits the 256 MB
+            # Infinity Cache, so filtering the same frame step after step would be served partly
+            # from it (profiles/r02/micro2d_cold.txt: 23.6 us back to back vs 29.5 us cold); 4
+            # frames move 512 MiB per step, so every step streams from HBM, as a video pipeline
+            # would, and one launch per batch spares the per-launch ramp (29.7 -> 26.1 us/frame).
+            self.frames = max(1, _env_int("FIR2D_FRAMES", 4))
+            self.frames_host = rng.integers(0, 256, (self.frames, self.h, self.w), dtype=np.uint8)
+            self.x_host = self.frames_host[0]  # the CPU legs' NumPy restatement times frame 0
             self.bytes_per_unit = 1 + 1
-            self.units = self.h * self.w
+            self.units = self.frames * self.h * self.w
             self.unit = "Gpixels/s"
             self.dtype = "int32 (u8 in, int32 wrap-around acc, u8 saturated out)"
             self.config = {"workload": "fir2d_u8_5x5_" + ("nonseparable_signed_seed55" if self.gen2d else
                                                           "simple_lp_outer_q4.12"), "frame": [self.h, self.w],
-                           "parallelism": "single GPU (replicas when N > 1)"}
+                           "frames_per_step": self.frames, "parallelism": "single GPU (replicas when N > 1)"}
         elif name in ("ideal_u8", "bank_u8", "fir1d_u8"):
             self.n = 1 << log2n
             self.x_host = rng.integers(0, 256, (self.n // ROW_W, ROW_W), dtype=np.uint8)
@@ -176,18 +184,22 @@ class Workload:
                            "parallelism": "single GPU (replicas when N > 1)"}
         else:
             raise SystemExit(f"unknown workload {name}")
-        self.x = torch.from_numpy(self.x_host).to(dev)
-        if name == "ideal_u8":
-            self.y = torch.empty(self.x.shape, dtype=torch.float64, device=dev)
-        elif name == "bank_u8":
-            self.y = torch.empty((len(BANK3),) + tuple(self.x.shape), dtype=torch.uint8, device=dev)
-        elif name == "restore_u8":
+        if name == "fir2d_u8":  # the resident batch of frames
+            self.x = torch.from_numpy(self.frames_host).to(dev)
             self.y = torch.empty(self.x.shape, dtype=torch.uint8, device=dev)
-        elif name == "metrics_u8":
-            self.y = torch.empty(9, dtype=torch.float64, device=dev)
         else:
-            u8 = name in ("fir2d_u8", "fir1d_u8")
-            self.y = torch.empty(self.x.shape, dtype=torch.uint8 if u8 else torch.int32, device=dev)
+            self.x = torch.from_numpy(self.x_host).to(dev)
+            if name == "ideal_u8":
+                self.y = torch.empty(self.x.shape, dtype=torch.float64, device=dev)
+            elif name == "bank_u8":
+                self.y = torch.empty((len(BANK3),) + tuple(self.x.shape), dtype=torch.uint8, device=dev)
+            elif name == "restore_u8":
+                self.y = torch.empty(self.x.shape, dtype=torch.uint8, device=dev)
+            elif name == "metrics_u8":
+                self.y = torch.empty(9, dtype=torch.float64, device=dev)
+            else:
+                u8 = name == "fir1d_u8"
+                self.y = torch.empty(self.x.shape, dtype=torch.uint8 if u8 else torch.int32, device=dev)
         self.left = self.right = None  # the halos the last step used (host copies for the oracle)
         self.halo_src, self.halo_kind = None, None
 
@@ -257,7 +269,8 @@ class Workload:
         out = None
         for _ in range(reps):
             if self.name == "fir2d_u8":
-                out = co.fir2d(self.x_host, self.hq2, 12, 32, co.OUT_U8_SAT, nthreads=nthreads)
+                out = np.stack([co.fir2d(f, self.hq2, 12, 32, co.OUT_U8_SAT, nthreads=nthreads)
+                                for f in self.frames_host])
             elif self.name == "ideal_u8":
                 out = co.fir1d_ideal_rows(self.x_host, SHARPEN5_F64, nthreads=nthreads)
             elif self.name == "bank_u8":
@@ -443,8 +456,7 @@ def main() -> int:
     # parity: full output vs the C oracle (every rank, its own segment with the received halos)
     parity = "skipped"
     if not args.no_parity:
-        ref = wl.oracle(_cpu_threads())
-        ok = wl.matches(ref)
+        ok = wl.matches(wl.oracle(_cpu_threads()))
         if world > 1:
             f = torch.tensor([0 if ok else 1], device=red_dev)
             dist.all_reduce(f, op=dist.ReduceOp.MAX)

@@ -133,6 +133,16 @@ int fir2d_fixed(const uint8_t* x, int64_t height, int64_t width, const int32_t* 
 int fir2d_fixed_dev(const uint8_t* x_dev, int64_t height, int64_t width, const int32_t* hq,
                     int tap_rows, int tap_cols, int frac_bits, int acc_bits, int out_stage,
                     void* y_dev, void* stream);
+/* A batch of `frames` (<= 65535) frames of height x width stored back to back, each filtered
+ * on its own (zero padding at every frame edge), in ONE launch: identical to `frames` calls of
+ * the single-frame entries.  A launch per 8192^2 frame leaves the chip idle at its start and end;
+ * a batch of 4 such frames streams from HBM 12 % faster per frame (profiles/r02). */
+int fir2d_fixed_frames(const uint8_t* x, int64_t frames, int64_t height, int64_t width, const int32_t* hq,
+                       int tap_rows, int tap_cols, int frac_bits, int acc_bits, int out_stage, void* y,
+                       int device);
+int fir2d_fixed_frames_dev(const uint8_t* x_dev, int64_t frames, int64_t height, int64_t width,
+                           const int32_t* hq, int tap_rows, int tap_cols, int frac_bits, int acc_bits,
+                           int out_stage, void* y_dev, void* stream);
 
 /* ---- float64 "ideal" model ----------------------------------------
  * y[r,n] = sum over k (in k order, products and sums rounded separately, zero terms for

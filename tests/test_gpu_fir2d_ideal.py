@@ -131,6 +131,23 @@ def test_fir2d_full_frame_8192_general():
     assert np.array_equal(y.cpu().numpy(), c_oracle().fir2d(x, hq))
 
 
+def test_fir2d_frame_batches_device_and_host():
+    """(frames, H, W) batches: one launch, every frame = its own single-frame result, on the
+    register (8192-wide, separable packed-16 and general) and generic (odd width) paths."""
+    rng = np.random.default_rng(77)
+    sep = (np.outer([1, 4, 6, 4, 1], [1, 4, 6, 4, 1]) * 16).tolist()
+    gen = rng.integers(-4, 5, (5, 5)).tolist()
+    for shape in ((3, 64, 8192), (2, 37, 1001), (4, 130, 640)):
+        x = rng.integers(0, 256, shape, dtype=np.uint8)
+        for k in (sep, gen):
+            got = fir_hip.fir2d_fixed(x, k)
+            dev = torch_ops.fir2d_fixed_dev(torch.from_numpy(x).cuda(), k)
+            torch.cuda.synchronize()
+            assert np.array_equal(dev.cpu().numpy(), got)
+            for f in range(shape[0]):
+                assert np.array_equal(got[f], c_oracle().fir2d(x[f], np.asarray(k), 12, 32, 0)), (shape, f)
+
+
 def test_fir2d_full_frame_8192():
     """BASELINE configs[4]: 8192 x 8192 u8 frame, 5x5 unity-gain kernel."""
     x = np.random.default_rng(20260227).integers(0, 256, (8192, 8192), dtype=np.uint8)

@@ -114,18 +114,22 @@ def fir2d_case(draw):
     frac = draw(st.one_of(st.just(12), st.integers(1, 22)))
     acc = draw(st.one_of(st.just(32), st.integers(16, 48)))
     stage = draw(st.sampled_from([fir_hip.OUT_U8_SAT, fir_hip.OUT_U8_SAT, fir_hip.OUT_I32]))
+    frames = draw(st.sampled_from([0, 0, 1, 2, 3]))  # 0: one 2-D frame; else a (frames, H, W) batch
     seed = draw(st.integers(0, 2**32 - 1))
-    return hq, H, W, frac, acc, stage, seed
+    return hq, H, W, frac, acc, stage, frames, seed
 
 
 @settings(max_examples=600, **SETTINGS)
 @given(fir2d_case())
 def test_fir2d_random_vs_oracle(case):
-    hq, H, W, frac, acc, stage, seed = case
-    x = np.random.default_rng(seed).integers(0, 256, (H, W), dtype=np.uint8)
+    """2-D kernels, single frames and batches of frames (each frame zero padded on its own)."""
+    hq, H, W, frac, acc, stage, frames, seed = case
+    x = np.random.default_rng(seed).integers(0, 256, (frames, H, W) if frames else (H, W), dtype=np.uint8)
     got = fir_hip.fir2d_fixed(x, hq, frac, acc, stage)
-    ref = c_oracle().fir2d(x, np.asarray(hq), frac, acc, stage)
-    assert np.array_equal(got, ref)
+    for f in range(max(frames, 1)):
+        xf = x[f] if frames else x
+        ref = c_oracle().fir2d(xf, np.asarray(hq), frac, acc, stage)
+        assert np.array_equal(got[f] if frames else got, ref), f
 
 
 @st.composite

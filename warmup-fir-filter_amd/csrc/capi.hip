@@ -514,21 +514,21 @@ int fir1d_fixed_segment_dev(const void* x_dev, int in_dtype, int64_t n, int chan
     }
 }
 
-int fir2d_fixed(const uint8_t* x, int64_t height, int64_t width, const int32_t* hq, int tap_rows, int tap_cols,
-                int frac_bits, int acc_bits, int out_stage, void* y, int device) {
+int fir2d_fixed_frames(const uint8_t* x, int64_t frames, int64_t height, int64_t width, const int32_t* hq,
+                       int tap_rows, int tap_cols, int frac_bits, int acc_bits, int out_stage, void* y, int device) {
     try {
-        int64_t n = 0;
-        if (!mul_ok(height, width, &n)) return fail(FIR_EINVAL, "invalid height/width");
+        int64_t n = 0, hw = 0;
+        if (!mul_ok(height, width, &hw) || !mul_ok(hw, frames, &n)) return fail(FIR_EINVAL, "invalid frames/height/width");
         if (n == 0) {
             std::string err;
-            int rc = fir::launch_fir2d(nullptr, 0, 0, hq, tap_rows, tap_cols, frac_bits, acc_bits, out_stage,
+            int rc = fir::launch_fir2d(nullptr, 0, 0, 0, hq, tap_rows, tap_cols, frac_bits, acc_bits, out_stage,
                                        nullptr, nullptr, &err);
             return rc ? fail(rc, err) : FIR_OK;
         }
         if (!x || !y) return fail(FIR_EINVAL, "x and y must not be NULL");
         return run_host(device, x, (size_t)n, y, (size_t)n * out_size(out_stage),
                         [&](void* dx, void* dy, hipStream_t s, std::string* err) {
-                            return fir::launch_fir2d((const uint8_t*)dx, height, width, hq, tap_rows, tap_cols,
+                            return fir::launch_fir2d((const uint8_t*)dx, frames, height, width, hq, tap_rows, tap_cols,
                                                      frac_bits, acc_bits, out_stage, dy, s, err);
                         });
     } catch (...) {
@@ -536,16 +536,28 @@ int fir2d_fixed(const uint8_t* x, int64_t height, int64_t width, const int32_t* 
     }
 }
 
-int fir2d_fixed_dev(const uint8_t* x_dev, int64_t height, int64_t width, const int32_t* hq, int tap_rows,
-                    int tap_cols, int frac_bits, int acc_bits, int out_stage, void* y_dev, void* stream) {
+int fir2d_fixed(const uint8_t* x, int64_t height, int64_t width, const int32_t* hq, int tap_rows, int tap_cols,
+                int frac_bits, int acc_bits, int out_stage, void* y, int device) {
+    return fir2d_fixed_frames(x, 1, height, width, hq, tap_rows, tap_cols, frac_bits, acc_bits, out_stage, y, device);
+}
+
+int fir2d_fixed_frames_dev(const uint8_t* x_dev, int64_t frames, int64_t height, int64_t width, const int32_t* hq,
+                           int tap_rows, int tap_cols, int frac_bits, int acc_bits, int out_stage, void* y_dev,
+                           void* stream) {
     try {
         std::string err;
-        int rc = fir::launch_fir2d(x_dev, height, width, hq, tap_rows, tap_cols, frac_bits, acc_bits, out_stage,
+        int rc = fir::launch_fir2d(x_dev, frames, height, width, hq, tap_rows, tap_cols, frac_bits, acc_bits, out_stage,
                                    y_dev, (hipStream_t)stream, &err);
         return rc ? fail(rc, err) : FIR_OK;
     } catch (...) {
         return fail(FIR_EHIP, "internal error");
     }
+}
+
+int fir2d_fixed_dev(const uint8_t* x_dev, int64_t height, int64_t width, const int32_t* hq, int tap_rows,
+                    int tap_cols, int frac_bits, int acc_bits, int out_stage, void* y_dev, void* stream) {
+    return fir2d_fixed_frames_dev(x_dev, 1, height, width, hq, tap_rows, tap_cols, frac_bits, acc_bits, out_stage, y_dev,
+                                  stream);
 }
 
 int fir1d_ideal_rows(const uint8_t* x, int64_t rows, int64_t width, const double* h, int taps, double* y,

@@ -58,6 +58,8 @@ __global__ __launch_bounds__(kBlock) void fir2d_generic_kernel(const uint8_t* __
     const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t i = blockIdx.y;
     if (j >= W) return;
+    x += (int64_t)blockIdx.z * H * W;  // frame blockIdx.z of a batch stored back to back
+    y += (int64_t)blockIdx.z * H * W;
     const int cr = R / 2, cc = C / 2;
     int64_t acc = 0;
     for (int m = 0; m < R; ++m) {
@@ -109,8 +111,8 @@ static bool rank1_factor(const int32_t* hq, int R, int C, int32_t* col, int32_t*
 }
 
 template <int R, int C, int STAGE>
-static hipError_t launch2d_reg(const uint8_t* x, void* y, int64_t H, int64_t W, const int32_t* hq, int frac,
-                               int acc_bits, hipStream_t s) {
+static hipError_t launch2d_reg(const uint8_t* x, void* y, int64_t frames, int64_t H, int64_t W, const int32_t* hq,
+                               int frac, int acc_bits, hipStream_t s) {
     using OutT = typename OutTraits<STAGE>::T;
     Taps2<R, C> t = {};
     for (int m = 0; m < R; ++m)
@@ -129,7 +131,7 @@ static hipError_t launch2d_reg(const uint8_t* x, void* y, int64_t H, int64_t W, 
         for (int m = 0; m < R; ++m) sep &= t.col[m] >= -(1 << 23) && t.col[m] < (1 << 23);
     }
     if (sep) {
-        const dim3 grid = fir2d_reg_grid<kVec2d, kStrip2dSep>(H, W);
+        const dim3 grid = fir2d_reg_grid<kVec2d, kStrip2dSep>(H, W, frames);
         // separable: R + (C+1)/2 instructions per pixel-row instead of R * (C+1)/2
         for (int p = 0; p < (C + 1) / 2; ++p) {
             const int lo = rowt[C - 1 - 2 * p];
@@ -152,7 +154,7 @@ static hipError_t launch2d_reg(const uint8_t* x, void* y, int64_t H, int64_t W, 
         // packed 16-bit pixel pairs when the whole sum provably fits 16 bits (u8 stage only)
         if constexpr (STAGE == FIR_OUT_U8_SAT) {
             const int pk = nowrap ? plan_pk16(t, t.col, rowt, frac) : 0;
-            const dim3 gpk = fir2d_reg_grid<kVec2d, kStrip2dPk>(H, W);
+            const dim3 gpk = fir2d_reg_grid<kVec2d, kStrip2dPk>(H, W, frames);
             if (pk == (kMode2dPk16 | kMode2dPkHi8)) {
                 hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dPk, SNW | kMode2dPk16 | kMode2dPkHi8, 1, kPdPk>),
                                    gpk, dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
@@ -186,7 +188,7 @@ static hipError_t launch2d_reg(const uint8_t* x, void* y, int64_t H, int64_t W, 
         if constexpr (STAGE == FIR_OUT_U8_SAT) {
             constexpr int GNW = kMode2dDot2 | kMode2dNoWrap | kMode2dPk16, ST = kStrip2dPkGen, PD = pd_pk_gen<R, C>();
             const int pk = nowrap ? plan_pk16_gen(t, hq, frac) : 0;
-            const dim3 gpk = fir2d_reg_grid<kVec2dPkGen, ST>(H, W);
+            const dim3 gpk = fir2d_reg_grid<kVec2dPkGen, ST>(H, W, frames);
             if (pk == (kMode2dPk16 | kMode2dPkHi8)) {
                 hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dPkGen, ST, GNW | kMode2dPkHi8, 1, PD>), gpk,
                                    dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
@@ -203,7 +205,7 @@ static hipError_t launch2d_reg(const uint8_t* x, void* y, int64_t H, int64_t W, 
                 return hipGetLastError();
             }
         }
-        const dim3 grid = fir2d_reg_grid<kVec2dGen, kStrip2dGen>(H, W);
+        const dim3 grid = fir2d_reg_grid<kVec2dGen, kStrip2dGen>(H, W, frames);
         if (nowrap)
             hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dGen, kStrip2dGen, kMode2dDot2 | kMode2dNoWrap, 4, kPdGen>),
                                grid, dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
@@ -215,10 +217,10 @@ static hipError_t launch2d_reg(const uint8_t* x, void* y, int64_t H, int64_t W, 
 }
 
 template <int STAGE>
-static hipError_t launch2d_reg_shape(int R, int C, const uint8_t* x, void* y, int64_t H, int64_t W,
+static hipError_t launch2d_reg_shape(int R, int C, const uint8_t* x, void* y, int64_t frames, int64_t H, int64_t W,
                                      const int32_t* hq, int frac, int acc_bits, hipStream_t s) {
 #define FIR2D_CASE(r, c) \
-    if (R == r && C == c) return launch2d_reg<r, c, STAGE>(x, y, H, W, hq, frac, acc_bits, s);
+    if (R == r && C == c) return launch2d_reg<r, c, STAGE>(x, y, frames, H, W, hq, frac, acc_bits, s);
     FIR2D_CASE(1, 1) FIR2D_CASE(1, 3) FIR2D_CASE(1, 5) FIR2D_CASE(3, 1) FIR2D_CASE(3, 3) FIR2D_CASE(3, 5)
     FIR2D_CASE(5, 1) FIR2D_CASE(5, 3) FIR2D_CASE(5, 5)
 #undef FIR2D_CASE
@@ -227,14 +229,15 @@ static hipError_t launch2d_reg_shape(int R, int C, const uint8_t* x, void* y, in
 
 static bool reg2d_shape(int R, int C) { return (R == 1 || R == 3 || R == 5) && (C == 1 || C == 3 || C == 5); }
 
-int launch_fir2d(const uint8_t* x, int64_t H, int64_t W, const int32_t* hq, int R, int C, int frac, int acc_bits,
-                 int stage, void* y, hipStream_t stream, std::string* err) {
+int launch_fir2d(const uint8_t* x, int64_t frames, int64_t H, int64_t W, const int32_t* hq, int R, int C, int frac,
+                 int acc_bits, int stage, void* y, hipStream_t stream, std::string* err) {
     if (stage != FIR_OUT_U8_SAT && stage != FIR_OUT_I32) return *err = "out_stage must be FIR_OUT_U8_SAT or FIR_OUT_I32", FIR_EINVAL;
-    if (H < 0 || W < 0) return *err = "height and width must be >= 0", FIR_EINVAL;
+    if (H < 0 || W < 0 || frames < 0) return *err = "frames, height and width must be >= 0", FIR_EINVAL;
+    if (frames > 65535) return *err = "frames must be <= 65535 per call", FIR_EINVAL;
     if (!hq) return *err = "hq must not be NULL", FIR_EINVAL;
     if (R < 1 || C < 1 || (int64_t)R * C > FIR_MAX_TAPS) return *err = "tap_rows*tap_cols must be in [1, 256]", FIR_EINVAL;
     if (frac < 1 || acc_bits < 1) return *err = "frac_bits and acc_bits must be >= 1", FIR_EINVAL;
-    if (H == 0 || W == 0) return FIR_OK;
+    if (H == 0 || W == 0 || frames == 0) return FIR_OK;
     if (!x || !y) return *err = "x and y must not be NULL", FIR_EINVAL;
     if (H > 65535 * (int64_t)kStrip2dSep) return *err = "height too large", FIR_EINVAL;
     bool taps16 = true;  // the register kernel multiplies on v_dot2_i32_i16
@@ -243,13 +246,13 @@ int launch_fir2d(const uint8_t* x, int64_t H, int64_t W, const int32_t* hq, int 
                       acc_bits <= 32 && frac <= 31 && taps16 && W >= kVec2d;
     hipError_t e;
     if (fast) {
-        e = stage == FIR_OUT_U8_SAT ? launch2d_reg_shape<FIR_OUT_U8_SAT>(R, C, x, y, H, W, hq, frac, acc_bits, stream)
-                                    : launch2d_reg_shape<FIR_OUT_I32>(R, C, x, y, H, W, hq, frac, acc_bits, stream);
+        e = stage == FIR_OUT_U8_SAT ? launch2d_reg_shape<FIR_OUT_U8_SAT>(R, C, x, y, frames, H, W, hq, frac, acc_bits, stream)
+                                    : launch2d_reg_shape<FIR_OUT_I32>(R, C, x, y, frames, H, W, hq, frac, acc_bits, stream);
     } else {
         if (H > 65535) return *err = "height > 65535 needs the fast path (W % 16 == 0)", FIR_EINVAL;
         Taps2G t;
         for (int k = 0; k < FIR_MAX_TAPS; ++k) t.h[k] = k < R * C ? hq[k] : 0;
-        dim3 grid((unsigned)((W + kBlock - 1) / kBlock), (unsigned)H);
+        dim3 grid((unsigned)((W + kBlock - 1) / kBlock), (unsigned)H, (unsigned)frames);
         if (stage == FIR_OUT_U8_SAT)
             hipLaunchKernelGGL((fir2d_generic_kernel<FIR_OUT_U8_SAT>), grid, dim3(kBlock), 0, stream, x, (uint8_t*)y, H,
                                W, t, R, C, frac, acc_bits);

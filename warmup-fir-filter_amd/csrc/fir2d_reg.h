@@ -189,6 +189,11 @@ __global__ __launch_bounds__(kBlock, MINW) void fir2d_reg_kernel(const uint8_t* 
                                                            typename OutTraits<STAGE>::T* __restrict__ y, int64_t H,
                                                            int64_t W, Taps2<R, C> taps, int shl, int frac) {
     using OutT = typename OutTraits<STAGE>::T;
+    {  // gridDim.z frames of H x W stored back to back (one launch for a batch of frames)
+        const int64_t fo = (int64_t)blockIdx.z * H * W;
+        x += fo;
+        y += fo;
+    }
     constexpr int ND = VEC / 4;  // dwords per lane per row
     constexpr int CC = C / 2;
     constexpr int HLE = C - 1 - CC, HRE = CC;  // horizontal halo
@@ -425,9 +430,9 @@ __global__ __launch_bounds__(kBlock, MINW) void fir2d_reg_kernel(const uint8_t* 
 }
 
 template <int VEC, int STRIP>
-inline dim3 fir2d_reg_grid(int64_t H, int64_t W) {
+inline dim3 fir2d_reg_grid(int64_t H, int64_t W, int64_t frames = 1) {
     const int64_t vecs = W / VEC;
-    return dim3((unsigned)((vecs + kBlock - 1) / kBlock), (unsigned)((H + STRIP - 1) / STRIP));
+    return dim3((unsigned)((vecs + kBlock - 1) / kBlock), (unsigned)((H + STRIP - 1) / STRIP), (unsigned)frames);
 }
 
 }  // namespace fir

@@ -27,9 +27,9 @@ int launch_fir1d_segment(const void* x, int in_dtype, int64_t n, int ch, const i
                          int acc_bits, int stage, const void* halo_left, const void* halo_right, void* y,
                          hipStream_t stream, std::string* err);
 
-// 2-D fixed FIR over a uint8 frame.
-int launch_fir2d(const uint8_t* x, int64_t height, int64_t width, const int32_t* hq, int tap_rows, int tap_cols,
-                 int frac, int acc_bits, int stage, void* y, hipStream_t stream, std::string* err);
+// 2-D fixed FIR over `frames` uint8 frames of height x width stored back to back (one launch).
+int launch_fir2d(const uint8_t* x, int64_t frames, int64_t height, int64_t width, const int32_t* hq, int tap_rows,
+                 int tap_cols, int frac, int acc_bits, int stage, void* y, hipStream_t stream, std::string* err);
 
 // float64 ideal model over uint8 rows.
 int launch_fir1d_ideal(const uint8_t* x, int64_t rows, int64_t width, const double* h, int L, double* y,

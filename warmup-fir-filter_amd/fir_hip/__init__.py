@@ -60,6 +60,8 @@ EXPORTS = {
     "fir1d_fixed_segment_dev": (_i32, [_vp, _i32, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "fir2d_fixed": (_i32, [_vp, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32]),
     "fir2d_fixed_dev": (_i32, [_vp, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
+    "fir2d_fixed_frames": (_i32, [_vp, _i64, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32]),
+    "fir2d_fixed_frames_dev": (_i32, [_vp, _i64, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
     "fir1d_ideal_rows": (_i32, [_vp, _i64, _i64, _vp, _i32, _vp, _i32]),
     "fir1d_ideal_rows_dev": (_i32, [_vp, _i64, _i64, _vp, _i32, _vp, _vp]),
     "fir_metrics_work_bytes": (_i64, []),
@@ -247,18 +249,20 @@ def fir1d_fixed_rows_multi(x: np.ndarray, hq2, frac_bits: int = 12, acc_bits: in
 
 def fir2d_fixed(x: np.ndarray, hq2, frac_bits: int = 12, acc_bits: int = 32, out_stage: int = OUT_U8_SAT,
                 device: int = 0, out: np.ndarray | None = None) -> np.ndarray:
-    """2-D same-mode fixed FIR of a uint8 frame with a (R, C) quantized kernel."""
+    """2-D same-mode fixed FIR of a uint8 frame (H, W), or of a batch of frames (F, H, W) each
+    filtered on its own in one launch, with a (R, C) quantized kernel."""
     x = np.ascontiguousarray(x, dtype=np.uint8)
-    if x.ndim != 2:
-        raise FirHipError("x must be 2-D")
+    if x.ndim not in (2, 3):
+        raise FirHipError("x must be 2-D (a frame) or 3-D (frames, height, width)")
     h2 = np.asarray(hq2, dtype=np.int64)
     if h2.ndim != 2:
         raise FirHipError("hq2 must be 2-D")
     R, C = h2.shape
     h = _taps_i32(h2.reshape(-1))
     y = _out_buf(out, x.shape, np.uint8 if out_stage == OUT_U8_SAT else np.int32, x)
-    _check(lib().fir2d_fixed(_ptr(x), x.shape[0], x.shape[1], _ptr(h), R, C, int(frac_bits), int(acc_bits),
-                             int(out_stage), _ptr(y), int(device)), "fir2d_fixed")
+    frames = x.shape[0] if x.ndim == 3 else 1
+    _check(lib().fir2d_fixed_frames(_ptr(x), frames, x.shape[-2], x.shape[-1], _ptr(h), R, C, int(frac_bits),
+                                    int(acc_bits), int(out_stage), _ptr(y), int(device)), "fir2d_fixed_frames")
     return y
 
 

@@ -154,9 +154,10 @@ def fir1d_fixed_segment_dev(x: torch.Tensor, hq, halo_left, halo_right, frac_bit
 
 def fir2d_fixed_dev(x: torch.Tensor, hq2, frac_bits: int = 12, acc_bits: int = 32, out_stage: int = OUT_U8_SAT,
                     out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """2-D fixed FIR of a uint8 device frame (H, W) or batch of frames (F, H, W), one launch."""
     _check_dev(x, "x")
-    if x.dtype != torch.uint8 or x.dim() != 2:
-        raise FirHipError("x must be a 2-D uint8 device tensor")
+    if x.dtype != torch.uint8 or x.dim() not in (2, 3):
+        raise FirHipError("x must be a 2-D (frame) or 3-D (frames, height, width) uint8 device tensor")
     h2 = np.asarray(hq2.h if isinstance(hq2, Taps) else hq2)
     if h2.ndim != 2:
         raise FirHipError("hq2 must be 2-D")
@@ -165,9 +166,12 @@ def fir2d_fixed_dev(x: torch.Tensor, hq2, frac_bits: int = 12, acc_bits: int = 3
     if out is None:
         out = torch.empty(x.shape, dtype=_OUT_DTYPE[out_stage], device=x.device)
     _check_dev(out, "out")
-    _check(lib().fir2d_fixed_dev(ctypes.c_void_p(x.data_ptr()), x.shape[0], x.shape[1], t.ptr, R, C, int(frac_bits),
-                                 int(acc_bits), int(out_stage), ctypes.c_void_p(out.data_ptr()),
-                                 _stream_ptr(x, stream)), "fir2d_fixed_dev")
+    if out.shape != x.shape or out.dtype != _OUT_DTYPE[out_stage]:
+        raise FirHipError("out must match x's shape and the out_stage dtype")
+    frames = x.shape[0] if x.dim() == 3 else 1
+    _check(lib().fir2d_fixed_frames_dev(ctypes.c_void_p(x.data_ptr()), frames, x.shape[-2], x.shape[-1], t.ptr, R, C,
+                                        int(frac_bits), int(acc_bits), int(out_stage), ctypes.c_void_p(out.data_ptr()),
+                                        _stream_ptr(x, stream)), "fir2d_fixed_frames_dev")
     return out
 
 
