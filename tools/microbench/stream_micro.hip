@@ -275,8 +275,14 @@ int main(int argc, char** argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 15;
     Bufs b;
     b.n = (int64_t)1 << 28;
+    // STREAM_ALLOC=1: output fine-grained, 3: output uncached (hipExtMallocWithFlags), 0: hipMalloc
+    const int alloc = getenv("STREAM_ALLOC") ? atoi(getenv("STREAM_ALLOC")) : 0;
     CK(hipMalloc(&b.x, b.n * 2));
-    CK(hipMalloc(&b.y, b.n * 4));
+    if (alloc)
+        CK(hipExtMallocWithFlags((void**)&b.y, b.n * 4, alloc == 1 ? hipDeviceMallocFinegrained : hipDeviceMallocUncached));
+    else
+        CK(hipMalloc(&b.y, b.n * 4));
+    printf("output allocation: %s\n", alloc == 1 ? "fine-grained" : (alloc == 3 ? "uncached" : "hipMalloc"));
     std::vector<int16_t> hx(b.n);
     uint32_t r = 12345;
     for (auto& v : hx) {
@@ -290,11 +296,11 @@ int main(int argc, char** argv) {
     std::vector<V> vs = {
         {"widen reg K1 b256", l_widen_reg<1, 256>, rw, true, {}},
         {"widen half row nt", l_wdpat<1, 0, 1, 256>, rw, true, {}},
-        {"half + edge load", l_whe<1>, rw, true, {}},
-        {"half + edge load + dpp", l_whe<2>, rw, true, {}},
-        {"half + LDS halo", l_whe<3>, rw, true, {}},
-        {"half + no edge", l_whe<0>, rw, true, {}},
+        {"widen half row plain", l_wdpat<1, 0, 0, 256>, rw, true, {}},
         {"widen rows nt", l_wdpat<0, 0, 1, 256>, rw, true, {}},
+        {"wpat rows R1 nt", l_wpat<0, 1, 1, 256>, wr, false, {}},
+        {"wpat rows R1 plain", l_wpat<0, 1, 0, 256>, wr, false, {}},
+        {"wpat rows R2 nt", l_wpat<0, 2, 1, 256>, wr, false, {}},
     };
     // correctness of every widen variant (sampled)
     std::vector<int32_t> hy(b.n);
