@@ -45,6 +45,11 @@ __device__ __forceinline__ u32x4 widen_lo(u32x2 d) {  // 4 int16 -> 4 int32
                  (uint32_t)((int32_t)d.y >> 16)};
 }
 
+template <int N>
+__device__ __forceinline__ void vmcnt_n() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
 // ---- widen copies: K KiB of int16 per wave -> 2K KiB of int32 ---------------------------
 // Register path: lane loads 16 B per KiB, LDS transpose, 1 KiB nt row stores (the FIR's shape).
 template <int K, int BLOCK>
@@ -163,6 +168,60 @@ __global__ __launch_bounds__(BLOCK) void widen_pat(const int16_t* __restrict__ x
 // lanes 0/63 the dwords around the wave, the rest their own), E=2 that plus the two DPP moves,
 // E=3 the halo through LDS instead: each wave publishes its edge dwords, one block barrier,
 // lanes 0/63 read the neighbours' (block edges load from memory).
+// Producer/consumer widen: wave 0 of a block only LOADS (LDS-DMA, so its vmcnt counts nothing
+// but its own loads, in order) and keeps D phase-groups of 3 tiles in flight; waves 1-3 only
+// read LDS, widen and STORE (nothing to wait for).  One s_barrier per phase; G = D + 1 LDS
+// groups of 3 x 1 KiB.  Each block walks a contiguous range of tiles.
+template <int D, bool NT>
+__global__ __launch_bounds__(256) void widen_pc(const int16_t* __restrict__ x, int32_t* __restrict__ y,
+                                                int64_t ntiles, int64_t per_block) {
+    constexpr int G = D + 1;
+    __shared__ u32x4 ring[G][3][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t t0 = (int64_t)blockIdx.x * per_block;
+    const int64_t t1 = t0 + per_block < ntiles ? t0 + per_block : ntiles;
+    const int64_t nph = (t1 - t0 + 2) / 3;  // phases of 3 tiles
+    const u32x4* src = reinterpret_cast<const u32x4*>(x);
+    u32x4* dst = reinterpret_cast<u32x4*>(y);
+    auto issue = [&](int64_t p) {  // loader: the 3 tiles of phase p into group p % G
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            int64_t t = t0 + 3 * p + c;
+            t = t < t1 ? t : t1 - 1;  // the last phase may be short: re-read a valid tile
+            glds16(src + t * 64 + lane, &ring[p % G][c][0], NT);
+        }
+    };
+    if (w == 0) {
+        for (int64_t p = 0; p < D && p < nph; ++p) issue(p);
+    }
+    for (int64_t p = 0; p < nph; ++p) {
+        if (w == 0) {
+            if (p + D < nph) {
+                issue(p + D);
+                vmcnt_n<3 * D>();  // phase p's 3 loads landed (3*D younger loads may be in flight)
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+        __builtin_amdgcn_s_barrier();  // phase p's group is in LDS for every wave
+        asm volatile("" ::: "memory");
+        if (w > 0) {
+            const int64_t t = t0 + 3 * p + (w - 1);
+            if (t < t1) {
+                const u32x2* s2 = reinterpret_cast<const u32x2*>(&ring[p % G][w - 1][0]);
+                const u32x2 a = s2[lane], b = s2[64 + lane];
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                st_nt(dst + t * 128 + lane, widen_lo(a));
+                st_nt(dst + t * 128 + 64 + lane, widen_lo(b));
+            }
+        }
+        // the group read in phase p is reloaded in phase p + G - D = p + 1 only after the next
+        // barrier, by which time every consumer has read it (the reads finish before the stores)
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    }
+}
+
 template <int E>
 __global__ __launch_bounds__(256) void widen_half_edge(const int16_t* __restrict__ x, int32_t* __restrict__ y,
                                                        int64_t nvec) {
@@ -266,6 +325,13 @@ void l_wdpat(const Bufs& b, hipStream_t s) {
                        dim3(BLOCK), 0, s, b.x, b.y);
 }
 
+template <int D, bool NT, int BPC>
+void l_pc(const Bufs& b, hipStream_t s) {
+    const int64_t ntiles = b.n / 512, blocks = 256 * BPC;
+    hipLaunchKernelGGL((widen_pc<D, NT>), dim3((unsigned)blocks), dim3(256), 0, s, b.x, b.y, ntiles,
+                       (ntiles + blocks - 1) / blocks);
+}
+
 template <int E>
 void l_whe(const Bufs& b, hipStream_t s) {
     hipLaunchKernelGGL((widen_half_edge<E>), dim3((unsigned)(b.n / 4 / 256)), dim3(256), 0, s, b.x, b.y, b.n / 4);
@@ -296,17 +362,19 @@ int main(int argc, char** argv) {
     std::vector<V> vs = {
         {"widen reg K1 b256", l_widen_reg<1, 256>, rw, true, {}},
         {"widen half row nt", l_wdpat<1, 0, 1, 256>, rw, true, {}},
-        {"widen half row plain", l_wdpat<1, 0, 0, 256>, rw, true, {}},
-        {"widen rows nt", l_wdpat<0, 0, 1, 256>, rw, true, {}},
-        {"wpat rows R1 nt", l_wpat<0, 1, 1, 256>, wr, false, {}},
-        {"wpat rows R1 plain", l_wpat<0, 1, 0, 256>, wr, false, {}},
-        {"wpat rows R2 nt", l_wpat<0, 2, 1, 256>, wr, false, {}},
+        {"pc D2 nt bpc2", l_pc<2, true, 2>, rw, true, {}},
+        {"pc D3 nt bpc2", l_pc<3, true, 2>, rw, true, {}},
+        {"pc D3 nt bpc4", l_pc<3, true, 4>, rw, true, {}},
+        {"pc D4 nt bpc4", l_pc<4, true, 4>, rw, true, {}},
+        {"pc D3 bpc4", l_pc<3, false, 4>, rw, true, {}},
+        {"pc D6 nt bpc2", l_pc<6, true, 2>, rw, true, {}},
     };
     // correctness of every widen variant (sampled)
     std::vector<int32_t> hy(b.n);
     for (auto& v : vs) {
         if (!v.widen) continue;
         CK(hipMemset(b.y, 0xA5, b.n * 4));
+        CK(hipDeviceSynchronize());  // the memset runs on the null stream; st is non-blocking
         v.fn(b, st);
         CK(hipStreamSynchronize(st));
         CK(hipMemcpy(hy.data(), b.y, b.n * 4, hipMemcpyDeviceToHost));
