@@ -71,6 +71,8 @@ def _worker(rank, world, port, hq, channels, q):
     (3, [5, -7, 9, 11], 1),
     (4, [32767, -32768, 32767, -32768, 32767], 1),
     (2, [4096], 1),
+    (8, [-256, -1024, 6656, -1024, -256], 1),  # the 8-rank layout of BASELINE configs[3]
+    (8, [3, -5, 7, -11, 13, -11, 7, -5, 3], 2),
 ])
 def test_sharded_halo_exchange_matches_unsharded(world, hq, channels):
     ctx = mp.get_context("spawn")
