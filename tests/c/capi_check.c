@@ -45,6 +45,10 @@ int main(void) {
         expect(fir_ipc_import(handle, -1, 0, &p) == FIR_EINVAL, "ipc import offset");
         expect(fir_ipc_close((void*)handle) == FIR_EINVAL, "ipc close unknown");
         expect(fir_peek(NULL, NULL, 8) == FIR_EINVAL, "peek null");
+        int can = 7;
+        char bus[16];
+        expect(fir_peer_access(0, NULL, &can) == FIR_EINVAL, "peer access null");
+        expect(fir_device_bus_id(0, bus, 8) == FIR_EINVAL, "bus id short buffer");
     }
     expect(strlen(fir_last_error()) > 0, "error text");
     if (!have) {
@@ -85,6 +89,28 @@ int main(void) {
         free(y8);
         free(y32);
         free(yd);
+    }
+    /* the chunked host path (>= 64 MiB inputs: 8 chunks, a second host thread issuing the
+     * device-to-host copies), one long row and row blocks, 3-channel frames, in place */
+    {
+        const int64_t n = ((int64_t)1 << 26) + 3 * 11;
+        uint8_t* x8 = malloc((size_t)n);
+        uint8_t* y8 = malloc((size_t)n);
+        for (int64_t i = 0; i < n; ++i) x8[i] = (uint8_t)(i * 131);
+        const int32_t h5[5] = {-256, -1024, 6656, -1024, -256};
+        expect(fir1d_fixed_rows(x8, FIR_IN_U8, 1, n / 3, 3, h5, 5, 12, 32, FIR_OUT_U8_SAT, y8, 0) == FIR_OK, "chunked row");
+        expect(fir1d_fixed_rows(x8, FIR_IN_U8, 4099, (n / 3) / 4099, 3, h5, 5, 12, 32, FIR_OUT_U8_SAT, y8, 0) == FIR_OK,
+               "chunked row blocks");
+        expect(fir1d_fixed_rows(x8, FIR_IN_U8, 1, n, 1, h5, 5, 12, 32, FIR_OUT_U8_SAT, x8, 0) == FIR_OK, "chunked in place");
+        const int32_t k5[25] = {1, 4, 6, 4, 1, 4, 16, 24, 16, 4, 6, 24, 36, 24, 6, 4, 16, 24, 16, 4, 1, 4, 6, 4, 1};
+        expect(fir2d_fixed_frames(x8, 3, 257, 4096, k5, 5, 5, 8, 32, FIR_OUT_U8_SAT, y8, 0) == FIR_OK, "2d frames");
+        char bus[64];
+        int can = 0;
+        expect(fir_device_bus_id(0, bus, (int)sizeof bus) == FIR_OK, "bus id");
+        expect(fir_peer_access(0, bus, &can) == FIR_OK && can == 1, "peer access self");
+        expect(fir_peer_access(0, "0000:ff:1f.7", &can) == FIR_OK && can == 0, "peer access unknown");
+        free(x8);
+        free(y8);
     }
     static uint8_t one = 1;
     expect(fir1d_fixed_rows_sharded(&one, 0, 1, 1, 1, h3, 3, 12, 32, 0, NULL, devs, 1) == FIR_EINVAL, "null y");
