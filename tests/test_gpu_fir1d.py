@@ -163,6 +163,35 @@ def test_int16_to_int32_vs_oracle(name, channels, n):
     assert np.array_equal(got, fo.fir1d_i16_i32(x, hq, channels=channels))
 
 
+@pytest.mark.parametrize("L", [10, 13, 16, 17, 24, 31, 32, 33, 48, 63, 64, 65])
+@pytest.mark.parametrize("dtype,stage", [(np.int16, fir_hip.OUT_I32), (np.uint8, fir_hip.OUT_U8_SAT),
+                                         (np.int16, fir_hip.OUT_U8_SAT), (np.uint8, fir_hip.OUT_I32)])
+@pytest.mark.parametrize("shape", [(1, 100_003), (1, 2048), (37, 4096), (5, 1000), (3, 1001), (9, 8)])
+def test_long_filters_vs_oracle(L, dtype, stage, shape):
+    """10..64 taps: the LDS-window v_dot2 kernel (fir1d_lds.hip) for one row or rows of a
+    multiple of 8 samples (narrow rows included), the generic kernel otherwise / beyond 64 taps;
+    32- and 24-bit accumulators."""
+    rng = np.random.default_rng(L * 1000 + shape[1])
+    info = np.iinfo(dtype)
+    x = rng.integers(info.min, info.max + 1, shape, dtype=dtype)
+    hq = rng.integers(-3000, 3000, L).tolist()
+    for acc in (32, 24):
+        got = fir_hip.fir1d_fixed_rows(x, hq, 12, acc, stage)
+        assert np.array_equal(got, _co().fir1d_rows(x, hq, 12, acc, stage)), acc
+
+
+def test_long_filter_large_vs_oracle():
+    """Many workgroups: 31 taps over 2^24 int16 samples, and over u8 images of 4096-sample rows."""
+    rng = np.random.default_rng(31)
+    hq = rng.integers(-32768, 32768, 31).tolist()  # full int16 taps: the 32-bit sums wrap
+    x = rng.integers(-32768, 32768, 1 << 24, dtype=np.int16)
+    assert np.array_equal(fir_hip.fir1d_fixed_rows(x, hq, 12, 32, fir_hip.OUT_I32),
+                          _co().fir1d_rows(x, hq, 12, 32, fir_hip.OUT_I32))
+    xu = rng.integers(0, 256, (1024, 4096), dtype=np.uint8)
+    assert np.array_equal(fir_hip.fir1d_fixed_rows(xu, hq[:20], 12, 32, fir_hip.OUT_U8_SAT),
+                          _co().fir1d_rows(xu, hq[:20], 12, 32, fir_hip.OUT_U8_SAT))
+
+
 @pytest.mark.parametrize("frac,acc", [(1, 32), (12, 16), (12, 24), (15, 31), (20, 32), (12, 40), (12, 64), (31, 32),
                                       (40, 48), (63, 64)])
 @pytest.mark.parametrize("stage", [fir_hip.OUT_I32, fir_hip.OUT_U8_SAT])

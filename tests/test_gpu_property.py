@@ -40,9 +40,10 @@ def _unaligned(a: np.ndarray, off: int) -> np.ndarray:
 def fir1d_case(draw):
     dtype = draw(st.sampled_from([np.uint8, np.int16]))
     ch = draw(st.sampled_from([1, 1, 1, 2, 2, 3]))
-    L = draw(st.one_of(st.integers(1, 9), st.integers(10, 24)))
+    L = draw(st.one_of(st.integers(1, 9), st.integers(10, 24), st.integers(25, 70)))
     rows = draw(st.one_of(st.just(1), st.integers(2, 40)))
-    width = draw(st.one_of(st.integers(1, 64), st.integers(65, 3000), st.sampled_from([256, 512, 4096])))
+    width = draw(st.one_of(st.integers(1, 64), st.integers(65, 3000), st.sampled_from([256, 512, 4096]),
+                           st.integers(1, 300).map(lambda k: 8 * k)))
     frac = draw(st.one_of(st.just(12), st.integers(1, 31), st.integers(32, 40)))
     acc = draw(st.one_of(st.just(32), st.integers(max(1, frac - 4), 64)))
     stage = draw(st.sampled_from([fir_hip.OUT_U8_SAT, fir_hip.OUT_I32]))

@@ -206,6 +206,8 @@ int launch_fir1d_rows(const void* x, int in_dtype, int64_t rows, int64_t width, 
                     ? launch_reg_taps<int16_t, FIR_OUT_U8_SAT, 2, 1>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream)
                     : launch_reg_taps<int16_t, FIR_OUT_I32, 2, 1>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
         }
+    } else if (lds_path_ok(x, y, in_dtype, rows, rowlen, total, ch, hq, L, frac, acc_bits)) {
+        e = launch_fir1d_lds(x, in_dtype, rows, rowlen, total, hq, L, frac, acc_bits, stage, y, stream);
     } else {
         e = dispatch_generic(in_dtype, stage, x, y, 0, total, total, rowlen, rows > 1, ch, nullptr, nullptr, hq, L,
                              frac, acc_bits, stream);

@@ -12,6 +12,13 @@ namespace fir {
 int launch_fir1d_rows(const void* x, int in_dtype, int64_t rows, int64_t width, int ch, const int32_t* hq, int L,
                       int frac, int acc_bits, int stage, void* y, hipStream_t stream, std::string* err);
 
+// Long filters (up to 64 taps, one channel, int16 taps, acc_bits <= 32): the LDS-window
+// v_dot2 kernel (fir1d_lds.hip).  lds_path_ok says whether it applies.
+bool lds_path_ok(const void* x, const void* y, int in_dtype, int64_t rows, int64_t rowlen, int64_t total, int ch,
+                 const int32_t* hq, int L, int frac, int acc_bits);
+hipError_t launch_fir1d_lds(const void* x, int in_dtype, int64_t rows, int64_t rowlen, int64_t total,
+                            const int32_t* hq, int L, int frac, int acc_bits, int stage, void* y, hipStream_t s);
+
 // F filters of L taps (hq row-major F x L) over the same x; y = F consecutive output planes.
 int launch_fir1d_rows_multi(const void* x, int in_dtype, int64_t rows, int64_t width, int ch, const int32_t* hq,
                             int L, int F, int frac, int acc_bits, int stage, void* y, hipStream_t stream,
