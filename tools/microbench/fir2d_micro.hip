@@ -26,20 +26,30 @@ using namespace fir;
 static int32_t g_h[5][5];
 
 static int32_t g_col[5], g_row[5];
+static int32_t g_hg[5][5];  // a non-separable kernel for the general packed-16 variants
 
 // Memory-only twin of the strip loop: the same row loads (PD ahead, + the halo dword) and
 // output-row stores, no arithmetic (output row o = input row o, XOR of the halo dword so the
 // loads stay live).  Bounds the 2-D kernel's memory time for this access pattern.
-template <int VEC, int STRIP, int PD, bool HALO>
+template <int VEC, int STRIP, int PD, bool HALO, bool NTS = false, bool XCD = false>
 __global__ __launch_bounds__(kBlock) void copy2d_kernel(const uint8_t* __restrict__ x, uint8_t* __restrict__ y,
                                                          int64_t H, int64_t W) {
     constexpr int ND = VEC / 4, T = STRIP + 4;
     typedef uint32_t vN __attribute__((ext_vector_type(ND)));
-    x += (int64_t)blockIdx.z * H * W;  // batched launches: frame blockIdx.z
-    y += (int64_t)blockIdx.z * H * W;
+    int64_t bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    if constexpr (XCD) {  // same remap as fir2d_reg_kernel<..., XCD = true>
+        const int64_t gx = gridDim.x, gy = gridDim.y, nb = gx * gy * gridDim.z;
+        const int64_t b = bx + gx * (by + gy * bz), q = nb / 8;
+        const int64_t p = b < q * 8 ? (b % 8) * q + b / 8 : b;
+        bx = p % gx;
+        by = (p / gx) % gy;
+        bz = p / (gx * gy);
+    }
+    x += bz * H * W;  // batched launches: frame bz
+    y += bz * H * W;
     const int lane = threadIdx.x & 63;
-    const int64_t col0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * VEC;
-    const int64_t r0 = (int64_t)blockIdx.y * STRIP;
+    const int64_t col0 = (bx * kBlock + threadIdx.x) * VEC;
+    const int64_t r0 = by * STRIP;
     const int64_t hcol = lane == 0 ? (col0 >= 4 ? col0 - 4 : col0) : (lane == 63 && col0 + VEC < W ? col0 + VEC : col0);
     vN rows[T];
     uint32_t hr[T];
@@ -57,9 +67,26 @@ __global__ __launch_bounds__(kBlock) void copy2d_kernel(const uint8_t* __restric
         if (o >= 0 && r0 + o < H) {
             vN v = rows[t];
             v[0] ^= hr[t];
-            *reinterpret_cast<vN*>(y + (r0 + o) * W + col0) = v;
+            vN* d = reinterpret_cast<vN*>(y + (r0 + o) * W + col0);
+            if constexpr (NTS) __builtin_nontemporal_store(v, d);
+            else *d = v;
         }
     }
+}
+
+// Contiguous copy with the 1-D u8 kernel's shape: a wave moves K consecutive 1 KiB chunks,
+// non-temporal stores.  The ceiling for the same bytes without the strip pattern.
+template <int K>
+__global__ __launch_bounds__(kBlock) void copy1d_nt_kernel(const uint8_t* __restrict__ x, uint8_t* __restrict__ y, int64_t n) {
+    typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / 64, lane = threadIdx.x & 63;
+    const int64_t base = wave * K * 1024 + lane * 16;
+    v4 d[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) d[k] = base + k * 1024 < n ? *reinterpret_cast<const v4*>(x + base + k * 1024) : v4{};
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        if (base + k * 1024 < n) __builtin_nontemporal_store(d[k], reinterpret_cast<v4*>(y + base + k * 1024));
 }
 
 template <int VEC, int STRIP, int PD, bool HALO>
@@ -74,11 +101,16 @@ static void launch_memcpy2d(const uint8_t* x, uint8_t* y, int64_t H, int64_t W, 
 
 static const uint8_t* g_bx;  // frame-batch base pointers (set in main)
 static uint8_t* g_by;
-template <int VEC, int STRIP, int PD>
+template <int VEC, int STRIP, int PD, bool NTS = false, bool XCD = false>
 static void launch_copy2d_x4(const uint8_t*, uint8_t*, int64_t H, int64_t W, hipStream_t s) {
     dim3 grid = fir2d_reg_grid<VEC, STRIP>(H, W);
     grid.z = 4;
-    hipLaunchKernelGGL((copy2d_kernel<VEC, STRIP, PD, true>), grid, dim3(kBlock), 0, s, g_bx, g_by, H, W);
+    hipLaunchKernelGGL((copy2d_kernel<VEC, STRIP, PD, true, NTS, XCD>), grid, dim3(kBlock), 0, s, g_bx, g_by, H, W);
+}
+template <int K>
+static void launch_copy1d_x4(const uint8_t*, uint8_t*, int64_t H, int64_t W, hipStream_t s) {
+    const int64_t n = 4 * H * W, waves = (n + K * 1024 - 1) / (K * 1024);
+    hipLaunchKernelGGL((copy1d_nt_kernel<K>), dim3((unsigned)((waves + 3) / 4)), dim3(kBlock), 0, s, g_bx, g_by, n);
 }
 static void launch_memcpy_x4(const uint8_t*, uint8_t*, int64_t H, int64_t W, hipStream_t s) {
     CK(hipMemcpyAsync(g_by, g_bx, 4 * H * W, hipMemcpyDeviceToDevice, s));
@@ -110,11 +142,12 @@ struct V {
     void (*fn)(const uint8_t*, uint8_t*, int64_t, int64_t, hipStream_t);
     std::vector<float> us;
     int frames = 1;  // frames per launch (batched variants run on g_x / g_y from frame 0)
+    bool gen = false;  // checked against g_hg instead of g_h
 };
 
 static const uint8_t* g_x;
 static uint8_t* g_y;
-template <int VEC, int STRIP, int MODE, int PD, int NF>
+template <int VEC, int STRIP, int MODE, int PD, int NF, bool NTS = false, bool XCD = false>
 static void launch_batch(const uint8_t*, uint8_t*, int64_t H, int64_t W, hipStream_t s) {
     Taps2<5, 5> t = {};
     for (int m = 0; m < 5; ++m)
@@ -123,8 +156,21 @@ static void launch_batch(const uint8_t*, uint8_t*, int64_t H, int64_t W, hipStre
     if (!(plan_pk16(t, g_col, g_row, 12) & kMode2dPk16)) exit(1);
     dim3 grid = fir2d_reg_grid<VEC, STRIP>(H, W);
     grid.z = NF;
-    hipLaunchKernelGGL((fir2d_reg_kernel<5, 5, FIR_OUT_U8_SAT, VEC, STRIP, MODE, 1, PD, false>), grid, dim3(kBlock), 0, s,
-                       g_x, g_y, H, W, t, 0, 12);
+    hipLaunchKernelGGL((fir2d_reg_kernel<5, 5, FIR_OUT_U8_SAT, VEC, STRIP, MODE, 1, PD, false, NTS, XCD>), grid, dim3(kBlock),
+                       0, s, g_x, g_y, H, W, t, 0, 12);
+}
+
+template <int VEC, int STRIP, int MODE, int PD, bool NTS, bool XCD>
+static void launch_batch_gen(const uint8_t*, uint8_t*, int64_t H, int64_t W, hipStream_t s) {
+    Taps2<5, 5> t = {};
+    for (int m = 0; m < 5; ++m)
+        for (int n = 0; n < 5; ++n) t.h[m][n] = g_hg[m][n];
+    pack_taps2(t);
+    if (plan_pk16_gen(t, &g_hg[0][0], 12) != (MODE & (kMode2dPk16 | kMode2dPkSigned | kMode2dPkHi8))) exit(2);
+    dim3 grid = fir2d_reg_grid<VEC, STRIP>(H, W);
+    grid.z = 4;
+    hipLaunchKernelGGL((fir2d_reg_kernel<5, 5, FIR_OUT_U8_SAT, VEC, STRIP, MODE, 1, PD, false, NTS, XCD>), grid, dim3(kBlock),
+                       0, s, g_x, g_y, H, W, t, 0, 12);
 }
 
 // Reads n 16-byte words grid-stride; writes one word only if a never-true condition holds.
@@ -146,6 +192,11 @@ int main(int argc, char** argv) {
         for (int n = 0; n < 5; ++n) g_h[m][n] = h1[m] * h1[n] / 4096;  // rank 1: (h1/256) x (h1/16)
     for (int m = 0; m < 5; ++m) g_col[m] = h1[m] / 16;
     for (int n = 0; n < 5; ++n) g_row[n] = h1[n] / 256;
+    {  // tests/test_gpu_fir2d_ideal.py GEN_PK_KERNELS-like: signed taps in [-4, 4], Laplacian-ish centre
+        const int32_t hg[5][5] = {{1, -2, 3, -1, 0}, {-3, 4, 2, -4, 1}, {2, 1, 4, 1, 2}, {0, -4, 2, 4, -3}, {-1, 3, -2, 1, 2}};
+        for (int m = 0; m < 5; ++m)
+            for (int n = 0; n < 5; ++n) g_hg[m][n] = hg[m][n];
+    }
     std::vector<uint8_t> hx(H * W), hy(H * W);
     uint64_t s = 88172645463325252ull;
     for (auto& v : hx) {
@@ -167,32 +218,39 @@ int main(int argc, char** argv) {
     g_by = dy;
     hipStream_t st;
     CK(hipStreamCreate(&st));
+    constexpr int PKM = kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap;
+    constexpr int GKM = kMode2dDot2 | kMode2dNoWrap | kMode2dPk16 | kMode2dPkSigned;
     std::vector<V> vs = {
-        {"pk16hi8 v16 s32 pd4 (lib)", true, launch<16, 32, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 1, 4>, {}},
-        {"x4 v16 s32 pd4 (lib)", true, launch_batch<16, 32, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 4, 4>, {}, 4},
-        {"x4 v16 s8 pd4", true, launch_batch<16, 8, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 4, 4>, {}, 4},
-        {"x4 v32 s32 pd3", true, launch_batch<32, 32, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 3, 4>, {}, 4},
-        {"x4 v32 s16 pd4", true, launch_batch<32, 16, kMode2dSep | kMode2dPk16 | kMode2dPkHi8 | kMode2dNoWrap, 4, 4>, {}, 4},
-        {"x4 copy2d v32 s32 pd3", false, launch_copy2d_x4<32, 32, 3>, {}, 4},
-        {"x4 copy2d v16 s32 pd3", false, launch_copy2d_x4<16, 32, 3>, {}, 4},
-        {"x4 copy2d v16 s32 pd8", false, launch_copy2d_x4<16, 32, 8>, {}, 4},
-        {"x4 copy2d v16 s16 pd4", false, launch_copy2d_x4<16, 16, 4>, {}, 4},
+        {"x4 v16 s32 pd4 (lib)", true, launch_batch<16, 32, PKM, 4, 4>, {}, 4},
+        {"x4 v16 s32 pd4 nts", true, launch_batch<16, 32, PKM, 4, 4, true>, {}, 4},
+        {"x4 v16 s32 pd4 nts xcd", true, launch_batch<16, 32, PKM, 4, 4, true, true>, {}, 4},
+        {"x4 v16 s32 pd3 nts xcd", true, launch_batch<16, 32, PKM, 3, 4, true, true>, {}, 4},
+        {"x4 v16 s32 pd6 nts xcd", true, launch_batch<16, 32, PKM, 6, 4, true, true>, {}, 4},
+        {"x4 v16 s16 pd4 nts", true, launch_batch<16, 16, PKM, 4, 4, true>, {}, 4},
+        {"x4 v16 s16 pd4 nts xcd", true, launch_batch<16, 16, PKM, 4, 4, true, true>, {}, 4},
+        {"x4 v16 s16 pd3 nts xcd", true, launch_batch<16, 16, PKM, 3, 4, true, true>, {}, 4},
+        {"x4 v16 s16 pd6 nts xcd", true, launch_batch<16, 16, PKM, 6, 4, true, true>, {}, 4},
+        {"x4 v16 s24 pd4 nts xcd", true, launch_batch<16, 24, PKM, 4, 4, true, true>, {}, 4},
+        {"x4 v16 s8 pd4 nts xcd", true, launch_batch<16, 8, PKM, 4, 4, true, true>, {}, 4},
+        {"x4 v16 s12 pd4 nts xcd", true, launch_batch<16, 12, PKM, 4, 4, true, true>, {}, 4},
+        {"x4 gen v16 s16 pd2 (lib)", true, launch_batch_gen<16, 16, GKM, 2, false, false>, {}, 4, true},
+        {"x4 gen v16 s16 pd2 nts", true, launch_batch_gen<16, 16, GKM, 2, true, false>, {}, 4, true},
+        {"x4 gen v16 s16 pd2 nts xcd", true, launch_batch_gen<16, 16, GKM, 2, true, true>, {}, 4, true},
+        {"x4 gen v16 s8 pd2 nts xcd", true, launch_batch_gen<16, 8, GKM, 2, true, true>, {}, 4, true},
+        {"x4 gen v16 s12 pd2 nts xcd", true, launch_batch_gen<16, 12, GKM, 2, true, true>, {}, 4, true},
+        {"x4 gen v8 s16 pd3 nts xcd", true, launch_batch_gen<8, 16, GKM, 3, true, true>, {}, 4, true},
+        {"x4 copy2d v16 s32 pd3 nts xcd", false, launch_copy2d_x4<16, 32, 3, true, true>, {}, 4},
+        {"x4 copy2d v16 s16 pd4 nts xcd", false, launch_copy2d_x4<16, 16, 4, true, true>, {}, 4},
+        {"x4 copy1d nt K1", false, launch_copy1d_x4<1>, {}, 4},
         {"x4 hipMemcpy D2D", false, launch_memcpy_x4, {}, 4},
-        {"copy2d v16 s16 pd3", false, launch_copy2d<16, 16, 3, true>, {}},
-        {"copy2d v16 s16 pd3 nohalo", false, launch_copy2d<16, 16, 3, false>, {}},
-        {"copy2d v16 s16 pd8", false, launch_copy2d<16, 16, 8, true>, {}},
-        {"copy2d v16 s32 pd8", false, launch_copy2d<16, 32, 8, true>, {}},
-        {"copy2d v16 s32 pd3", false, launch_copy2d<16, 32, 3, true>, {}},
-        {"copy2d v16 s64 pd4", false, launch_copy2d<16, 64, 4, true>, {}},
-        {"copy2d v8 s16 pd3", false, launch_copy2d<8, 16, 3, true>, {}},
-        {"hipMemcpy D2D", false, launch_memcpy2d, {}},
     };
-    auto ref = [&](int64_t i, int64_t j) {
+    auto ref = [&](int64_t i, int64_t j, bool gen) {
         uint32_t a = 0;
         for (int m = 0; m < 5; ++m)
             for (int n = 0; n < 5; ++n) {
                 const int64_t ii = i - m + 2, jj = j - n + 2;
-                if (ii >= 0 && ii < H && jj >= 0 && jj < W) a += (uint32_t)(g_h[m][n] * (int32_t)hx[ii * W + jj]);
+                const int32_t h = gen ? g_hg[m][n] : g_h[m][n];
+                if (ii >= 0 && ii < H && jj >= 0 && jj < W) a += (uint32_t)(h * (int32_t)hx[ii * W + jj]);
             }
         const int32_t q = ((int32_t)a >> 12) + (((int32_t)a >> 11) & 1);
         return (uint8_t)std::min(std::max(q, 0), 255);
@@ -210,9 +268,9 @@ int main(int argc, char** argv) {
             const bool edge_row = i < 3 || i >= H - 3 || i % 31 == 0 || i % 32 < 3;
             for (int64_t j = 0; j < W; j += (edge_row || j < 3 || j >= W - 3) ? 1 : 61) {
                 ++n;
-                if (hy[i * W + j] != ref(i, j) && bad++ < 3)
+                if (hy[i * W + j] != ref(i, j, v.gen) && bad++ < 3)
                     fprintf(stderr, "%s: (%lld,%lld) %d vs %d\n", v.name.c_str(), (long long)i, (long long)j,
-                            hy[i * W + j], ref(i, j));
+                            hy[i * W + j], ref(i, j, v.gen));
             }
         }
         printf("check %-16s %s (%lld px, %lld bad)\n", v.name.c_str(), bad ? "FAIL" : "ok", (long long)n,

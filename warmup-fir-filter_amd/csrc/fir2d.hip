@@ -18,6 +18,9 @@
 namespace fir {
 
 // Shape chosen by the A/B microbenchmark (tools/microbench/fir2d_micro.hip, profiles/).
+// Every launch stores non-temporally and remaps blocks XCD-major (fir2d_reg_kernel's NTS / XCD):
+// 4 HBM-resident 8192^2 frames per launch, packed-16 separable 26.5 -> 21.8 us per frame,
+// general packed-16 38.5 -> 35.8 us (profiles/r02/micro2d_nts_sweep.txt).
 constexpr int kVec2d = 16;       // separable path: 16 pixels per lane, 16-row strips
 constexpr int kStrip2dSep = 16;
 constexpr int kVec2dGen = 8;     // general (dot2) path: 8 pixels per lane, 16-row strips, <= 128
@@ -156,32 +159,32 @@ static hipError_t launch2d_reg(const uint8_t* x, void* y, int64_t frames, int64_
             const int pk = nowrap ? plan_pk16(t, t.col, rowt, frac) : 0;
             const dim3 gpk = fir2d_reg_grid<kVec2d, kStrip2dPk>(H, W, frames);
             if (pk == (kMode2dPk16 | kMode2dPkHi8)) {
-                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dPk, SNW | kMode2dPk16 | kMode2dPkHi8, 1, kPdPk>),
+                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dPk, SNW | kMode2dPk16 | kMode2dPkHi8, 1, kPdPk, false, true, true>),
                                    gpk, dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
                 return hipGetLastError();
             }
             if (pk == kMode2dPk16) {
-                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dPk, SNW | kMode2dPk16, 1, kPdPk>), gpk,
+                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dPk, SNW | kMode2dPk16, 1, kPdPk, false, true, true>), gpk,
                                    dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
                 return hipGetLastError();
             }
             if (pk == (kMode2dPk16 | kMode2dPkSigned)) {
-                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dPk, SNW | kMode2dPk16 | kMode2dPkSigned, 1, kPdPk>),
+                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dPk, SNW | kMode2dPk16 | kMode2dPkSigned, 1, kPdPk, false, true, true>),
                                    gpk, dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
                 return hipGetLastError();
             }
         }
         if (sep16 && nowrap)
-            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, S16 | kMode2dNoWrap, 1, kPdSep>), grid,
+            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, S16 | kMode2dNoWrap, 1, kPdSep, false, true, true>), grid,
                                dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
         else if (sep16)
-            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, S16, 1, kPdSep>), grid, dim3(kBlock), 0, s, x,
+            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, S16, 1, kPdSep, false, true, true>), grid, dim3(kBlock), 0, s, x,
                                (OutT*)y, H, W, t, 32 - acc_bits, frac);
         else if (nowrap)
-            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, kMode2dSep | kMode2dNoWrap, 1, kPdSep>), grid,
+            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, kMode2dSep | kMode2dNoWrap, 1, kPdSep, false, true, true>), grid,
                                dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
         else
-            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, kMode2dSep, 1, kPdSep>), grid, dim3(kBlock), 0, s,
+            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dSep, kMode2dSep, 1, kPdSep, false, true, true>), grid, dim3(kBlock), 0, s,
                                x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
     } else {
         // packed 16-bit pixel pairs when the whole sum provably fits 16 bits (u8 stage only)
@@ -190,27 +193,27 @@ static hipError_t launch2d_reg(const uint8_t* x, void* y, int64_t frames, int64_
             const int pk = nowrap ? plan_pk16_gen(t, hq, frac) : 0;
             const dim3 gpk = fir2d_reg_grid<kVec2dPkGen, ST>(H, W, frames);
             if (pk == (kMode2dPk16 | kMode2dPkHi8)) {
-                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dPkGen, ST, GNW | kMode2dPkHi8, 1, PD>), gpk,
+                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dPkGen, ST, GNW | kMode2dPkHi8, 1, PD, false, true, true>), gpk,
                                    dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
                 return hipGetLastError();
             }
             if (pk == kMode2dPk16) {
-                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dPkGen, ST, GNW, 1, PD>), gpk, dim3(kBlock), 0, s, x,
+                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dPkGen, ST, GNW, 1, PD, false, true, true>), gpk, dim3(kBlock), 0, s, x,
                                    (OutT*)y, H, W, t, 32 - acc_bits, frac);
                 return hipGetLastError();
             }
             if (pk == (kMode2dPk16 | kMode2dPkSigned)) {
-                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dPkGen, ST, GNW | kMode2dPkSigned, 1, PD>), gpk,
+                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dPkGen, ST, GNW | kMode2dPkSigned, 1, PD, false, true, true>), gpk,
                                    dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
                 return hipGetLastError();
             }
         }
         const dim3 grid = fir2d_reg_grid<kVec2dGen, kStrip2dGen>(H, W, frames);
         if (nowrap)
-            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dGen, kStrip2dGen, kMode2dDot2 | kMode2dNoWrap, 4, kPdGen>),
+            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dGen, kStrip2dGen, kMode2dDot2 | kMode2dNoWrap, 4, kPdGen, false, true, true>),
                                grid, dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
         else
-            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dGen, kStrip2dGen, kMode2dDot2, 4, kPdGen>), grid,
+            hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2dGen, kStrip2dGen, kMode2dDot2, 4, kPdGen, false, true, true>), grid,
                                dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
     }
     return hipGetLastError();

@@ -184,13 +184,26 @@ __device__ __forceinline__ void load_row_px(const uint8_t* __restrict__ p, bool 
     for (int i = 0; i < ND; ++i) d[i] = ok ? q[i] : 0u;
 }
 
-template <int R, int C, int STAGE, int VEC, int STRIP, int MODE, int MINW = 1, int PD = 1, bool NTL = false>
+// NTS: non-temporal output stores.  XCD: the (strip, column, frame) order is remapped so that
+// the blocks one XCD runs are consecutive strips (their R-1 overlapping rows then hit that XCD's
+// L2 instead of being fetched again through another XCD's).
+template <int R, int C, int STAGE, int VEC, int STRIP, int MODE, int MINW = 1, int PD = 1, bool NTL = false,
+          bool NTS = false, bool XCD = false>
 __global__ __launch_bounds__(kBlock, MINW) void fir2d_reg_kernel(const uint8_t* __restrict__ x,
                                                            typename OutTraits<STAGE>::T* __restrict__ y, int64_t H,
                                                            int64_t W, Taps2<R, C> taps, int shl, int frac) {
     using OutT = typename OutTraits<STAGE>::T;
+    int64_t bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    if constexpr (XCD) {  // dispatch order is x fastest, then y, then z; blocks b, b+8, ... share an XCD
+        const int64_t gx = gridDim.x, gy = gridDim.y, nb = gx * gy * gridDim.z;
+        const int64_t b = bx + gx * (by + gy * bz), q = nb / 8;
+        const int64_t p = b < q * 8 ? (b % 8) * q + b / 8 : b;
+        bx = p % gx;
+        by = (p / gx) % gy;
+        bz = p / (gx * gy);
+    }
     {  // gridDim.z frames of H x W stored back to back (one launch for a batch of frames)
-        const int64_t fo = (int64_t)blockIdx.z * H * W;
+        const int64_t fo = bz * H * W;
         x += fo;
         y += fo;
     }
@@ -202,11 +215,11 @@ __global__ __launch_bounds__(kBlock, MINW) void fir2d_reg_kernel(const uint8_t* 
     constexpr int T = STRIP + R - 1;  // input rows per strip (the strip loop is fully unrolled)
 
     const int lane = threadIdx.x & (kWave - 1);
-    const int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // vector column index
+    const int64_t v = bx * kBlock + threadIdx.x;  // vector column index
     const int64_t col0 = v * VEC;
     const bool active = col0 < W;
     const int64_t colc = active ? col0 : W - VEC;  // in-bounds column for idle lanes
-    const int64_t r0 = (int64_t)blockIdx.y * STRIP;
+    const int64_t r0 = by * STRIP;
     // halo dword: lane 0 reads the 4 pixels left of its vector, lane 63 the 4 right of it;
     // every other lane re-reads its own first dword (same cache line, value unused)
     const int64_t hraw = lane == 0 ? col0 - 4 : (lane == kWave - 1 ? col0 + VEC : col0);
@@ -412,7 +425,8 @@ __global__ __launch_bounds__(kBlock, MINW) void fir2d_reg_kernel(const uint8_t* 
                                 val[i] = o4;
                             }
                         }
-                        *reinterpret_cast<vN*>(dst) = val;  // non-temporal: 24.6 vs 24.05 us, within noise
+                        if constexpr (NTS) __builtin_nontemporal_store(val, reinterpret_cast<vN*>(dst));
+                        else *reinterpret_cast<vN*>(dst) = val;
                     } else {
                         typedef uint32_t v4 __attribute__((ext_vector_type(4)));
 #pragma unroll
@@ -420,7 +434,8 @@ __global__ __launch_bounds__(kBlock, MINW) void fir2d_reg_kernel(const uint8_t* 
                             v4 val;
 #pragma unroll
                             for (int b = 0; b < 4; ++b) val[b] = (uint32_t)(NOWRAP ? (int32_t)acc[slot][4 * i + b] >> frac : round32(acc[slot][4 * i + b], shl, frac));
-                            reinterpret_cast<v4*>(dst)[i] = val;
+                            if constexpr (NTS) __builtin_nontemporal_store(val, reinterpret_cast<v4*>(dst) + i);
+                            else reinterpret_cast<v4*>(dst)[i] = val;
                         }
                     }
                 }
