@@ -1,32 +1,46 @@
-"""Dev A/B: the headline kernel (2^28 int16 -> int32, 5-tap sharpen) from two builds of
-libfir_hip.so in one process, interleaved batches of back-to-back launches timed by HIP
-events.  Usage: python tools/lib_ab.py <lib A> <lib B> [rounds]"""
+"""Dev A/B: one register-kernel workload from two builds of libfir_hip.so in one process,
+interleaved batches of back-to-back launches timed by HIP events (outputs must be equal).
+Workloads: i16 = the headline (2^28 int16 -> int32, 5-tap sharpen), u8 = 2^28 u8 -> sat-u8 in
+4096-sample rows (5-tap sharpen), bank = the 4-filter 3-tap u8 bank (h_coeff_3tap_map).
+Usage: python tools/lib_ab.py <lib A> <lib B> [rounds] [i16|u8|bank]"""
 import ctypes
 import sys
 
 import numpy as np
 import torch
 
+SHARPEN5 = (-256, -1024, 6656, -1024, -256)
+BANK3 = (1365, 1365, 1365, 1024, 2048, 1024, -4096, 0, 4096, -512, 5120, -512)
+
 
 def main():
     libs = [ctypes.CDLL(p) for p in sys.argv[1:3]]
     rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 10
+    wl = sys.argv[4] if len(sys.argv) > 4 else "i16"
     dev = torch.device("cuda", 0)
     s = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(s)
-    x = torch.from_numpy(np.random.default_rng(1).integers(-32768, 32768, 1 << 28, dtype=np.int16)).to(dev)
-    ys = [torch.empty(x.shape, dtype=torch.int32, device=dev) for _ in libs]
-    h = (ctypes.c_int32 * 5)(-256, -1024, 6656, -1024, -256)
-    vp = ctypes.c_void_p
-    for lib in libs:
-        lib.fir1d_fixed_rows_dev.argtypes = [vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, vp,
-                                             ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp]
+    rng = np.random.default_rng(1)
+    n = 1 << 28
+    if wl == "i16":
+        x = torch.from_numpy(rng.integers(-32768, 32768, n, dtype=np.int16)).to(dev)
+        ys = [torch.empty(n, dtype=torch.int32, device=dev) for _ in libs]
+        in_dt, rows, width, stage, h, L, F = 1, 1, n, 1, SHARPEN5, 5, 1
+    else:
+        x = torch.from_numpy(rng.integers(0, 256, n, dtype=np.uint8)).to(dev)
+        F = 4 if wl == "bank" else 1
+        ys = [torch.empty(F * n, dtype=torch.uint8, device=dev) for _ in libs]
+        in_dt, rows, width, stage = 0, n // 4096, 4096, 0
+        h, L = (BANK3, 3) if wl == "bank" else (SHARPEN5, 5)
+    hc = (ctypes.c_int32 * len(h))(*h)
+    vp, ci = ctypes.c_void_p, ctypes.c_int
 
-    def run(i, n):
-        for _ in range(n):
-            rc = libs[i].fir1d_fixed_rows_dev(vp(x.data_ptr()), 1, 1, x.numel(), 1, h, 5, 12, 32, 1,
-                                              vp(ys[i].data_ptr()), vp(s.cuda_stream))
-            assert rc == 0
+    def run(i, k):
+        for _ in range(k):
+            rc = libs[i].fir1d_fixed_rows_multi_dev(vp(x.data_ptr()), ci(in_dt), ctypes.c_int64(rows),
+                                                    ctypes.c_int64(width), ci(1), hc, ci(L), ci(F), ci(12), ci(32),
+                                                    ci(stage), vp(ys[i].data_ptr()), vp(s.cuda_stream))
+            assert rc == 0, rc
     for i in range(len(libs)):
         run(i, 50)
     torch.cuda.synchronize()
@@ -42,7 +56,7 @@ def main():
             t[i].append(a.elapsed_time(b) / 50 * 1e3)
     for i, p in enumerate(sys.argv[1:3]):
         v = sorted(t[i])
-        print(f"{p}: median {v[len(v) // 2]:.1f} us  min {v[0]:.1f} us", flush=True)
+        print(f"{wl} {p}: median {v[len(v) // 2]:.1f} us  min {v[0]:.1f} us", flush=True)
 
 
 if __name__ == "__main__":

@@ -261,9 +261,9 @@ int main(int argc, char** argv) {
 
     std::vector<Variant> vs = {
         {"fir U1 coal ntst (lib)", true, launch_fir<1, kDot2 | kAcc32 | kCoal | kNtStore>, 0, {}},
-        {"lean ntst", true, launch_lean<true>, 0, {}},
-        {"lean plain st", true, launch_lean<false>, 0, {}},
+        {"fir U1 coal ntst edw", true, launch_fir<1, kDot2 | kAcc32 | kCoal | kNtStore | kEdgeDword>, 0, {}},
         {"fir U1 coal ntst (lib) b", true, launch_fir<1, kDot2 | kAcc32 | kCoal | kNtStore>, 0, {}},
+        {"fir U1 coal ntst edw b", true, launch_fir<1, kDot2 | kAcc32 | kCoal | kNtStore | kEdgeDword>, 0, {}},
         {"copy U1 coal (LDS)", false, launch_copy_coal, 0, {}},
     };
 

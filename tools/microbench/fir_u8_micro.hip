@@ -63,7 +63,7 @@ static void launch_bank(const uint8_t* x, uint8_t* y, int64_t n, hipStream_t s) 
                        dim3(kBlock), 0, s, x, y, g, t, 0, 12, ntiles);
 }
 
-template <int U>
+template <int U, bool NT = false>
 __global__ __launch_bounds__(kBlock) void copy16(const uint8_t* __restrict__ x, uint8_t* __restrict__ y, int64_t nvec) {
     typedef uint32_t v4 __attribute__((ext_vector_type(4)));
     const int lane = threadIdx.x & 63;
@@ -72,12 +72,15 @@ __global__ __launch_bounds__(kBlock) void copy16(const uint8_t* __restrict__ x, 
 #pragma unroll
     for (int u = 0; u < U; ++u) d[u] = reinterpret_cast<const v4*>(x)[w + u * 64 + lane];
 #pragma unroll
-    for (int u = 0; u < U; ++u) reinterpret_cast<v4*>(y)[w + u * 64 + lane] = d[u];
+    for (int u = 0; u < U; ++u) {
+        v4* p = reinterpret_cast<v4*>(y) + w + u * 64 + lane;
+        if (NT) __builtin_nontemporal_store(d[u], p); else *p = d[u];
+    }
 }
-template <int U>
+template <int U, bool NT = false>
 static void launch_copy(const uint8_t* x, uint8_t* y, int64_t n, hipStream_t s) {
     const int64_t nvec = n / 16;
-    hipLaunchKernelGGL((copy16<U>), dim3((unsigned)(nvec / U / kBlock)), dim3(kBlock), 0, s, x, y, nvec);
+    hipLaunchKernelGGL((copy16<U, NT>), dim3((unsigned)(nvec / U / kBlock)), dim3(kBlock), 0, s, x, y, nvec);
 }
 
 static void launch_memcpy(const uint8_t* x, uint8_t* y, int64_t n, hipStream_t s) {
@@ -121,15 +124,17 @@ int main(int argc, char** argv) {
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     constexpr int PK = kU8Dot2 | kU8Pk16;
-    std::vector<V> vs = {{"fir U4 ntst (lib)", 1, launch_fir<4, kU8Dot2 | kNtStore>, {}},
-                         {"fir U1 ntst", 1, launch_fir<1, kU8Dot2 | kNtStore>, {}},
-                         {"fir U2 ntst", 1, launch_fir<2, kU8Dot2 | kNtStore>, {}},
-                         {"fir U1 ntld+st", 1, launch_fir<1, kU8Dot2 | kNtLoad | kNtStore>, {}},
-                         {"fir U4 ntst (lib) b", 1, launch_fir<4, kU8Dot2 | kNtStore>, {}},
-                         {"bank pk16 U1 ntst (lib)", 2, launch_bank<1, PK | kNtStore>, {}},
-                         {"bank pk16 U1 ntld+st", 2, launch_bank<1, PK | kNtLoad | kNtStore>, {}},
-                         {"copy16 U1", 0, launch_copy<1>, {}},
-                         {"hipMemcpy D2D", 0, launch_memcpy, {}}};
+    constexpr int NS = kU8Dot2 | kNtStore;
+    std::vector<V> vs = {{"fir U4 ntst (lib)", 1, launch_fir<4, NS>, {}},
+                         {"fir U4 ntst pk16", 1, launch_fir<4, NS | kU8Pk16>, {}},
+                         {"fir U4 ntst pk16 edw", 1, launch_fir<4, NS | kU8Pk16 | kEdgeDword>, {}},
+                         {"fir U2 ntst pk16 edw", 1, launch_fir<2, NS | kU8Pk16 | kEdgeDword>, {}},
+                         {"fir U1 ntst pk16 edw", 1, launch_fir<1, NS | kU8Pk16 | kEdgeDword>, {}},
+                         {"fir U4 ntst pk16 edw xcd", 1, launch_fir<4, NS | kU8Pk16 | kEdgeDword | kXcd>, {}},
+                         {"fir U4 ntst (lib) b", 1, launch_fir<4, NS>, {}},
+                         {"fir U4 ntst pk16 b", 1, launch_fir<4, NS | kU8Pk16>, {}},
+                         {"copy16 U1 nt", 0, launch_copy<1, true>, {}},
+                         {"copy16 U4 nt", 0, launch_copy<4, true>, {}}};
     for (auto& v : vs) {
         if (v.kind == 0) continue;
         const int64_t nb = v.kind == 2 ? 4 * n : n;

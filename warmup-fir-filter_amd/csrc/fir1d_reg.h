@@ -43,6 +43,10 @@ enum RegFlags : int {
     kHalo = 2048,     // a shard with halos (RowGeom::halo_l / halo_r) instead of zero padding; a
                       // separate instantiation: the extra edge-load branches cost the plain
                       // kernel 1.5 % (256.9 -> 260.8 us, tools/lib_ab.py)
+    kEdgeDword = 4096,  // halo of at most one dword per side: a tile away from both buffer ends
+                        // fetches both edge dwords with ONE wave-wide dword load (lane 0: the
+                        // dword before the tile, lane 63: the dword after it) instead of two
+                        // lane-masked 16-byte loads in branches
 };
 
 // One non-temporal 16-byte row-store of the coalesced path, as inline asm: the same
@@ -472,7 +476,13 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
     for (; tile < ntiles; tile += stride) {
         const int64_t vb = tile * (kWave * U);
         uint32_t hv[4] = {0, 0, 0, 0};
-        if (lane == 0) {
+        constexpr bool EDW = (FLAGS & kEdgeDword) && NDL <= 1 && NDR <= 1;
+        if (EDW && vb > 0 && (vb + kWave * U + 1) * VEC <= total) {  // wave-uniform
+            const int64_t e = lane == 0 ? vb * VEC - EPD : (lane == kWave - 1 ? (vb + kWave * U) * VEC : vb * VEC);
+            const uint32_t d = *reinterpret_cast<const uint32_t*>(x + e);
+            hv[0] = d;  // lane 63's right seam (dword 0 of the vector after the tile)
+            hv[3] = d;  // lane 0's left seam (dword 3 of the vector before it)
+        } else if (lane == 0) {
             if (NDL > 0) {
                 if (HALO && vb == 0 && g.halo_l != nullptr)
                     load_halo_vec<InT>(g.halo_l, true, HLE, hv);

@@ -21,7 +21,13 @@ namespace fir {
 // 4 KiB; 104.6 -> 94.0 us at 2^28, micro_u8_chunks.txt), non-temporal stores 94.7 -> 82.2 us
 // (micro_u8_nts.txt).  A fused u8 bank: 1 chunk per wave with non-temporal stores (222.6 us vs
 // 229.3 at 2 chunks with plain stores).
-constexpr int kRegFlags = kCoal | kNtStore;
+// Edge dwords (kEdgeDword): one wave-wide dword load for both tile edges instead of two
+// lane-masked 16-byte loads: headline 246.6-250.6 -> 244.4-244.9 us, u8 bank 230.6 -> 224.3 us,
+// one u8 filter unchanged (profiles/r02/micro_i16_edw.txt, micro_u8_edw.txt).
+#ifndef FIR_REG_EDGE_DWORD  // overridable for A/B builds (make abreg)
+#define FIR_REG_EDGE_DWORD 1
+#endif
+constexpr int kRegFlags = kCoal | kNtStore | (FIR_REG_EDGE_DWORD ? kEdgeDword : 0);
 constexpr int kPersistBlocks = 2048;
 
 template <typename InT, int STAGE, int L, int CH, int F, int FL>
