@@ -168,9 +168,10 @@ def test_int16_to_int32_vs_oracle(name, channels, n):
                                          (np.int16, fir_hip.OUT_U8_SAT), (np.uint8, fir_hip.OUT_I32)])
 @pytest.mark.parametrize("shape", [(1, 100_003), (1, 2048), (37, 4096), (5, 1000), (3, 1001), (9, 8)])
 def test_long_filters_vs_oracle(L, dtype, stage, shape):
-    """10..64 taps: the LDS-window v_dot2 kernel (fir1d_lds.hip) for one row or rows of a
-    multiple of 8 samples (narrow rows included), the generic kernel otherwise / beyond 64 taps;
-    32- and 24-bit accumulators."""
+    """10..64 taps: the int8 matrix-core kernel (fir1d_mfma.hip) or the LDS-window v_dot2 kernel
+    (fir1d_lds.hip, int16 -> int32 below 40 taps, and ragged single rows) for one row or rows of
+    a multiple of 8 samples (narrow rows included), the generic kernel otherwise / beyond 64
+    taps; 32- and 24-bit accumulators."""
     rng = np.random.default_rng(L * 1000 + shape[1])
     info = np.iinfo(dtype)
     x = rng.integers(info.min, info.max + 1, shape, dtype=dtype)
@@ -178,6 +179,28 @@ def test_long_filters_vs_oracle(L, dtype, stage, shape):
     for acc in (32, 24):
         got = fir_hip.fir1d_fixed_rows(x, hq, 12, acc, stage)
         assert np.array_equal(got, _co().fir1d_rows(x, hq, 12, acc, stage)), acc
+
+
+@pytest.mark.parametrize("L", [10, 17, 32, 33, 48, 64])
+def test_long_filters_matrix_core_extremes(L):
+    """The int8 matrix-core path (fir1d_mfma.hip) at the edges of its signed-byte splits: taps at
+    -32768 and 32639 (the largest tap whose high byte stays a signed byte; 32640 goes to the v_dot2
+    kernel), full-range int16 samples so the 32-bit sums wrap, 32/24/20-bit accumulators, tiles cut
+    by rows of 1000 and 8 samples and by a ragged single row; u8 runs of 0 and 255 (saturation)."""
+    rng = np.random.default_rng(7000 + L)
+    co = _co()
+    for taps in (rng.choice([-32768, 32639, -1, 1, 127, 128, -128, -129, 255, -256], L).tolist(),
+                 rng.integers(-600, 600, L).tolist(), [32640] + [3] * (L - 1)):
+        for shape in [(1, 70_001), (3, 1000), (2, 4096), (40, 8)]:
+            x16 = rng.integers(-32768, 32768, shape, dtype=np.int16)
+            xu = rng.integers(0, 256, shape, dtype=np.uint8)
+            xu[:, : shape[1] // 3] = 255
+            xu[:, shape[1] // 3: shape[1] // 2] = 0
+            for acc in (32, 24, 20):
+                for stage in (fir_hip.OUT_I32, fir_hip.OUT_U8_SAT):
+                    for x in (x16, xu):
+                        got = fir_hip.fir1d_fixed_rows(x, taps, 12, acc, stage)
+                        assert np.array_equal(got, co.fir1d_rows(x, taps, 12, acc, stage)), (shape, acc, stage, x.dtype)
 
 
 def test_long_filter_large_vs_oracle():

@@ -1,7 +1,8 @@
-"""Dev probe: device-resident 1-D FIR time per launch vs tap count (2^28 int16 -> int32 and
-u8 -> sat-u8 in 4096-sample rows), HIP events around back-to-back launches.  Shows where the
-register kernel (<= 9 taps) hands over to the LDS sliding-window kernel (10..64 taps).
-Usage: python tools/long_taps_rate.py [log2n]"""
+"""Dev probe: device-resident 1-D FIR time per launch vs tap count, 2^28 samples in 4096-sample
+rows (int16 -> int32 as one row), for the four sample/stage pairs; HIP events around
+back-to-back launches.  Shows where the register kernel (<= 9 taps) hands over to the long-filter
+kernels (fir1d_mfma.hip / fir1d_lds.hip).  FIR_HIP_LIB picks another build for an A/B.
+Usage: python tools/long_taps_rate.py [taps,taps,...]"""
 import sys
 from pathlib import Path
 
@@ -15,21 +16,24 @@ from fir_hip import torch_ops  # noqa: E402
 
 
 def main():
-    log2n = int(sys.argv[1]) if len(sys.argv) > 1 else 28
-    n = 1 << log2n
+    taps = [int(t) for t in sys.argv[1].split(",")] if len(sys.argv) > 1 else [3, 5, 9, 10, 13, 17, 24, 31, 48, 64]
+    n = 1 << 28
     dev = torch.device("cuda", 0)
     s = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(s)
     rng = np.random.default_rng(3)
     x16 = torch.from_numpy(rng.integers(-32768, 32768, n, dtype=np.int16)).to(dev)
-    y32 = torch.empty(n, dtype=torch.int32, device=dev)
     x8 = torch.from_numpy(rng.integers(0, 256, (n // 4096, 4096), dtype=np.uint8)).to(dev)
-    y8 = torch.empty(x8.shape, dtype=torch.uint8, device=dev)
-    print(f"{'taps':>5s} {'i16->i32 us':>12s} {'%8TB/s':>7s} {'u8 us':>9s} {'%8TB/s':>7s}")
-    for L in (3, 5, 9, 10, 13, 17, 24, 31, 48, 64):
+    y32 = torch.empty(n, dtype=torch.int32, device=dev)
+    y8 = torch.empty(n, dtype=torch.uint8, device=dev)
+    cases = (("i16->i32", x16, y32, fir_hip.OUT_I32, 6), ("u8->u8", x8, y8.view(x8.shape), fir_hip.OUT_U8_SAT, 2),
+             ("i16->u8", x16.view(n // 4096, 4096), y8.view(n // 4096, 4096), fir_hip.OUT_U8_SAT, 3),
+             ("u8->i32", x8, y32.view(x8.shape), fir_hip.OUT_I32, 5))
+    print(f"{'taps':>5s}" + "".join(f" {c[0] + ' us':>13s} {'%8TB/s':>7s}" for c in cases))
+    for L in taps:
         hq = torch_ops.Taps(rng.integers(-2000, 2000, L).tolist())
         res = []
-        for x, y, st, bps in ((x16, y32, fir_hip.OUT_I32, 6), (x8, y8, fir_hip.OUT_U8_SAT, 2)):
+        for _, x, y, st, bps in cases:
             for _ in range(5):
                 torch_ops.fir1d_fixed_rows_dev(x, hq, 12, 32, st, out=y)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -41,7 +45,7 @@ def main():
             e1.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / reps
             res += [us, n * bps / us / 1e3 / 80]
-        print(f"{L:5d} {res[0]:12.1f} {res[1]:7.1f} {res[2]:9.1f} {res[3]:7.1f}", flush=True)
+        print(f"{L:5d}" + "".join(f" {res[2 * i]:13.1f} {res[2 * i + 1]:7.1f}" for i in range(len(cases))), flush=True)
 
 
 if __name__ == "__main__":

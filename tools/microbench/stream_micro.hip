@@ -332,6 +332,23 @@ void l_pc(const Bufs& b, hipStream_t s) {
                        (ntiles + blocks - 1) / blocks);
 }
 
+// widen_pat H=1 with the output moved OFF bytes past the allocation start (HBM channel phase
+// of the write stream relative to the read stream)
+template <int64_t OFF>
+void l_wdpat_off(const Bufs& b, hipStream_t s) {
+    hipLaunchKernelGGL((widen_pat<1, 0, 1, 256>), dim3((unsigned)(b.n / 256 / 4)), dim3(256), 0, s, b.x,
+                       reinterpret_cast<int32_t*>(reinterpret_cast<char*>(b.y) + OFF));
+}
+// 1:1 copy of the int16 input into the output buffer (16 B per lane, one 1 KiB nt store per wave)
+__global__ __launch_bounds__(256) void copy_nt(const u32x4* __restrict__ x, u32x4* __restrict__ y) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    st16<1>(y + i, __builtin_nontemporal_load(x + i));
+}
+void l_copy(const Bufs& b, hipStream_t s) {
+    hipLaunchKernelGGL(copy_nt, dim3((unsigned)(b.n * 2 / 16 / 256)), dim3(256), 0, s, reinterpret_cast<const u32x4*>(b.x),
+                       reinterpret_cast<u32x4*>(b.y));
+}
+
 template <int E>
 void l_whe(const Bufs& b, hipStream_t s) {
     hipLaunchKernelGGL((widen_half_edge<E>), dim3((unsigned)(b.n / 4 / 256)), dim3(256), 0, s, b.x, b.y, b.n / 4);
@@ -347,7 +364,7 @@ int main(int argc, char** argv) {
     if (alloc)
         CK(hipExtMallocWithFlags((void**)&b.y, b.n * 4, alloc == 1 ? hipDeviceMallocFinegrained : hipDeviceMallocUncached));
     else
-        CK(hipMalloc(&b.y, b.n * 4));
+        CK(hipMalloc(&b.y, b.n * 4 + (8 << 20)));  // + room for the output-offset variants
     printf("output allocation: %s\n", alloc == 1 ? "fine-grained" : (alloc == 3 ? "uncached" : "hipMalloc"));
     std::vector<int16_t> hx(b.n);
     uint32_t r = 12345;
@@ -360,14 +377,17 @@ int main(int argc, char** argv) {
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     const double rw = b.n * 6.0, rd = b.n * 2.0, wr = b.n * 4.0;
     std::vector<V> vs = {
-        {"widen reg K1 b256", l_widen_reg<1, 256>, rw, true, {}},
         {"widen half row nt", l_wdpat<1, 0, 1, 256>, rw, true, {}},
-        {"pc D2 nt bpc2", l_pc<2, true, 2>, rw, true, {}},
-        {"pc D3 nt bpc2", l_pc<3, true, 2>, rw, true, {}},
-        {"pc D3 nt bpc4", l_pc<3, true, 4>, rw, true, {}},
-        {"pc D4 nt bpc4", l_pc<4, true, 4>, rw, true, {}},
-        {"pc D3 bpc4", l_pc<3, false, 4>, rw, true, {}},
-        {"pc D6 nt bpc2", l_pc<6, true, 2>, rw, true, {}},
+        {"widen half row nt +4K", l_wdpat_off<4096>, rw, false, {}},
+        {"widen half row nt +64K", l_wdpat_off<65536>, rw, false, {}},
+        {"widen half row nt +1M4K", l_wdpat_off<(1 << 20) + 4096>, rw, false, {}},
+        {"widen half row nt +2M", l_wdpat_off<(2 << 20)>, rw, false, {}},
+        {"widen half row nt +3M", l_wdpat_off<(3 << 20)>, rw, false, {}},
+        {"widen half row nt +256", l_wdpat_off<256>, rw, false, {}},
+        {"widen half row nt b", l_wdpat<1, 0, 1, 256>, rw, true, {}},
+        {"copy 1:1 int16 nt", l_copy, b.n * 4.0, false, {}},
+        {"read reg K1 b256", l_read_reg<1, 256>, rd, false, {}},
+        {"write nt rows R1", l_wpat<0, 1, 1, 256>, wr, false, {}},
     };
     // correctness of every widen variant (sampled)
     std::vector<int32_t> hy(b.n);

@@ -1,0 +1,351 @@
+// fir1d_mfma.hip — long 1-D fixed-point filters (10..64 taps) on the matrix cores, SURVEY §8 a1/a6.
+//
+// Arithmetic: fir_1d/model/python/fir_1d_fixed_ref.py:95-126 (reference root): y[n] =
+// sum_t h[t] x[n - t + L/2] wrapped to acc_bits, rounded, staged (u8 saturate or int32).
+//
+// Why MFMA: past ~20 taps the v_dot2 kernel (fir1d_lds.hip) is VALU-bound (L/2 dot2 per output:
+// 432 us for 64 taps over 2^28 int16, 47 % of HBM peak).  A FIR is a Toeplitz product: with
+// tile outputs y[ts + 32n + r] (n = block 0..31, r = offset 0..31),
+//     Y[r][n] = sum_k A[r][k] * B[k][n],   A[r][k] = h[r + L/2 + P - k],   B[k][n] = x[ts + 32n + k - P],
+// one 32x32 output tile per wave of v_mfma_i32_32x32x32_i8 over K = 32 + L/2 + P (P = the left
+// halo rounded up to 8) in KS steps of 32.  The products are exact integers, so the split into
+// signed bytes only has to be exact too:
+//   samples: u8 x = xs + 128 (xs = x ^ 0x80); int16 x = 256 xh + xls + 128 (xh the high byte,
+//            xls = low byte ^ 0x80); zero padding is x = 0 (xs = -128) like every other sample;
+//   taps:    h = 256 hh + hl, hl = ((h + 128) & 255) - 128, hh = (h - hl) / 256 (a signed byte for
+//            h <= 32639; larger taps stay on the v_dot2 kernel);
+//   sum h x = 65536 sum hh xh + 256 (sum hl xh + sum hh xls) + sum hl xls + 128 sum h   (int16)
+//   sum h x = 256 sum hh xs + sum hl xs + 128 sum h                                   (u8)
+// with int32 accumulators combined mod 2^32: the reference's wrap-around sum bit for bit.
+//
+// Per wave and tile: the 1024 + K - 32 window samples are loaded one tile ahead (branch-free
+// 16-/8-byte vectors), split into signed-byte planes on the way into wave-private LDS (u8: one
+// XOR per 4 samples; int16: 6 VALU per 8), read back as B fragments (one ds_read_b128 per plane
+// and step); the tap fragments (a function of r - k only) sit in VGPRs for the whole grid-stride
+// loop.  Outputs go back through the same LDS as whole 1 KiB rows.  Rows (images) whose length
+// is a multiple of 8 are tiled row by row, samples of other rows zeroed while staging.
+#include <string>
+
+#include "fir_common.h"
+#include "fir_launch.h"
+
+namespace fir {
+
+constexpr int kMfTile = 1024;        // outputs per wave tile (32 B columns x 32 A rows)
+constexpr int kMfMaxTaps = 64;
+constexpr int kMfWaves = kBlock / kWave;
+constexpr int kMfMaxBlocks = 1024;   // grid-stride, one resident round (4 blocks per CU)
+#ifndef FIR_MFMA_MINB                // blocks per CU the register allocation must allow (A/B builds)
+#define FIR_MFMA_MINB 4
+#endif
+
+// Tap fragments by diagonal: entry e holds a signed byte of h[d + L/2 + P], d = 31 - e (d = r - k
+// of A[r][k]), 0 outside the filter.  Lane (r, h) of k-step s reads entries
+// e = 31 - r + 32 s + 16 h + j, j = 0..15 (straight from the kernarg segment, once per wave).
+struct MfmaTaps {
+    int8_t hi[128];  // hh
+    int8_t lo[128];  // hl
+};
+
+typedef int mf_i32x4 __attribute__((ext_vector_type(4)));
+typedef int mf_i32x16 __attribute__((ext_vector_type(16)));
+
+// LDS byte of window sample i: a 16-byte pad per 32 samples (48-byte rows keep the 32 lanes of a
+// B-fragment read on distinct banks)
+__host__ __device__ constexpr int mf_pos(int i) { return i + (i >> 5) * 16; }
+
+// Buffer descriptor over [p, p + bytes): loads outside it return 0, stores outside it are dropped
+// (the range check is per dword; every row or tile edge here is 8-sample aligned).  Built from
+// wave-uniform values only, so the buffer ops need no waterfall loop.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mf_rsrc(const void* p, uint32_t bytes) {
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    void* q = (void*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+constexpr int kMfAuxNt = 2;  // non-temporal cache policy of a buffer op (gfx950)
+constexpr uint32_t kMfOff = 0x80000000u;  // a voffset far outside every descriptor (zero padding)
+
+struct MfTile {
+    int64_t rs, re, ts;
+};
+
+// tile -> row bounds and start; tile and tiles_per_row are wave-uniform and below 2^32 (total <
+// 2^40 samples), so this is one 32-bit scalar division per tile, not a 64-bit VALU one
+__device__ __forceinline__ MfTile mf_tile(uint32_t tile, int64_t rowlen, uint32_t tiles_per_row) {
+    const uint32_t row = __builtin_amdgcn_readfirstlane(tile / tiles_per_row);
+    const uint32_t tr = __builtin_amdgcn_readfirstlane(tile - row * tiles_per_row);
+    MfTile t;
+    t.rs = (int64_t)row * rowlen;
+    t.re = t.rs + rowlen;
+    t.ts = t.rs + (int64_t)tr * kMfTile;
+    return t;
+}
+
+template <typename InT, int STAGE, int KS, bool ACC32, bool FAST>
+__global__ __launch_bounds__(kBlock, FIR_MFMA_MINB) void fir1d_mfma_kernel(const InT* __restrict__ x,
+                                                            typename OutTraits<STAGE>::T* __restrict__ y,
+                                                            int64_t rowlen, int64_t tiles_per_row, int64_t ntiles,
+                                                            MfmaTaps taps, int P, uint32_t bias, int shl, int frac) {
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+    constexpr bool I16 = sizeof(InT) == 2;
+    constexpr int WL = 32 * 31 + 32 * KS;  // window samples (from tile start - P)
+    constexpr int NV = WL / 8;              // 8-sample vectors
+    constexpr int NIT = (NV + kWave - 1) / kWave;
+    constexpr int PLANE = mf_pos(WL);       // bytes per byte plane
+    constexpr int WBYTES = (I16 ? 2 * PLANE : PLANE) > 4608 ? (I16 ? 2 * PLANE : PLANE) : 4608;  // + int32 output image
+    static_assert(WL <= 1088, "window exceeds the planes");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kMfWaves][WBYTES];
+
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
+    const int r = lane & 31, hf = lane >> 5;  // A row / B column, lane half
+    uint8_t* pl = lds[wv];             // xs (u8) or xls (int16) plane
+    uint8_t* ph = lds[wv] + PLANE;     // xh plane (int16)
+
+    // tap fragments A[r][32 s + 16 hf + j], j = 0..15
+    mf_i32x4 a_lo[KS], a_hi[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+        uint32_t lo[4] = {0u, 0u, 0u, 0u}, hi[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int e = 31 - r + 32 * s + 16 * hf + j;
+            lo[j / 4] |= (uint32_t)(uint8_t)taps.lo[e] << (8 * (j % 4));
+            hi[j / 4] |= (uint32_t)(uint8_t)taps.hi[e] << (8 * (j % 4));
+        }
+        a_lo[s] = mf_i32x4{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3]};
+        a_hi[s] = mf_i32x4{(int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+    const int32_t sat_hi = (256 << frac) - 1;  // FAST u8 stage: clamp the biased sum, then shift
+
+    const uint32_t step = gridDim.x * kMfWaves, nt32 = (uint32_t)ntiles, tpr = (uint32_t)tiles_per_row;
+    uint32_t tile = blockIdx.x * kMfWaves + wv;
+    // the window of a tile: 8-sample vectors v (lanes past the window re-load its last one),
+    // through a descriptor over the tile's part of its row; other rows' samples read as zeros
+    uint32_t raw[NIT][4];
+    auto load_window = [&](const MfTile& t) __attribute__((always_inline)) {
+        const int64_t w0 = t.ts - P, base = w0 > t.rs ? w0 : t.rs, end = t.re < w0 + WL ? t.re : w0 + WL;
+        const __amdgpu_buffer_rsrc_t rs = mf_rsrc(x + base, (uint32_t)((end - base) * (int64_t)sizeof(InT)));
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int v = min(it * kWave + lane, NV - 1);
+            const int64_t g = w0 + 8 * v;
+            const uint32_t off = g >= base ? (uint32_t)((g - base) * (int64_t)sizeof(InT)) : kMfOff;
+            if constexpr (I16) {
+                const mf_i32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+                raw[it][0] = q.x, raw[it][1] = q.y, raw[it][2] = q.z, raw[it][3] = q.w;
+            } else {
+                typedef int i32x2 __attribute__((ext_vector_type(2)));
+                const i32x2 q = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+                raw[it][0] = q.x, raw[it][1] = q.y, raw[it][2] = 0u, raw[it][3] = 0u;
+            }
+        }
+    };
+    if (tile < nt32) load_window(mf_tile(tile, rowlen, tpr));  // the first tile's window
+
+    // A tile's outputs leave LDS into registers at the end of its iteration and are stored one
+    // iteration later, right AFTER the next window's conversion: hipcc's wait for a prefetched
+    // window does not count stores issued after it (it drains them: vmcnt(2) with 4 stores
+    // younger), so stores placed between a window's loads and its use would be waited for
+    // every tile.  In this order the wait covers the window and older stores only.
+    constexpr int NST = STAGE == FIR_OUT_I32 ? 4 : 1;  // 16-byte stores per lane and tile
+    u4 pend[NST];
+    __amdgpu_buffer_rsrc_t pend_rd;
+    auto flush = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < NST; ++k)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(mf_i32x4, pend[k]), pend_rd,
+                                                   STAGE == FIR_OUT_I32 ? (uint32_t)(256 * k + 4 * lane) * 4u
+                                                                        : (uint32_t)(16 * lane),
+                                                   0, kMfAuxNt);
+    };
+
+    // One tile: convert its prefetched window, store the previous tile, prefetch the next window,
+    // MFMA, stage the outputs.
+    auto body = [&](uint32_t tile, bool first) __attribute__((always_inline)) {
+        const MfTile t = mf_tile(tile, rowlen, tpr);
+        const int m = (int)min((int64_t)kMfTile, t.re - t.ts);  // outputs of this tile
+
+        // ---- the window as signed-byte planes in LDS
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int v = it * kWave + lane;
+            if (NV % kWave == 0 || v < NV) {
+                const uint32_t* d = raw[it];
+                if constexpr (I16) {  // samples 2q, 2q+1 in dword q: high bytes (1, 3), low bytes (0, 2)
+                    *reinterpret_cast<u2*>(&ph[mf_pos(8 * v)]) =
+                        u2{__builtin_amdgcn_perm(d[1], d[0], 0x07050301u), __builtin_amdgcn_perm(d[3], d[2], 0x07050301u)};
+                    *reinterpret_cast<u2*>(&pl[mf_pos(8 * v)]) =
+                        u2{__builtin_amdgcn_perm(d[1], d[0], 0x06040200u) ^ 0x80808080u,
+                           __builtin_amdgcn_perm(d[3], d[2], 0x06040200u) ^ 0x80808080u};
+                } else {
+                    *reinterpret_cast<u2*>(&pl[mf_pos(8 * v)]) = u2{d[0] ^ 0x80808080u, d[1] ^ 0x80808080u};
+                }
+            }
+        }
+        if (!first) flush();  // the previous tile's outputs
+        // ---- the next tile's window goes out now, its latency hidden behind this tile's math
+        // (unconditional: past the last tile it re-loads this one, so every path into the loop
+        // header has the same memory operations in flight and the compiler's wait there stays exact)
+        load_window(mf_tile(tile + step < nt32 ? tile + step : tile, rowlen, tpr));
+        __builtin_amdgcn_wave_barrier();  // one wave's LDS ops complete in order
+        asm volatile("" ::: "memory");
+
+        // ---- Y = A B over KS k-steps: B[32 s + 16 hf + j][n = r] = window sample 32 r + 32 s + 16 hf + j
+        // one accumulator per product: each MFMA's C comes from the one issued 2 (u8) or 4 (int16)
+        // MFMAs earlier, never from the one just before it (a back-to-back dependent 32x32 MFMA
+        // stalls the wave for the whole latency: one shared middle accumulator cost int16 ~20 %)
+        mf_i32x16 acc_ll = {}, acc_mid = {}, acc_m2 = {}, acc_hh = {};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int i = mf_pos(32 * r + 32 * s + 16 * hf);
+            const mf_i32x4 b_l = *reinterpret_cast<const mf_i32x4*>(&pl[i]);
+            acc_ll = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_lo[s], b_l, acc_ll, 0, 0, 0);
+            acc_mid = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_hi[s], b_l, acc_mid, 0, 0, 0);
+            if constexpr (I16) {
+                const mf_i32x4 b_h = *reinterpret_cast<const mf_i32x4*>(&ph[i]);
+                acc_m2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_lo[s], b_h, acc_m2, 0, 0, 0);
+                acc_hh = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_hi[s], b_h, acc_hh, 0, 0, 0);
+            }
+        }
+        // u8: acc_mid = sum hh xs, acc_ll = sum hl xs; int16: acc_hh = sum hh xh,
+        // acc_mid + acc_m2 = sum hh xls + sum hl xh, acc_ll = sum hl xls
+
+        // ---- combine (mod 2^32), wrap, round; C[row][col = r]: register i is tile output
+        // 32 r + (i & 3) + 8 (i >> 2) + 4 hf.  FAST (host-proven: no wrap, no overflow of the
+        // rounding add): the bias already holds 2^(frac-1), the round is one shift.
+        int32_t q[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            uint32_t a;
+            if constexpr (I16)
+                a = ((uint32_t)(acc_mid[i] + acc_m2[i]) << 8) + (uint32_t)acc_ll[i] + ((uint32_t)acc_hh[i] << 16) + bias;
+            else
+                a = ((uint32_t)acc_mid[i] << 8) + (uint32_t)acc_ll[i] + bias;
+            if constexpr (FAST)
+                q[i] = STAGE == FIR_OUT_U8_SAT ? min(max((int32_t)a, 0), sat_hi) : (int32_t)a >> frac;
+            else
+                q[i] = round_acc<ACC32>(a, shl, frac);
+        }
+        __builtin_amdgcn_wave_barrier();  // every B read of this tile is done before LDS is reused
+        asm volatile("" ::: "memory");
+        if constexpr (STAGE == FIR_OUT_I32) {
+            // LDS image: block n at dwords [36 n, 36 n + 32) (a 16-byte pad against bank conflicts)
+            uint32_t* ob = reinterpret_cast<uint32_t*>(lds[wv]);
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4)
+                *reinterpret_cast<u4*>(&ob[36 * r + 8 * g4 + 4 * hf]) =
+                    u4{(uint32_t)q[4 * g4], (uint32_t)q[4 * g4 + 1], (uint32_t)q[4 * g4 + 2], (uint32_t)q[4 * g4 + 3]};
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            // one descriptor over the tile's m valid outputs: the stores of a partial tile that
+            // fall past m are dropped by the range check, so every tile issues the same 4 stores
+            pend_rd = mf_rsrc(y + t.ts, (uint32_t)m * 4u);
+#pragma unroll
+            for (int rho = 0; rho < 4; ++rho) {  // 1 KiB rows: outputs 256 rho + 4 lane .. + 3
+                const int o = 256 * rho + 4 * lane;
+                pend[rho] = *reinterpret_cast<const u4*>(&ob[36 * (o >> 5) + (o & 31)]);
+            }
+        } else {
+            // bytes: block n at [48 n, 48 n + 32)
+            uint8_t* ob = lds[wv];
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                uint32_t w;
+                if constexpr (FAST) {  // clamped biased sums: the byte is (c >> frac), c in [0, 2^(frac+8))
+                    w = (uint32_t)q[4 * g4] >> frac;
+                    w |= ((uint32_t)q[4 * g4 + 1] >> frac) << 8;
+                    w |= ((uint32_t)q[4 * g4 + 2] >> frac) << 16;
+                    w |= ((uint32_t)q[4 * g4 + 3] >> frac) << 24;
+                } else {
+                    w = (uint32_t)stage_out32<STAGE>(q[4 * g4]) | ((uint32_t)stage_out32<STAGE>(q[4 * g4 + 1]) << 8) |
+                        ((uint32_t)stage_out32<STAGE>(q[4 * g4 + 2]) << 16) |
+                        ((uint32_t)stage_out32<STAGE>(q[4 * g4 + 3]) << 24);
+                }
+                *reinterpret_cast<uint32_t*>(&ob[48 * r + 8 * g4 + 4 * hf]) = w;
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            const int o = 16 * lane;
+            pend[0] = *reinterpret_cast<const u4*>(&ob[48 * (o >> 5) + (o & 31)]);
+            pend_rd = mf_rsrc(y + t.ts, (uint32_t)m);
+        }
+        __builtin_amdgcn_wave_barrier();  // the output reads are done before the next tile's staging
+        asm volatile("" ::: "memory");
+    };
+    if (tile < nt32) {
+        body(tile, true);
+        tile += step;
+        for (; tile < nt32; tile += step) body(tile, false);
+        flush();  // the last tile's outputs
+    }
+}
+
+template <typename InT, int STAGE, int KS>
+static hipError_t launch_mfma_ks(const void* x, void* y, int64_t rowlen, int64_t tpr, int64_t ntiles, const MfmaTaps& t,
+                                 int P, uint32_t bias, bool fast, int frac, int acc_bits, hipStream_t s) {
+    using OutT = typename OutTraits<STAGE>::T;
+    const int64_t want = (ntiles + kMfWaves - 1) / kMfWaves;
+    const unsigned blocks = (unsigned)(want < kMfMaxBlocks ? want : kMfMaxBlocks);
+    if (fast)
+        hipLaunchKernelGGL((fir1d_mfma_kernel<InT, STAGE, KS, true, true>), dim3(blocks), dim3(kBlock), 0, s, (const InT*)x,
+                           (OutT*)y, rowlen, tpr, ntiles, t, P, bias, 0, frac);
+    else if (acc_bits == 32)
+        hipLaunchKernelGGL((fir1d_mfma_kernel<InT, STAGE, KS, true, false>), dim3(blocks), dim3(kBlock), 0, s, (const InT*)x,
+                           (OutT*)y, rowlen, tpr, ntiles, t, P, bias, 0, frac);
+    else
+        hipLaunchKernelGGL((fir1d_mfma_kernel<InT, STAGE, KS, false, false>), dim3(blocks), dim3(kBlock), 0, s,
+                           (const InT*)x, (OutT*)y, rowlen, tpr, ntiles, t, P, bias, 32 - acc_bits, frac);
+    return hipGetLastError();
+}
+
+template <typename InT, int STAGE>
+static hipError_t launch_mfma_t(const void* x, void* y, int64_t rows, int64_t rowlen, int64_t total, const int32_t* hq,
+                                int L, int frac, int acc_bits, hipStream_t s) {
+    const int c = L / 2, hl = L - 1 - c;
+    const int P = (hl + 7) & ~7;
+    const int K = 32 + c + P, KS = (K + 31) / 32;  // 2..3
+    MfmaTaps t;
+    for (int e = 0; e < 128; ++e) {
+        const int tap = 31 - e + c + P;
+        const int v = tap >= 0 && tap < L ? hq[tap] : 0;
+        const int lo = ((v + 128) & 255) - 128;  // balanced split: v = 256 hi + lo
+        t.lo[e] = (int8_t)lo;
+        t.hi[e] = (int8_t)((v - lo) / 256);
+    }
+    int64_t hsum = 0, habs = 0;
+    for (int k = 0; k < L; ++k) hsum += hq[k], habs += hq[k] < 0 ? -(int64_t)hq[k] : hq[k];
+    uint32_t bias = (uint32_t)(128 * hsum);  // mod 2^32
+    // FAST: no sum can wrap acc_bits, nor overflow int32 once the rounding half is added
+    const int64_t xmax = sizeof(InT) == 1 ? 255 : 32768;
+    const bool fast = frac <= 22 && habs * xmax + ((int64_t)1 << (frac - 1)) < ((int64_t)1 << (acc_bits - 1));
+    if (fast) bias += 1u << (frac - 1);
+    const int64_t rl = rows > 1 ? rowlen : total;
+    const int64_t tpr = (rl + kMfTile - 1) / kMfTile;
+    const int64_t ntiles = (rows > 1 ? rows : 1) * tpr;
+    if (KS == 2) return launch_mfma_ks<InT, STAGE, 2>(x, y, rl, tpr, ntiles, t, P, bias, fast, frac, acc_bits, s);
+    return launch_mfma_ks<InT, STAGE, 3>(x, y, rl, tpr, ntiles, t, P, bias, fast, frac, acc_bits, s);
+}
+
+bool mfma_path_ok(const void* x, const void* y, int in_dtype, int64_t rows, int64_t rowlen, int64_t total, int ch,
+                  const int32_t* hq, int L, int frac, int acc_bits) {
+    bool taps_ok = true;  // the high byte of the balanced split must be a signed byte
+    for (int k = 0; k < L; ++k) taps_ok &= hq[k] >= -32768 && hq[k] <= 32639;
+    return L >= 2 && L <= kMfMaxTaps && ch == 1 && taps_ok && acc_bits <= 32 && frac <= 31 &&
+           (rows == 1 ? total : rowlen) % 8 == 0 &&  // row and tile edges on 8-sample vectors
+           (uintptr_t)x % (in_dtype == FIR_IN_U8 ? 8 : 16) == 0 && (uintptr_t)y % 16 == 0 && total >= 8 &&
+           total < ((int64_t)1 << 40);
+}
+
+hipError_t launch_fir1d_mfma(const void* x, int in_dtype, int64_t rows, int64_t rowlen, int64_t total,
+                             const int32_t* hq, int L, int frac, int acc_bits, int stage, void* y, hipStream_t s) {
+    if (in_dtype == FIR_IN_U8)
+        return stage == FIR_OUT_U8_SAT ? launch_mfma_t<uint8_t, FIR_OUT_U8_SAT>(x, y, rows, rowlen, total, hq, L, frac, acc_bits, s)
+                                       : launch_mfma_t<uint8_t, FIR_OUT_I32>(x, y, rows, rowlen, total, hq, L, frac, acc_bits, s);
+    return stage == FIR_OUT_U8_SAT ? launch_mfma_t<int16_t, FIR_OUT_U8_SAT>(x, y, rows, rowlen, total, hq, L, frac, acc_bits, s)
+                                   : launch_mfma_t<int16_t, FIR_OUT_I32>(x, y, rows, rowlen, total, hq, L, frac, acc_bits, s);
+}
+
+}  // namespace fir

@@ -14,6 +14,12 @@ int launch_fir1d_rows(const void* x, int in_dtype, int64_t rows, int64_t width, 
 
 // Long filters (up to 64 taps, one channel, int16 taps, acc_bits <= 32): the LDS-window
 // v_dot2 kernel (fir1d_lds.hip).  lds_path_ok says whether it applies.
+// Long filters on the matrix cores (fir1d_mfma.hip): 2..64 int16 taps, one channel,
+// acc_bits <= 32, one row or rows of a multiple of 8 samples, aligned buffers.
+bool mfma_path_ok(const void* x, const void* y, int in_dtype, int64_t rows, int64_t rowlen, int64_t total, int ch,
+                  const int32_t* hq, int L, int frac, int acc_bits);
+hipError_t launch_fir1d_mfma(const void* x, int in_dtype, int64_t rows, int64_t rowlen, int64_t total,
+                             const int32_t* hq, int L, int frac, int acc_bits, int stage, void* y, hipStream_t s);
 bool lds_path_ok(const void* x, const void* y, int in_dtype, int64_t rows, int64_t rowlen, int64_t total, int ch,
                  const int32_t* hq, int L, int frac, int acc_bits);
 hipError_t launch_fir1d_lds(const void* x, int in_dtype, int64_t rows, int64_t rowlen, int64_t total,
