@@ -80,9 +80,11 @@ SEP_KERNELS = [  # (col, row): rank-1 kernels reaching each separable variant
 # clamped shift of 4 at frac 8, and sep16 at frac 16 (its 16-bit sum would overflow there).
 
 
+@pytest.mark.parametrize("path", ["auto", "mfma"])
 @pytest.mark.parametrize("k", range(len(SEP_KERNELS)))
 @pytest.mark.parametrize("shape", [(1, 16), (29, 64), (64, 1280), (300, 4096 + 16)])
-def test_fir2d_separable_variants_vs_oracle(k, shape):
+def test_fir2d_separable_variants_vs_oracle(k, shape, path, monkeypatch):
+    monkeypatch.setenv("FIR2D_PATH", path)  # rank-1 kernels: register form by default, or MFMA
     col, row = SEP_KERNELS[k]
     hq = np.outer(np.array(col, np.int64), np.array(row, np.int64))
     rng = np.random.default_rng(k * 7 + shape[0])
@@ -108,9 +110,11 @@ GEN_PK_KERNELS = [  # non-separable kernels reaching the general packed-16 forms
 # 16-bit shifts (f - s > 15) or the range and fall back to v_dot2; acc 24 keeps the no-wrap proof.
 
 
+@pytest.mark.parametrize("path", ["auto", "reg"])
 @pytest.mark.parametrize("k", range(len(GEN_PK_KERNELS)))
 @pytest.mark.parametrize("shape", [(1, 16), (29, 64), (64, 1280), (300, 4096 + 16)])
-def test_fir2d_general_packed16_vs_oracle(k, shape):
+def test_fir2d_general_packed16_vs_oracle(k, shape, path, monkeypatch):
+    monkeypatch.setenv("FIR2D_PATH", path)  # general kernels: MFMA by default, or the register form
     hq = np.array(GEN_PK_KERNELS[k], np.int64)
     rng = np.random.default_rng(k * 11 + shape[0])
     x = rng.integers(0, 256, shape, dtype=np.uint8)
@@ -122,13 +126,63 @@ def test_fir2d_general_packed16_vs_oracle(k, shape):
                                   co.fir2d(x, hq, frac, acc, stage)), (frac, acc, stage)
 
 
-def test_fir2d_full_frame_8192_general():
-    """configs[4] frame with a non-separable 5x5 kernel (general packed-16 form)."""
+@pytest.mark.parametrize("path", ["auto", "reg"])
+def test_fir2d_full_frame_8192_general(path, monkeypatch):
+    """configs[4] frame with a non-separable 5x5 kernel (MFMA by default, general packed-16 form)."""
+    monkeypatch.setenv("FIR2D_PATH", path)
     x = np.random.default_rng(20260228).integers(0, 256, (8192, 8192), dtype=np.uint8)
     hq = np.array(GEN_PK_KERNELS[6], np.int64)
     y = torch_ops.fir2d_fixed_dev(torch.from_numpy(x).to(DEV), hq)
     torch.cuda.synchronize()
     assert np.array_equal(y.cpu().numpy(), c_oracle().fir2d(x, hq))
+
+
+MFMA_KERNELS = [  # fir2d_mfma.hip: one tap byte plane after the power-of-two factor, or two
+    np.random.default_rng(55).integers(-4, 5, (5, 5)),                # 1 plane
+    np.random.default_rng(7).integers(-3000, 3000, (5, 5)),           # 2 planes (Q4.12-sized)
+    np.random.default_rng(8).integers(-32768, 32640, (5, 5)),         # 2 planes, wraps 32 bits
+    np.random.default_rng(9).integers(-100, 100, (3, 4)),             # even width: halo 1 + 2
+    np.random.default_rng(10).integers(-100, 100, (5, 2)),
+    np.array([[2], [-1], [7], [-1], [2]]) * 64,                       # column filter, s = 6
+    np.random.default_rng(11).integers(-127, 128, (3, 5)) | 1,        # odd taps: s = 0
+    np.zeros((5, 5), np.int64),                                       # all zero
+]
+
+
+@pytest.mark.parametrize("k", range(len(MFMA_KERNELS)))
+@pytest.mark.parametrize("shape", [(1, 16), (2, 1024), (7, 48), (33, 1040), (100, 4096 + 16), (37, 3072 + 512)])
+def test_fir2d_mfma_vs_oracle(k, shape, monkeypatch):
+    """The matrix-core path forced on: ragged widths (partial 1024-pixel tiles), heights that
+    are not a whole strip, saturating corners, every bit width class (fast byte-2 form at
+    frac <= 16, rounded wrap form above it or when the sum can wrap)."""
+    monkeypatch.setenv("FIR2D_PATH", "mfma")
+    hq = MFMA_KERNELS[k]
+    rng = np.random.default_rng(k * 13 + shape[0])
+    x = rng.integers(0, 256, shape, dtype=np.uint8)
+    x[0, : min(32, shape[1])] = 255
+    x[-1, -min(32, shape[1]):] = 0
+    co = c_oracle()
+    for frac, acc in ((12, 32), (8, 24), (16, 32), (10, 32), (20, 32), (12, 20)):
+        assert np.array_equal(fir_hip.fir2d_fixed(x, hq, frac, acc, fir_hip.OUT_U8_SAT),
+                              co.fir2d(x, hq, frac, acc, 0)), (frac, acc)
+
+
+def test_fir2d_mfma_frames_and_full_frame(monkeypatch):
+    """Batched frames and the configs[4] frame size on the matrix-core path, rank-1 bench kernel
+    included (forced: by default it stays on the separable register form)."""
+    monkeypatch.setenv("FIR2D_PATH", "mfma")
+    rng = np.random.default_rng(91)
+    co = c_oracle()
+    x = rng.integers(0, 256, (3, 70, 2048 + 64), dtype=np.uint8)
+    for hq in (MFMA_KERNELS[0], MFMA_KERNELS[1]):
+        got = fir_hip.fir2d_fixed(x, hq)
+        for f in range(3):
+            assert np.array_equal(got[f], co.fir2d(x[f], hq, 12, 32, 0)), f
+    xf = rng.integers(0, 256, (8192, 8192), dtype=np.uint8)
+    sep = np.outer([256, 1024, 1536, 1024, 256], [256, 1024, 1536, 1024, 256]) // 4096
+    y = torch_ops.fir2d_fixed_dev(torch.from_numpy(xf).to(DEV), sep)
+    torch.cuda.synchronize()
+    assert np.array_equal(y.cpu().numpy(), co.fir2d(xf, sep))
 
 
 def test_fir2d_frame_batches_device_and_host():

@@ -9,6 +9,8 @@
 // DPP wave shifts, and the vertical (R-1)-row halo is carried in a register ring of R
 // partial-output rows (input-stationary, no LDS, no re-read inside a strip).
 // fir2d_generic_kernel handles every other shape/width/alignment.
+#include <cstdlib>
+#include <cstring>
 #include <string>
 
 #include "fir2d_reg.h"
@@ -230,6 +232,13 @@ static hipError_t launch2d_reg_shape(int R, int C, const uint8_t* x, void* y, in
     return hipErrorInvalidValue;
 }
 
+// rank-1 kernels have a register form with R + C/2 MACs per pixel; measured against the MFMA path
+// in profiles/r02 (the default dispatch keeps the faster one)
+static bool sep2d_register_form(const int32_t* hq, int R, int C) {
+    int32_t col[FIR_MAX_TAPS], row[FIR_MAX_TAPS];
+    return R > 1 && C > 1 && rank1_factor(hq, R, C, col, row);
+}
+
 static bool reg2d_shape(int R, int C) { return (R == 1 || R == 3 || R == 5) && (C == 1 || C == 3 || C == 5); }
 
 int launch_fir2d(const uint8_t* x, int64_t frames, int64_t H, int64_t W, const int32_t* hq, int R, int C, int frac,
@@ -247,8 +256,16 @@ int launch_fir2d(const uint8_t* x, int64_t frames, int64_t H, int64_t W, const i
     for (int k = 0; k < R * C; ++k) taps16 &= (hq[k] >= -32768 && hq[k] <= 32767);
     const bool fast = reg2d_shape(R, C) && W % kVec2d == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)y % 16 == 0 &&
                       acc_bits <= 32 && frac <= 31 && taps16 && W >= kVec2d;
-    hipError_t e;
-    if (fast) {
+    hipError_t e = hipErrorNotSupported;
+    // matrix-core path (fir2d_mfma.hip) unless FIR2D_PATH=reg; rank-1 kernels keep the packed-16
+    // separable register form by default (FIR2D_PATH=mfma takes the MFMA path for them too)
+    const char* path = getenv("FIR2D_PATH");
+    const bool force = path && !strcmp(path, "mfma"), off = path && !strcmp(path, "reg");
+    if (!off && (force || !sep2d_register_form(hq, R, C)))
+        e = launch_fir2d_mfma(x, frames, H, W, hq, R, C, frac, acc_bits, stage, y, stream);
+    if (e != hipErrorNotSupported) {
+        // launched (or failed to launch) on the matrix cores
+    } else if (fast) {
         e = stage == FIR_OUT_U8_SAT ? launch2d_reg_shape<FIR_OUT_U8_SAT>(R, C, x, y, frames, H, W, hq, frac, acc_bits, stream)
                                     : launch2d_reg_shape<FIR_OUT_I32>(R, C, x, y, frames, H, W, hq, frac, acc_bits, stream);
     } else {

@@ -41,6 +41,10 @@ int launch_fir1d_segment(const void* x, int in_dtype, int64_t n, int ch, const i
                          hipStream_t stream, std::string* err);
 
 // 2-D fixed FIR over `frames` uint8 frames of height x width stored back to back (one launch).
+// 2-D u8 -> sat-u8 frames on the int8 matrix cores (fir2d_mfma.hip); hipErrorNotSupported when
+// the shape, alignment or taps are outside its cover (the caller then takes fir2d_reg_kernel)
+hipError_t launch_fir2d_mfma(const uint8_t* x, int64_t frames, int64_t H, int64_t W, const int32_t* hq, int R, int C,
+                             int frac, int acc_bits, int stage, void* y, hipStream_t s);
 int launch_fir2d(const uint8_t* x, int64_t frames, int64_t height, int64_t width, const int32_t* hq, int tap_rows,
                  int tap_cols, int frac, int acc_bits, int stage, void* y, hipStream_t stream, std::string* err);
 
