@@ -95,7 +95,7 @@ def timing(reps: int = 200) -> None:
                 us = e0.elapsed_time(e1) * 1000 / reps
                 res.setdefault((name, path), []).append(us)
                 print(f"round {rnd} {name:9s} {path:5s} {us:8.1f} us / 4 frames = {us / 4:6.2f} us/frame "
-                      f"({2 * 4 * 8192 * 8192 / us / 1e6 / 8000 * 100:5.1f} % of 8 TB/s)", flush=True)
+                      f"({2 * 4 * 8192 * 8192 / us / 8e6 * 100:5.1f} % of 8 TB/s)", flush=True)
     print("best of rounds:")
     for (name, path), v in res.items():
         print(f"  {name:9s} {path:5s} {min(v):8.1f} us ({min(v) / 4:6.2f} us/frame)")

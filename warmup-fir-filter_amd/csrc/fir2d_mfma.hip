@@ -34,11 +34,20 @@
 namespace fir {
 
 constexpr int kM2Tile = 1024;   // output pixels per wave and row (32 blocks of 32)
-constexpr int kM2Ring = 8;      // input rows in the register ring (R used + 8 - R in flight)
+#ifndef FIR2D_MFMA_RING         // input rows in the register ring (R used + RING - R in flight)
+#define FIR2D_MFMA_RING 8
+#endif
+constexpr int kM2Ring = FIR2D_MFMA_RING;
 constexpr int kM2MaxR = 7;
 constexpr int kM2MaxC = 5;      // horizontal halo <= 2 pixels per side
 #ifndef FIR2D_MFMA_STRIP        // output rows per wave (A/B builds)
 #define FIR2D_MFMA_STRIP 32
+#endif
+#ifndef FIR2D_MFMA_LDS_STORE    // outputs through LDS into lane-contiguous 16-byte pieces
+#define FIR2D_MFMA_LDS_STORE 1
+#endif
+#ifndef FIR2D_MFMA_COLFAST       // wave order: column tiles fastest (1) or strips fastest (0)
+#define FIR2D_MFMA_COLFAST 1
 #endif
 #ifndef FIR2D_MFMA_MINW
 #define FIR2D_MFMA_MINW 3
@@ -91,7 +100,12 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
     // addressing below is scalar
     const uint32_t w = __builtin_amdgcn_readfirstlane(b * (kBlock / kWave) + (threadIdx.x >> 6));
     if (w >= nwaves) return;  // wave-uniform
+#if FIR2D_MFMA_COLFAST
+    // column tiles fastest: the 4 waves of a block read 4 KiB contiguous of each row
+    const uint32_t col = w % ncol, strip = (w / ncol) % nstrip, frame = w / (nstrip * ncol);
+#else
     const uint32_t strip = w % nstrip, col = (w / nstrip) % ncol, frame = w / (nstrip * ncol);
+#endif
     const int64_t fo = (int64_t)frame * H * W;
     const uint8_t* xf = x + fo;
     uint8_t* yf = y + fo;
@@ -129,11 +143,20 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
     // edge dword: lane 63 (never a left-halo source) the 4 pixels left of the tile, lane 0
     // (never a right-halo source) the 4 right of it
     const uint32_t eoff = lane == 63 ? (j0 >= 4 ? (uint32_t)j0 - 4u : kM2Off) : (lane == 0 ? (uint32_t)j0 + kM2Tile : kM2Off);
+    // rows outside the frame: a descriptor of 0 bytes (every load of it returns 0)
     auto load_row = [&](int64_t rho, int slot) __attribute__((always_inline)) {
         const bool in = rho >= 0 && rho < H;
-        const __amdgpu_buffer_rsrc_t rs = m2_rsrc(xf + (in ? rho : 0) * W, wb);
-        ring[slot] = __builtin_bit_cast(m2_u4, __builtin_amdgcn_raw_buffer_load_b128(rs, in ? voff : kM2Off, 0, 0));
-        edge[slot] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, in ? eoff : kM2Off, 0, 0);
+        const __amdgpu_buffer_rsrc_t rs = m2_rsrc(xf + (in ? rho : 0) * W, in ? wb : 0u);
+#if FIR2D_MFMA_COPYONLY >= 3  // twin with lane-contiguous loads
+        ring[slot] = __builtin_bit_cast(m2_u4, __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)j0 + 16u * lane, 0, 0));
+#else
+        ring[slot] = __builtin_bit_cast(m2_u4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0));
+#endif
+#if FIR2D_MFMA_COPYONLY == 2 || FIR2D_MFMA_COPYONLY == 4
+        edge[slot] = 0u;
+#else
+        edge[slot] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, eoff, 0, 0);
+#endif
     };
     // signed bytes and the halo dword [x(32n-2), x(32n-1), x(32n+32), x(32n+33)] of block n
     const int srcl = 4 * (32 + ((n + 31) & 31)), srcr = 4 * ((n + 1) & 31);
@@ -147,23 +170,74 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
         tl[slot] = __builtin_amdgcn_perm(r, l, 0x05040302u);  // l.b2, l.b3, r.b0, r.b1
     };
 
-    // rows i0 - U .. i0 + D + PD - 1 into slots 0 .. 6; slot(rho) = (rho - i0 + U) % 8
+    // rows i0 - U .. i0 + D + PD - 1 into slots 0 .. RING - 2; slot(rho) = (rho - i0 + U) % RING
 #pragma unroll
     for (int s = 0; s < kM2Ring - 1; ++s) load_row(i0 - U + s, s);
 #pragma unroll
     for (int s = 0; s < R - 1; ++s) prep_row(s);
 
-    m2_u4 pend = {0u, 0u, 0u, 0u};
-    __amdgpu_buffer_rsrc_t pend_rd = m2_rsrc(yf, wb);
-    uint32_t pend_off = kM2Off;
-    auto flush = [&]() __attribute__((always_inline)) {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(m2_i32x4, pend), pend_rd, pend_off, 0, kM2AuxNt);
-    };
     const int32_t sat_hi = 0xFFFFFF;
     const uint32_t hmask = hf ? 0xFFFFFFFFu : 0u;
     uint32_t shv;  // the shift in a VGPR (gfx9 VOP3: one SGPR operand per instruction)
     asm("v_mov_b32 %0, %1" : "=v"(shv) : "s"(sh));
 
+    // ---- stage of one output row, 4 of its 16 outputs (group gi): register e of lane (n, hf) is
+    // output pixel 32n + (e & 3) + 8 (e >> 2) + 4 hf; the byte ends up in bits 16..23
+    auto stage4 = [&](const m2_i32x16& acc, const m2_i32x16& acch, int gi) __attribute__((always_inline)) {
+        uint32_t c[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = 4 * gi + q;
+            uint32_t a = (uint32_t)acc[e];
+            if constexpr (NP == 2) a += (uint32_t)acch[e] << 8;
+            if constexpr (FAST) {
+                // (sum + 2^(f-1)) << (16 - f), clamped.  Plain C for the first use of the MFMA
+                // result (v_add_lshl_u32: the shift is in a VGPR): hipcc does not pad inline asm
+                // that reads an MFMA destination with the wait states it needs (measured: wrong
+                // bytes 0, 1 of every block)
+                const uint32_t v = (a + bias) << shv;
+                asm("v_med3_i32 %0, %1, 0, %2" : "=v"(c[q]) : "v"(v), "s"(sat_hi));
+            } else {
+                c[q] = (uint32_t)min(max(round_acc<ACC32>((a + bias) << sh, shl, frac), 0), 255) << 16;
+            }
+        }
+        const uint32_t lo = __builtin_amdgcn_perm(c[1], c[0], 0x0C0C0602u);  // c0.b2, c1.b2
+        const uint32_t hi = __builtin_amdgcn_perm(c[3], c[2], 0x06020C0Cu);  // c2.b2, c3.b2 in bytes 2, 3
+        return lo | hi;
+    };
+    // lane n: bytes 32n + 0..15, lane n + 32: bytes 32n + 16..31 (two v_permlane32_swap), then
+    // (FIR2D_MFMA_LDS_STORE) through 1 KiB of wave-private LDS so that lane L stores bytes
+    // 16L..16L+15: each 16-lane pass of the store then writes 256 contiguous bytes, whole lines,
+    // instead of every other 16 bytes of 512.  One non-temporal store, dropped when the row is
+    // outside the strip or the frame.
+#if FIR2D_MFMA_LDS_STORE
+    __shared__ __attribute__((aligned(16))) uint8_t obuf[kBlock / kWave][kM2Tile];
+    uint8_t* ob = obuf[threadIdx.x >> 6];
+    const uint32_t soff = (uint32_t)j0 + 16u * lane;
+#else
+    const uint32_t soff = voff;
+#endif
+    auto store_row = [&](const uint32_t* g, int64_t i, bool ok) __attribute__((always_inline)) {
+        const auto s02 = __builtin_amdgcn_permlane32_swap(g[0], g[2], false, false);
+        const auto s13 = __builtin_amdgcn_permlane32_swap(g[1], g[3], false, false);
+        m2_u4 v = m2_u4{s02[0], s02[1], s13[0], s13[1]};
+#if FIR2D_MFMA_LDS_STORE
+        *reinterpret_cast<m2_u4*>(ob + 32 * n + 16 * hf) = v;
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        v = *reinterpret_cast<const m2_u4*>(ob + 16 * lane);
+        __builtin_amdgcn_wave_barrier();  // the read is done before the next row's write
+        asm volatile("" ::: "memory");
+#endif
+        const bool in = ok && i < H;
+        const __amdgpu_buffer_rsrc_t rs = m2_rsrc(yf + (in ? i : 0) * W, in ? wb : 0u);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(m2_i32x4, v), rs, soff, 0, kM2AuxNt);
+    };
+
+    // Software-pipelined by one row: iteration i issues the MFMAs of output row i into one
+    // accumulator pair and, between them, stages row i - 1 out of the other, so the matrix
+    // core and the VALU work at the same time inside a wave.
+    m2_i32x16 acc[2] = {}, acch[2] = {};
     for (int64_t iq = i0; iq < i0 + kM2Strip; iq += kM2Ring) {
 #pragma unroll
         for (int k = 0; k < kM2Ring; ++k) {
@@ -171,64 +245,55 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
             // keep each iteration's instructions in place: hipcc otherwise hoists a row's signed-
             // byte XOR up to its load, several iterations early, and waits for that load there
             __builtin_amdgcn_sched_barrier(0);
-            prep_row((k + U + D) % kM2Ring);            // row i + D has arrived
-            flush();                                     // output row i - 1
-            load_row(i + D + PD, (k + U + D + PD) % kM2Ring);  // slot of row i - U (done last iteration)
+            prep_row((k + U + D) % kM2Ring);                   // row i + D has arrived
+            load_row(i + D + PD, (k + U + D + PD) % kM2Ring);  // slot of row i - U - 1
 
-            // ---- Y = sum_m A_m B_{i-m+D} + A_tail B_tail: one accumulator per tap byte plane (a
-            // single dependent chain of 32x32 MFMAs issues at the full rate, MI355X_MICROARCH.md)
-            m2_i32x16 acc = {}, acch = {};
-#pragma unroll
-            for (int mm = 0; mm < R; ++mm) {  // input row i - U + mm, tap row R - 1 - mm
-                const m2_i32x4 bv = __builtin_bit_cast(m2_i32x4, ring[(k + mm) % kM2Ring]);
-                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(am[0][R - 1 - mm], bv, acc, 0, 0, 0);
-                if constexpr (NP == 2) acch = __builtin_amdgcn_mfma_i32_32x32x32_i8(am[1][R - 1 - mm], bv, acch, 0, 0, 0);
-            }
+#if FIR2D_MFMA_COPYONLY  // memory-only twin (A/B builds): the same loads and stores, no arithmetic
             {
-                uint32_t tv[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {  // a bit-select, not a select of array elements (hipcc
-                    // turns that into a dynamically indexed array and moves the ring to LDS)
-                    const uint32_t lo = tl[(k + q) % kM2Ring], hi = tl[(k + 4 + q) % kM2Ring];
-                    tv[q] = (hi & hmask) | (lo & ~hmask);
-                }
-                const m2_i32x4 bt = m2_i32x4{(int)tv[0], (int)tv[1], (int)tv[2], (int)tv[3]};
-                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(at[0], bt, acc, 0, 0, 0);
-                if constexpr (NP == 2) acch = __builtin_amdgcn_mfma_i32_32x32x32_i8(at[1], bt, acch, 0, 0, 0);
+                const m2_u4 rv = ring[(k + U) % kM2Ring];
+                const uint32_t g[4] = {rv.x, rv.y, rv.z, rv.w};
+                store_row(g, i - 1, k > 0 || iq > i0);
+                continue;
             }
-
-            // ---- stage: register e of lane (n, hf) is output pixel 32n + (e & 3) + 8 (e >> 2) + 4 hf
+#endif
+            m2_i32x16& a = acc[k & 1];
+            m2_i32x16& ah = acch[k & 1];
+            const m2_i32x16& pa = acc[(k + 1) & 1];
+            const m2_i32x16& pah = acch[(k + 1) & 1];
             uint32_t g[4];
 #pragma unroll
-            for (int gi = 0; gi < 4; ++gi) {
-                uint32_t c[4];
+            for (int mm = 0; mm < R + 1; ++mm) {
+                m2_i32x4 bv, av0, av1;
+                if (mm < R) {  // input row i - U + mm, tap row R - 1 - mm
+                    bv = __builtin_bit_cast(m2_i32x4, ring[(k + mm) % kM2Ring]);
+                    av0 = am[0][mm < R ? R - 1 - mm : 0];
+                    if constexpr (NP == 2) av1 = am[1][mm < R ? R - 1 - mm : 0];
+                } else {  // the tail: halo dwords of rows i - U + q (lanes h = 0), i - U + 4 + q (h = 1)
+                    uint32_t tv[4];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int e = 4 * gi + q;
-                    uint32_t a = (uint32_t)acc[e];
-                    if constexpr (NP == 2) a += (uint32_t)acch[e] << 8;
-                    if constexpr (FAST) {
-                        uint32_t v;  // (sum + 2^(f-1)) << (16 - f), clamped: the byte is bits 16..23
-                        asm("v_add_lshl_u32 %0, %1, %2, %3" : "=v"(v) : "v"(a), "s"(bias), "v"(shv));
-                        asm("v_med3_i32 %0, %1, 0, %2" : "=v"(c[q]) : "v"(v), "s"(sat_hi));
-                    } else {
-                        c[q] = (uint32_t)min(max(round_acc<ACC32>((a + bias) << sh, shl, frac), 0), 255) << 16;
+                    for (int q = 0; q < 4; ++q) {  // a bit-select, not a select of array elements
+                        // (hipcc turns that into a dynamically indexed array in LDS)
+                        const uint32_t lo = tl[(k + q) % kM2Ring], hi = tl[(k + 4 + q) % kM2Ring];
+                        tv[q] = (hi & hmask) | (lo & ~hmask);
                     }
+                    bv = m2_i32x4{(int)tv[0], (int)tv[1], (int)tv[2], (int)tv[3]};
+                    av0 = at[0];
+                    if constexpr (NP == 2) av1 = at[1];
                 }
-                const uint32_t lo = __builtin_amdgcn_perm(c[1], c[0], 0x0C0C0602u);  // c0.b2, c1.b2
-                const uint32_t hi = __builtin_amdgcn_perm(c[3], c[2], 0x06020C0Cu);  // c2.b2, c3.b2 in bytes 2, 3
-                g[gi] = lo | hi;
+                a = __builtin_amdgcn_mfma_i32_32x32x32_i8(av0, bv, mm ? a : m2_i32x16{}, 0, 0, 0);
+                if constexpr (NP == 2) ah = __builtin_amdgcn_mfma_i32_32x32x32_i8(av1, bv, mm ? ah : m2_i32x16{}, 0, 0, 0);
+                if (mm < 4) g[mm] = stage4(pa, pah, mm);  // row i - 1, between the MFMAs
             }
-            // lane n: bytes 32n + 0..15, lane n + 32: bytes 32n + 16..31
-            const auto s02 = __builtin_amdgcn_permlane32_swap(g[0], g[2], false, false);
-            const auto s13 = __builtin_amdgcn_permlane32_swap(g[1], g[3], false, false);
-            pend = m2_u4{s02[0], s02[1], s13[0], s13[1]};
-            const bool iin = i < H;
-            pend_rd = m2_rsrc(yf + (iin ? i : 0) * W, wb);
-            pend_off = iin ? voff : kM2Off;
+            store_row(g, i - 1, k > 0 || iq > i0);
         }
     }
-    flush();
+    {  // the strip's last row
+        constexpr int kl = (kM2Strip - 1) % kM2Ring;
+        uint32_t g[4];
+#pragma unroll
+        for (int gi = 0; gi < 4; ++gi) g[gi] = stage4(acc[kl & 1], acch[kl & 1], gi);
+        store_row(g, i0 + kM2Strip - 1, true);
+    }
 }
 
 template <int R, int NP>
