@@ -76,8 +76,8 @@ constexpr int kM2AuxNt = 2;                // non-temporal cache policy (gfx950)
 constexpr uint32_t kM2Off = 0x80000000u;   // a voffset outside every descriptor: loads 0, stores dropped
 
 // R: tap rows; NP: tap byte planes (1 or 2); FAST: host-proven no wrap, f <= 16 and
-// (255 sum|h| + 2^(f-1)) 2^(16-f) < 2^31, so (sum + 2^(f-1)) << (16 - f) clamped to
-// [0, 2^24) holds the output byte in bits 16..23.
+// (255 sum|h| + 2^(f-1)) 2^(16-f) < 2^31, so bits 16..31 of (sum + 2^(f-1)) << (16 - f) are the
+// rounded output as an int16, saturated to u8 by v_sat_pk_u8_i16.
 template <int R, int NP, bool FAST, bool ACC32>
 __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_mfma_kernel(
     const uint8_t* __restrict__ x, uint8_t* __restrict__ y, int64_t H, int64_t W, uint32_t ncol, uint32_t nstrip,
@@ -176,7 +176,6 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
 #pragma unroll
     for (int s = 0; s < R - 1; ++s) prep_row(s);
 
-    const int32_t sat_hi = 0xFFFFFF;
     const uint32_t hmask = hf ? 0xFFFFFFFFu : 0u;
     uint32_t shv;  // the shift in a VGPR (gfx9 VOP3: one SGPR operand per instruction)
     asm("v_mov_b32 %0, %1" : "=v"(shv) : "s"(sh));
@@ -191,19 +190,25 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
             uint32_t a = (uint32_t)acc[e];
             if constexpr (NP == 2) a += (uint32_t)acch[e] << 8;
             if constexpr (FAST) {
-                // (sum + 2^(f-1)) << (16 - f), clamped.  Plain C for the first use of the MFMA
-                // result (v_add_lshl_u32: the shift is in a VGPR): hipcc does not pad inline asm
-                // that reads an MFMA destination with the wait states it needs (measured: wrong
-                // bytes 0, 1 of every block)
-                const uint32_t v = (a + bias) << shv;
-                asm("v_med3_i32 %0, %1, 0, %2" : "=v"(c[q]) : "v"(v), "s"(sat_hi));
+                // (sum + 2^(f-1)) << (16 - f): the rounded output as an int16 in bits 16..31.
+                // Plain C for the first use of the MFMA result (v_add_lshl_u32, the shift in a
+                // VGPR): hipcc does not pad inline asm that reads an MFMA destination with the
+                // wait states it needs (measured: wrong bytes 0, 1 of every block)
+                c[q] = (a + bias) << shv;
             } else {
                 c[q] = (uint32_t)min(max(round_acc<ACC32>((a + bias) << sh, shl, frac), 0), 255) << 16;
             }
         }
-        const uint32_t lo = __builtin_amdgcn_perm(c[1], c[0], 0x0C0C0602u);  // c0.b2, c1.b2
-        const uint32_t hi = __builtin_amdgcn_perm(c[3], c[2], 0x06020C0Cu);  // c2.b2, c3.b2 in bytes 2, 3
-        return lo | hi;
+        if constexpr (FAST) {  // two int16 outputs per dword, saturated to u8 pairs by v_sat_pk_u8_i16
+            uint32_t s01, s23;
+            asm("v_sat_pk_u8_i16 %0, %1" : "=v"(s01) : "v"(__builtin_amdgcn_perm(c[1], c[0], 0x07060302u)));
+            asm("v_sat_pk_u8_i16 %0, %1" : "=v"(s23) : "v"(__builtin_amdgcn_perm(c[3], c[2], 0x07060302u)));
+            return s01 | (s23 << 16);
+        } else {
+            const uint32_t lo = __builtin_amdgcn_perm(c[1], c[0], 0x0C0C0602u);  // c0.b2, c1.b2
+            const uint32_t hi = __builtin_amdgcn_perm(c[3], c[2], 0x06020C0Cu);  // c2.b2, c3.b2 in bytes 2, 3
+            return lo | hi;
+        }
     };
     // lane n: bytes 32n + 0..15, lane n + 32: bytes 32n + 16..31 (two v_permlane32_swap), then
     // (FIR2D_MFMA_LDS_STORE) through 1 KiB of wave-private LDS so that lane L stores bytes
