@@ -536,8 +536,9 @@ def main() -> int:
         "config": wl.config,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": KERNELS[args.workload],
-                     "limiter": ("VALU (12.5 v_pk_mad_u16/pixel: general packed-16 form, DESIGN.md §5)" if wl.gen2d else
+                     "kernel": "fir2d_mfma_kernel" if wl.gen2d else KERNELS[args.workload],
+                     "limiter": ("HBM (int8 MFMA Toeplitz rows; the memory-only twin of its loads and stores "
+                                 "takes 82.5 us per 4 frames, DESIGN.md §5)" if wl.gen2d else
                                  "VALU (~8.8 VALU instructions/pixel on packed 16-bit pixel pairs, DESIGN.md §5)")
                      if args.workload == "fir2d_u8" else "HBM",
                      "kernel_avg_us": round(kern_avg_s * 1e6, 2), "algorithmic_bytes_per_launch": alg_bytes,
