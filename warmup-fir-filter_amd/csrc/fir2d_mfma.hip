@@ -34,15 +34,8 @@
 namespace fir {
 
 constexpr int kM2Tile = 1024;   // output pixels per wave and row (32 blocks of 32)
-#ifndef FIR2D_MFMA_RING         // input rows in the register ring (R used + RING - R in flight)
-#define FIR2D_MFMA_RING 8
-#endif
-constexpr int kM2Ring = FIR2D_MFMA_RING;
 constexpr int kM2MaxR = 7;
 constexpr int kM2MaxC = 5;      // horizontal halo <= 2 pixels per side
-#ifndef FIR2D_MFMA_STRIP        // output rows per wave (A/B builds)
-#define FIR2D_MFMA_STRIP 32
-#endif
 #ifndef FIR2D_MFMA_LDS_STORE    // outputs through LDS into lane-contiguous 16-byte pieces
 #define FIR2D_MFMA_LDS_STORE 1
 #endif
@@ -52,8 +45,21 @@ constexpr int kM2MaxC = 5;      // horizontal halo <= 2 pixels per side
 #ifndef FIR2D_MFMA_MINW
 #define FIR2D_MFMA_MINW 3
 #endif
-constexpr int kM2Strip = FIR2D_MFMA_STRIP;
-static_assert(kM2Strip % kM2Ring == 0, "strip must be a multiple of the ring");
+// Register-ring rows (R in use + RING - R in flight) and output rows per wave, by tap rows:
+// 5 rows: a 7-row ring over 56-row strips, 86.5 vs 87.2 us (general 5x5) and 112.3 vs 119.1 us
+// (two byte planes) per 4-frame launch against 8 / 32; 3 rows: 8 / 32 (7 / 56: 88.2 vs 86.6 us);
+// deeper rings are slower (16 rows: 110-165 us) (profiles/r02/ab2d_mfma_ring_*.txt).
+// FIR2D_MFMA_RING / FIR2D_MFMA_STRIP override both (A/B builds).
+template <int R>
+struct M2Geom {
+#if defined(FIR2D_MFMA_RING) && defined(FIR2D_MFMA_STRIP)
+    static constexpr int RING = FIR2D_MFMA_RING, STRIP = FIR2D_MFMA_STRIP;
+#else
+    static constexpr int RING = R == 5 ? 7 : 8, STRIP = R == 5 ? 56 : 32;
+#endif
+    static_assert(STRIP % RING == 0, "strip must be a multiple of the ring");
+};
+constexpr int kM2MinStrip = 32;  // the shortest strip of any R (grid-size checks)
 
 // Tap bytes by diagonal: tm[p][m][33 - d] = byte p of h'[m][C/2 + d] (0 outside the row), d = r - k
 // of A_m[r][k] in [-33, 33]: the main k-steps use d in [-31, 31], the tail d = r + 2, r + 1,
@@ -84,6 +90,7 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
     uint32_t nwaves, Mfma2Taps taps, int cc, uint32_t bias, int sh, int shl, int frac) {
     constexpr int U = R - 1 - R / 2;  // input rows above an output row
     constexpr int D = R / 2;          // and below
+    constexpr int kM2Ring = M2Geom<R>::RING, kM2Strip = M2Geom<R>::STRIP;
     constexpr int PD = kM2Ring - R;   // rows in flight ahead of the newest one in use
     static_assert(PD >= 1, "ring too small");
 
@@ -243,10 +250,15 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
     // accumulator pair and, between them, stages row i - 1 out of the other, so the matrix
     // core and the VALU work at the same time inside a wave.
     m2_i32x16 acc[2] = {}, acch[2] = {};
-    for (int64_t iq = i0; iq < i0 + kM2Strip; iq += kM2Ring) {
+    // unrolled over a whole number of ring turns with an even number of rows, so that both the
+    // ring slot and the accumulator parity of every row are compile-time
+    constexpr int UN = (kM2Ring & 1) ? 2 * kM2Ring : kM2Ring;
+    static_assert(kM2Strip % UN == 0, "strip must be a multiple of the unrolled rows");
+    for (int64_t iq = i0; iq < i0 + kM2Strip; iq += UN) {
 #pragma unroll
-        for (int k = 0; k < kM2Ring; ++k) {
-            const int64_t i = iq + k;
+        for (int kk = 0; kk < UN; ++kk) {
+            const int k = kk % kM2Ring;  // ring position
+            const int64_t i = iq + kk;
             // keep each iteration's instructions in place: hipcc otherwise hoists a row's signed-
             // byte XOR up to its load, several iterations early, and waits for that load there
             __builtin_amdgcn_sched_barrier(0);
@@ -257,14 +269,14 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
             {
                 const m2_u4 rv = ring[(k + U) % kM2Ring];
                 const uint32_t g[4] = {rv.x, rv.y, rv.z, rv.w};
-                store_row(g, i - 1, k > 0 || iq > i0);
+                store_row(g, i - 1, kk > 0 || iq > i0);
                 continue;
             }
 #endif
-            m2_i32x16& a = acc[k & 1];
-            m2_i32x16& ah = acch[k & 1];
-            const m2_i32x16& pa = acc[(k + 1) & 1];
-            const m2_i32x16& pah = acch[(k + 1) & 1];
+            m2_i32x16& a = acc[kk & 1];
+            m2_i32x16& ah = acch[kk & 1];
+            const m2_i32x16& pa = acc[(kk + 1) & 1];
+            const m2_i32x16& pah = acch[(kk + 1) & 1];
             uint32_t g[4];
 #pragma unroll
             for (int mm = 0; mm < R + 1; ++mm) {
@@ -289,11 +301,11 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
                 if constexpr (NP == 2) ah = __builtin_amdgcn_mfma_i32_32x32x32_i8(av1, bv, mm ? ah : m2_i32x16{}, 0, 0, 0);
                 if (mm < 4) g[mm] = stage4(pa, pah, mm);  // row i - 1, between the MFMAs
             }
-            store_row(g, i - 1, k > 0 || iq > i0);
+            store_row(g, i - 1, kk > 0 || iq > i0);
         }
     }
     {  // the strip's last row
-        constexpr int kl = (kM2Strip - 1) % kM2Ring;
+        constexpr int kl = (kM2Strip - 1) % UN;
         uint32_t g[4];
 #pragma unroll
         for (int gi = 0; gi < 4; ++gi) g[gi] = stage4(acc[kl & 1], acch[kl & 1], gi);
@@ -304,6 +316,7 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
 template <int R, int NP>
 static hipError_t launch_m2(const uint8_t* x, uint8_t* y, int64_t frames, int64_t H, int64_t W, const Mfma2Taps& t,
                             int cc, uint32_t bias, int sh, bool fast, int acc_bits, int frac, hipStream_t s) {
+    constexpr int kM2Strip = M2Geom<R>::STRIP;
     const int64_t ncol = (W + kM2Tile - 1) / kM2Tile, nstrip = (H + kM2Strip - 1) / kM2Strip;
     const int64_t nw = frames * ncol * nstrip;
     const unsigned blocks = (unsigned)((nw + (kBlock / kWave) - 1) / (kBlock / kWave));
@@ -378,7 +391,7 @@ hipError_t launch_fir2d_mfma(const uint8_t* x, int64_t frames, int64_t H, int64_
     if (stage != FIR_OUT_U8_SAT || W % 16 || W < 16 || W >= ((int64_t)1 << 31) || (uintptr_t)x % 16 ||
         (uintptr_t)y % 16 || frames < 1 || H < 1)
         return hipErrorNotSupported;
-    const int64_t waves = frames * ((W + kM2Tile - 1) / kM2Tile) * ((H + kM2Strip - 1) / kM2Strip);
+    const int64_t waves = frames * ((W + kM2Tile - 1) / kM2Tile) * ((H + kM2MinStrip - 1) / kM2MinStrip);
     if (waves >= ((int64_t)1 << 31)) return hipErrorNotSupported;
     Mfma2Taps t;
     uint32_t bias;
