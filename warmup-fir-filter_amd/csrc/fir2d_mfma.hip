@@ -93,6 +93,7 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
     constexpr int kM2Ring = M2Geom<R>::RING, kM2Strip = M2Geom<R>::STRIP;
     constexpr int PD = kM2Ring - R;   // rows in flight ahead of the newest one in use
     static_assert(PD >= 1, "ring too small");
+    static_assert(R >= 3, "the stage of row i - 1 is spread over the R + 1 >= 4 MFMAs of row i");
 
     const int lane = threadIdx.x & (kWave - 1);
     const int n = lane & 31, hf = lane >> 5;
