@@ -87,7 +87,7 @@ constexpr uint32_t kM2Off = 0x80000000u;   // a voffset outside every descriptor
 template <int R, int NP, bool FAST, bool ACC32>
 __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_mfma_kernel(
     const uint8_t* __restrict__ x, uint8_t* __restrict__ y, int64_t H, int64_t W, uint32_t ncol, uint32_t nstrip,
-    uint32_t nwaves, Mfma2Taps taps, int cc, uint32_t bias, int sh, int shl, int frac) {
+    uint32_t nwaves, Mfma2Taps taps, uint32_t bias, int sh, int shl, int frac) {
     constexpr int U = R - 1 - R / 2;  // input rows above an output row
     constexpr int D = R / 2;          // and below
     constexpr int kM2Ring = M2Geom<R>::RING, kM2Strip = M2Geom<R>::STRIP;
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
 
 template <int R, int NP>
 static hipError_t launch_m2(const uint8_t* x, uint8_t* y, int64_t frames, int64_t H, int64_t W, const Mfma2Taps& t,
-                            int cc, uint32_t bias, int sh, bool fast, int acc_bits, int frac, hipStream_t s) {
+                            uint32_t bias, int sh, bool fast, int acc_bits, int frac, hipStream_t s) {
     constexpr int kM2Strip = M2Geom<R>::STRIP;
     const int64_t ncol = (W + kM2Tile - 1) / kM2Tile, nstrip = (H + kM2Strip - 1) / kM2Strip;
     const int64_t nw = frames * ncol * nstrip;
@@ -324,13 +324,13 @@ static hipError_t launch_m2(const uint8_t* x, uint8_t* y, int64_t frames, int64_
     const int shl = 32 - acc_bits;
     if (fast)
         hipLaunchKernelGGL((fir2d_mfma_kernel<R, NP, true, true>), dim3(blocks), dim3(kBlock), 0, s, x, y, H, W,
-                           (uint32_t)ncol, (uint32_t)nstrip, (uint32_t)nw, t, cc, bias, sh, shl, frac);
+                           (uint32_t)ncol, (uint32_t)nstrip, (uint32_t)nw, t, bias, sh, shl, frac);
     else if (acc_bits == 32)
         hipLaunchKernelGGL((fir2d_mfma_kernel<R, NP, false, true>), dim3(blocks), dim3(kBlock), 0, s, x, y, H, W,
-                           (uint32_t)ncol, (uint32_t)nstrip, (uint32_t)nw, t, cc, bias, sh, shl, frac);
+                           (uint32_t)ncol, (uint32_t)nstrip, (uint32_t)nw, t, bias, sh, shl, frac);
     else
         hipLaunchKernelGGL((fir2d_mfma_kernel<R, NP, false, false>), dim3(blocks), dim3(kBlock), 0, s, x, y, H, W,
-                           (uint32_t)ncol, (uint32_t)nstrip, (uint32_t)nw, t, cc, bias, sh, shl, frac);
+                           (uint32_t)ncol, (uint32_t)nstrip, (uint32_t)nw, t, bias, sh, shl, frac);
     return hipGetLastError();
 }
 
@@ -400,12 +400,11 @@ hipError_t launch_fir2d_mfma(const uint8_t* x, int64_t frames, int64_t H, int64_
     bool fast;
     const int np = plan_mfma2(hq, R, C, frac, acc_bits, &t, &bias, &sh, &fast);
     if (!np) return hipErrorNotSupported;
-    const int cc = C / 2;
     uint8_t* yy = (uint8_t*)y;
 #define FIR2D_M2(r)                                                                                    \
     if (R == r)                                                                                        \
-        return np == 1 ? launch_m2<r, 1>(x, yy, frames, H, W, t, cc, bias, sh, fast, acc_bits, frac, s) \
-                       : launch_m2<r, 2>(x, yy, frames, H, W, t, cc, bias, sh, fast, acc_bits, frac, s);
+        return np == 1 ? launch_m2<r, 1>(x, yy, frames, H, W, t, bias, sh, fast, acc_bits, frac, s) \
+                       : launch_m2<r, 2>(x, yy, frames, H, W, t, bias, sh, fast, acc_bits, frac, s);
     FIR2D_M2(3) FIR2D_M2(5)
 #undef FIR2D_M2
     return hipErrorNotSupported;
