@@ -26,6 +26,7 @@
 // the reference's wrap bit for bit).  Outputs: the 16 accumulators of a lane are bytes
 // 32n + 8g + 4h + 0..3; two v_permlane32_swap give every lane 16 contiguous output bytes, so each
 // output row leaves as one 1 KiB store instruction (non-temporal).
+#include <cstdlib>
 #include <string>
 
 #include "fir_common.h"
@@ -45,21 +46,19 @@ constexpr int kM2MaxC = 5;      // horizontal halo <= 2 pixels per side
 #ifndef FIR2D_MFMA_MINW
 #define FIR2D_MFMA_MINW 3
 #endif
-// Register-ring rows (R in use + RING - R in flight) and output rows per wave, by tap rows:
-// 5 rows: a 7-row ring over 56-row strips, 86.5 vs 87.2 us (general 5x5) and 112.3 vs 119.1 us
-// (two byte planes) per 4-frame launch against 8 / 32; 3 rows: 8 / 32 (7 / 56: 88.2 vs 86.6 us);
-// deeper rings are slower (16 rows: 110-165 us) (profiles/r02/ab2d_mfma_ring_*.txt).
-// FIR2D_MFMA_RING / FIR2D_MFMA_STRIP override both (A/B builds).
+// Register-ring rows (R in use + RING - R in flight), by tap rows: 5 rows: a 7-row ring, 86.5 vs
+// 87.2 us (general 5x5) and 112.3 vs 119.1 us (two byte planes) per 4-frame launch against 8 rows
+// (with 56- vs 32-row strips); 3 rows: 8; deeper rings are slower (16 rows: 110-165 us)
+// (profiles/r02/ab2d_mfma_ring_*.txt).  FIR2D_MFMA_RING overrides it (A/B builds); the strip
+// length is chosen at launch (m2_rows_per_strip).
 template <int R>
 struct M2Geom {
-#if defined(FIR2D_MFMA_RING) && defined(FIR2D_MFMA_STRIP)
-    static constexpr int RING = FIR2D_MFMA_RING, STRIP = FIR2D_MFMA_STRIP;
+#ifdef FIR2D_MFMA_RING
+    static constexpr int RING = FIR2D_MFMA_RING;
 #else
-    static constexpr int RING = R == 5 ? 7 : 8, STRIP = R == 5 ? 56 : 32;
+    static constexpr int RING = R == 5 ? 7 : 8;
 #endif
-    static_assert(STRIP % RING == 0, "strip must be a multiple of the ring");
 };
-constexpr int kM2MinStrip = 32;  // the shortest strip of any R (grid-size checks)
 
 // Tap bytes by diagonal: tm[p][m][33 - d] = byte p of h'[m][C/2 + d] (0 outside the row), d = r - k
 // of A_m[r][k] in [-33, 33]: the main k-steps use d in [-31, 31], the tail d = r + 2, r + 1,
@@ -87,10 +86,11 @@ constexpr uint32_t kM2Off = 0x80000000u;   // a voffset outside every descriptor
 template <int R, int NP, bool FAST, bool ACC32>
 __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_mfma_kernel(
     const uint8_t* __restrict__ x, uint8_t* __restrict__ y, int64_t H, int64_t W, uint32_t ncol, uint32_t nstrip,
-    uint32_t nwaves, Mfma2Taps taps, uint32_t bias, int sh, int shl, int frac) {
+    uint32_t nwaves, int rows_per_strip, Mfma2Taps taps, uint32_t bias, int sh, int shl, int frac) {
     constexpr int U = R - 1 - R / 2;  // input rows above an output row
     constexpr int D = R / 2;          // and below
-    constexpr int kM2Ring = M2Geom<R>::RING, kM2Strip = M2Geom<R>::STRIP;
+    constexpr int kM2Ring = M2Geom<R>::RING;
+    const int kM2Strip = rows_per_strip;  // a multiple of UN (host)
     constexpr int PD = kM2Ring - R;   // rows in flight ahead of the newest one in use
     static_assert(PD >= 1, "ring too small");
     static_assert(R >= 3, "the stage of row i - 1 is spread over the R + 1 >= 4 MFMAs of row i");
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
     // unrolled over a whole number of ring turns with an even number of rows, so that both the
     // ring slot and the accumulator parity of every row are compile-time
     constexpr int UN = (kM2Ring & 1) ? 2 * kM2Ring : kM2Ring;
-    static_assert(kM2Strip % UN == 0, "strip must be a multiple of the unrolled rows");
+    static_assert(UN % 2 == 0, "rows per unrolled turn must be even (accumulator parity)");
     for (int64_t iq = i0; iq < i0 + kM2Strip; iq += UN) {
 #pragma unroll
         for (int kk = 0; kk < UN; ++kk) {
@@ -306,7 +306,7 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
         }
     }
     {  // the strip's last row
-        constexpr int kl = (kM2Strip - 1) % UN;
+        constexpr int kl = UN - 1;  // the strip's last row: (strip - 1) % UN
         uint32_t g[4];
 #pragma unroll
         for (int gi = 0; gi < 4; ++gi) g[gi] = stage4(acc[kl & 1], acch[kl & 1], gi);
@@ -314,24 +314,56 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
     }
 }
 
+// Output rows per wave: by default the strips are sized so that the launch is ONE round of
+// resident waves (occupancy x CUs x 4), which removes the partial last round of fixed strips;
+// FIR2D_MFMA_ROWS=n forces n (rounded up to the unrolled turn; A/B).
+template <int R, int NP, bool FAST, bool ACC32>
+static int m2_rows_per_strip(int64_t frames, int64_t ncol, int64_t H) {
+    constexpr int UN = (M2Geom<R>::RING & 1) ? 2 * M2Geom<R>::RING : M2Geom<R>::RING;
+    int64_t rows;
+    const char* env = getenv("FIR2D_MFMA_ROWS");
+    if (env && atoi(env) > 0) {
+        rows = atoi(env);
+    } else {
+        static int resident = 0;  // waves of this instantiation resident on the device at once
+        if (!resident) {
+            int dev = 0, cus = 0, nb = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fir2d_mfma_kernel<R, NP, FAST, ACC32>, kBlock, 0) !=
+                    hipSuccess || cus <= 0 || nb <= 0) {
+                (void)hipGetLastError();
+                cus = 256, nb = 3;
+            }
+            resident = cus * nb * (kBlock / kWave);
+        }
+        const int64_t per = frames * ncol, strips = resident / per > 1 ? resident / per : 1;
+        rows = (H + strips - 1) / strips;
+    }
+    rows = (rows + UN - 1) / UN * UN;
+    const int64_t hmax = (H + UN - 1) / UN * UN;
+    return (int)(rows < hmax ? rows : hmax);
+}
+
+template <int R, int NP, bool FAST, bool ACC32>
+static hipError_t launch_m2v(const uint8_t* x, uint8_t* y, int64_t frames, int64_t H, int64_t W, const Mfma2Taps& t,
+                             uint32_t bias, int sh, int acc_bits, int frac, hipStream_t s) {
+    const int64_t ncol = (W + kM2Tile - 1) / kM2Tile;
+    const int rows = m2_rows_per_strip<R, NP, FAST, ACC32>(frames, ncol, H);
+    const int64_t nstrip = (H + rows - 1) / rows, nw = frames * ncol * nstrip;
+    if (nw >= ((int64_t)1 << 31)) return hipErrorNotSupported;
+    const unsigned blocks = (unsigned)((nw + (kBlock / kWave) - 1) / (kBlock / kWave));
+    hipLaunchKernelGGL((fir2d_mfma_kernel<R, NP, FAST, ACC32>), dim3(blocks), dim3(kBlock), 0, s, x, y, H, W,
+                       (uint32_t)ncol, (uint32_t)nstrip, (uint32_t)nw, rows, t, bias, sh, 32 - acc_bits, frac);
+    return hipGetLastError();
+}
+
 template <int R, int NP>
 static hipError_t launch_m2(const uint8_t* x, uint8_t* y, int64_t frames, int64_t H, int64_t W, const Mfma2Taps& t,
                             uint32_t bias, int sh, bool fast, int acc_bits, int frac, hipStream_t s) {
-    constexpr int kM2Strip = M2Geom<R>::STRIP;
-    const int64_t ncol = (W + kM2Tile - 1) / kM2Tile, nstrip = (H + kM2Strip - 1) / kM2Strip;
-    const int64_t nw = frames * ncol * nstrip;
-    const unsigned blocks = (unsigned)((nw + (kBlock / kWave) - 1) / (kBlock / kWave));
-    const int shl = 32 - acc_bits;
-    if (fast)
-        hipLaunchKernelGGL((fir2d_mfma_kernel<R, NP, true, true>), dim3(blocks), dim3(kBlock), 0, s, x, y, H, W,
-                           (uint32_t)ncol, (uint32_t)nstrip, (uint32_t)nw, t, bias, sh, shl, frac);
-    else if (acc_bits == 32)
-        hipLaunchKernelGGL((fir2d_mfma_kernel<R, NP, false, true>), dim3(blocks), dim3(kBlock), 0, s, x, y, H, W,
-                           (uint32_t)ncol, (uint32_t)nstrip, (uint32_t)nw, t, bias, sh, shl, frac);
-    else
-        hipLaunchKernelGGL((fir2d_mfma_kernel<R, NP, false, false>), dim3(blocks), dim3(kBlock), 0, s, x, y, H, W,
-                           (uint32_t)ncol, (uint32_t)nstrip, (uint32_t)nw, t, bias, sh, shl, frac);
-    return hipGetLastError();
+    if (fast) return launch_m2v<R, NP, true, true>(x, y, frames, H, W, t, bias, sh, acc_bits, frac, s);
+    if (acc_bits == 32) return launch_m2v<R, NP, false, true>(x, y, frames, H, W, t, bias, sh, acc_bits, frac, s);
+    return launch_m2v<R, NP, false, false>(x, y, frames, H, W, t, bias, sh, acc_bits, frac, s);
 }
 
 // Host plan: the power of two 2^s common to every tap moves into the final shift, the rest
@@ -392,8 +424,6 @@ hipError_t launch_fir2d_mfma(const uint8_t* x, int64_t frames, int64_t H, int64_
     if (stage != FIR_OUT_U8_SAT || W % 16 || W < 16 || W >= ((int64_t)1 << 31) || (uintptr_t)x % 16 ||
         (uintptr_t)y % 16 || frames < 1 || H < 1)
         return hipErrorNotSupported;
-    const int64_t waves = frames * ((W + kM2Tile - 1) / kM2Tile) * ((H + kM2MinStrip - 1) / kM2MinStrip);
-    if (waves >= ((int64_t)1 << 31)) return hipErrorNotSupported;
     Mfma2Taps t;
     uint32_t bias;
     int sh;
