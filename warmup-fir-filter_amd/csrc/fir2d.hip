@@ -33,7 +33,10 @@ constexpr int kPdSep = 3;
 constexpr int kPdGen = 2;
 // packed-16 form: 32-row strips, rows 4 ahead (23.5 vs 24.3 us for 16 rows / 3 ahead; a
 // memory-only twin of the same loop takes 21.1 us, profiles/r01/micro2d_copy.txt)
-constexpr int kStrip2dPk = 32;
+#ifndef FIR2D_PK_STRIP  // A/B builds
+#define FIR2D_PK_STRIP 32
+#endif
+constexpr int kStrip2dPk = FIR2D_PK_STRIP;
 constexpr int kPdPk = 4;
 // general packed-16 form: 16-row strips (a 32-row strip's R*C MACs per row exceed the forced
 // unroll budget: the loop stays rolled and its ring spills to scratch)
