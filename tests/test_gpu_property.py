@@ -4,10 +4,12 @@ the C oracle (itself pinned to the reference's golden vectors by tests/test_orac
 
 Complements the fixed parameter grids of test_gpu_fir1d.py / test_gpu_fir2d_ideal.py: the
 strategies cover every kernel the launchers can pick (register v_dot2 / byte-pair / packed-16 /
-mad24 forms, the generic LDS kernel, the 2-D separable, packed-16 and general forms, the halo
-segment path) without enumerating them, and hypothesis shrinks any failure to a small case.
+mad24 forms, the generic LDS kernel, the 2-D separable, packed-16 and general forms, the 2-D
+int8 matrix-core kernel forced on, the halo segment path) without enumerating them, and hypothesis shrinks any failure to a small case.
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 import torch
@@ -20,6 +22,7 @@ from oracle import c_oracle
 SETTINGS = dict(deadline=None, database=None, derandomize=True,
                 suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
 DEV = torch.device("cuda:0")
+
 
 
 def _taps(draw, n: int) -> list[int]:
@@ -130,6 +133,47 @@ def test_fir2d_random_vs_oracle(case):
     for f in range(max(frames, 1)):
         xf = x[f] if frames else x
         ref = c_oracle().fir2d(xf, np.asarray(hq), frac, acc, stage)
+        assert np.array_equal(got[f] if frames else got, ref), f
+
+
+@st.composite
+def fir2d_mfma_case(draw):
+    R = draw(st.sampled_from([3, 5]))
+    C = draw(st.integers(1, 5))
+    kind = draw(st.sampled_from(["byte", "byte", "pow2", "pair", "pair_wide"]))
+    lim = {"byte": 127, "pow2": 127, "pair": 8192, "pair_wide": 32639}[kind]
+    hq = np.asarray(draw(st.lists(st.integers(-lim - 1, lim), min_size=R * C, max_size=R * C))).reshape(R, C)
+    if kind == "pow2":  # a common power of two moves into the shift
+        hq = hq * (1 << draw(st.integers(1, 10)))
+    H = draw(st.one_of(st.integers(1, 40), st.integers(41, 300)))
+    W = 16 * draw(st.one_of(st.integers(1, 70), st.integers(63, 66), st.integers(120, 200)))
+    frac = draw(st.one_of(st.just(12), st.integers(1, 24)))
+    acc = draw(st.one_of(st.just(32), st.integers(12, 32)))
+    frames = draw(st.sampled_from([0, 0, 1, 2, 3]))
+    seed = draw(st.integers(0, 2**32 - 1))
+    return hq.tolist(), H, W, frac, acc, frames, seed
+
+
+@settings(max_examples=400, **SETTINGS)
+@given(fir2d_mfma_case())
+def test_fir2d_mfma_random_vs_oracle(case):
+    """The 2-D matrix-core kernel forced on (FIR2D_PATH=mfma): one or two tap byte planes, a power
+    of two factored into the shift, 16-byte rows around the 1024-pixel tile edges, any height
+    (strips sized at launch), batches of frames, the fast byte-2 stage and the rounded wrap form."""
+    hq, H, W, frac, acc, frames, seed = case
+    x = np.random.default_rng(seed).integers(0, 256, (frames, H, W) if frames else (H, W), dtype=np.uint8)
+    old = os.environ.get("FIR2D_PATH")
+    os.environ["FIR2D_PATH"] = "mfma"
+    try:
+        got = fir_hip.fir2d_fixed(x, hq, frac, acc, fir_hip.OUT_U8_SAT)
+    finally:
+        if old is None:
+            os.environ.pop("FIR2D_PATH")
+        else:
+            os.environ["FIR2D_PATH"] = old
+    for f in range(max(frames, 1)):
+        xf = x[f] if frames else x
+        ref = c_oracle().fir2d(xf, np.asarray(hq), frac, acc, fir_hip.OUT_U8_SAT)
         assert np.array_equal(got[f] if frames else got, ref), f
 
 
