@@ -46,9 +46,10 @@ constexpr int kM2MaxC = 5;      // horizontal halo <= 2 pixels per side
 #ifndef FIR2D_MFMA_MINW
 #define FIR2D_MFMA_MINW 3
 #endif
-// Register-ring rows (R in use + RING - R in flight), by tap rows: 5 rows: a 7-row ring, 86.5 vs
-// 87.2 us (general 5x5) and 112.3 vs 119.1 us (two byte planes) per 4-frame launch against 8 rows
-// (with 56- vs 32-row strips); 3 rows: 8; deeper rings are slower (16 rows: 110-165 us)
+// Register-ring rows (R in use + 8 - R in flight).  With strips sized to one resident round an
+// 8-row ring (8-row strip granularity: 3008 waves for 3072 slots at 8192^2 x 4) beats the 7-row
+// ring (14-row granularity: 2688 waves): general 5x5 88.0 -> 87.4 us, two byte planes 109.0 ->
+// 105.1 us per 4-frame launch; deeper rings are slower (16 rows: 110-165 us)
 // (profiles/r02/ab2d_mfma_ring_*.txt).  FIR2D_MFMA_RING overrides it (A/B builds); the strip
 // length is chosen at launch (m2_rows_per_strip).
 template <int R>
@@ -56,7 +57,7 @@ struct M2Geom {
 #ifdef FIR2D_MFMA_RING
     static constexpr int RING = FIR2D_MFMA_RING;
 #else
-    static constexpr int RING = R == 5 ? 7 : 8;
+    static constexpr int RING = 8;
 #endif
 };
 
