@@ -34,7 +34,13 @@ namespace fir {
 constexpr int kMfTile = 1024;        // outputs per wave tile (32 B columns x 32 A rows)
 constexpr int kMfMaxTaps = 64;
 constexpr int kMfWaves = kBlock / kWave;
-constexpr int kMfMaxBlocks = 1024;   // grid-stride, one resident round (4 blocks per CU)
+#ifndef FIR_MFMA_MAXBLOCKS
+#define FIR_MFMA_MAXBLOCKS 1024
+#endif
+constexpr int kMfMaxBlocks = FIR_MFMA_MAXBLOCKS;   // grid-stride, one resident round (4 blocks per CU)
+#ifndef FIR_MFMA_SCHED               // A/B builds: a scheduling barrier at each tile
+#define FIR_MFMA_SCHED 0
+#endif
 #ifndef FIR_MFMA_MINB                // blocks per CU the register allocation must allow (A/B builds)
 #define FIR_MFMA_MINB 4
 #endif
@@ -165,6 +171,9 @@ __global__ __launch_bounds__(kBlock, FIR_MFMA_MINB) void fir1d_mfma_kernel(const
     // One tile: convert its prefetched window, store the previous tile, prefetch the next window,
     // MFMA, stage the outputs.
     auto body = [&](uint32_t tile, bool first) __attribute__((always_inline)) {
+#if FIR_MFMA_SCHED
+        __builtin_amdgcn_sched_barrier(0);  // A/B: keep each tile's instructions in place
+#endif
         const MfTile t = mf_tile(tile, rowlen, tpr);
         const int m = (int)min((int64_t)kMfTile, t.re - t.ts);  // outputs of this tile
 
