@@ -34,10 +34,13 @@ namespace fir {
 constexpr int kMfTile = 1024;        // outputs per wave tile (32 B columns x 32 A rows)
 constexpr int kMfMaxTaps = 64;
 constexpr int kMfWaves = kBlock / kWave;
+// grid-stride blocks: 2048 (two resident rounds at 4 blocks per CU) rather than one round, 1-5 %
+// faster for u8 input (u8 -> u8 at 31 taps 95.7 -> 91.5 us, u8 -> int32 196.5 -> 193.3 us;
+// 3072 / 4096 within noise of 2048; profiles/r02/long_taps_mfma_grid.txt)
 #ifndef FIR_MFMA_MAXBLOCKS
-#define FIR_MFMA_MAXBLOCKS 1024
+#define FIR_MFMA_MAXBLOCKS 2048
 #endif
-constexpr int kMfMaxBlocks = FIR_MFMA_MAXBLOCKS;   // grid-stride, one resident round (4 blocks per CU)
+constexpr int kMfMaxBlocks = FIR_MFMA_MAXBLOCKS;
 #ifndef FIR_MFMA_SCHED               // A/B builds: a scheduling barrier at each tile
 #define FIR_MFMA_SCHED 0
 #endif
