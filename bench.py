@@ -5,9 +5,10 @@ Default workload (BASELINE.json configs[1]; configs[3] at --gpus 8): 5-tap int16
 FIR-1D (Q4.12 "sharpen" taps [-256,-1024,6656,-1024,-256], 32-bit wrap, round, no
 saturation) over 2^28 synthetic samples PER GPU (weak scaling: 2^31 samples on 8 GPUs),
 inputs resident in HBM before the timed region.  For N > 1 each rank owns one contiguous
-segment; a step is ONE launch of the FIR kernel whose edge lanes read the 2+2-sample halo
-from the neighbours' HBM over xGMI (mapped once; FIR_HALO=rccl: RCCL send/recv every step,
-overlapped with the bulk kernel, then an edge kernel).
+segment; a step is a one-wave gate kernel that hands the 2+2-sample halo over through the
+neighbours' HBM over xGMI, ordered per step (device atomics on mailboxes mapped once), then ONE
+launch of the FIR kernel reading it (FIR_HALO=rccl: RCCL send/recv every step, overlapped with
+the bulk kernel, then an edge kernel).
 
 Contract: `python bench.py --gpus N --steps K --warmup W` (torchrun for N > 1); rank 0
 prints ONE JSON line.  Extra keys:
@@ -246,12 +247,17 @@ class Workload:
                 self.halo_kind, self.halo_src = sharded.make_halo_source(self.x, self.taps.n, self.channels,
                                                                          prefer=HALO_PREF)
             self.config["parallelism"] = (
-                f"contiguous shards x{self.world}, halo " + ("read by the FIR kernel from the neighbours' HBM over "
-                                                             "xGMI (peer IPC mapping)" if self.halo_kind == "xgmi"
-                                                             else "exchanged by RCCL send/recv every step"))
-        if self.halo_kind == "xgmi":  # ONE launch: the kernel reads the halos from the neighbours' HBM
-            self.left, self.right = self.halo_src.left_host, self.halo_src.right_host
-            torch_ops.fir1d_fixed_segment_dev(self.x, self.taps, *self.halo_src.halos(), 12, 32, fir_hip.OUT_I32,
+                f"contiguous shards x{self.world}, " + (
+                    "halo handed over through the neighbours' HBM over xGMI, ordered per step: a one-wave gate "
+                    "kernel publishes this rank's edge samples with the step's epoch, waits for both neighbours' "
+                    "epoch (device atomics on IPC-mapped mailboxes) and copies their edges; then one FIR launch "
+                    "reads them" if self.halo_kind == "xgmi"
+                    else "halo exchanged by RCCL send/recv every step (ordered by the messages), overlapped with "
+                         "the bulk kernel, then an edge kernel"))
+        if self.halo_kind == "xgmi":  # the ordered hand-off, then ONE FIR launch reading the received halos
+            self.halo_src.gate()
+            self.left, self.right = self.halo_src.halos()
+            torch_ops.fir1d_fixed_segment_dev(self.x, self.taps, self.left, self.right, 12, 32, fir_hip.OUT_I32,
                                               self.channels, out=self.y)
             return
         works = self.halo_src.post()  # RCCL: bulk || exchange, then the edge kernel
@@ -452,6 +458,8 @@ def main() -> int:
 
     wl.step()  # restore the full step's output (the loop above ran the bulk kernel alone)
     torch.cuda.synchronize()
+    if isinstance(wl.halo_src, sharded.XgmiHalo):
+        wl.halo_src.check()  # every gate's wait arrived (raises otherwise)
 
     # parity: full output vs the C oracle (every rank, its own segment with the received halos)
     parity = "skipped"

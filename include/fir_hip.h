@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define FIR_HIP_ABI_VERSION 1
+#define FIR_HIP_ABI_VERSION 2
 #define FIR_MAX_TAPS 256 /* 1-D taps; 2-D: tap_rows * tap_cols <= FIR_MAX_TAPS */
 
 typedef enum {
@@ -63,8 +63,11 @@ typedef enum {
 typedef enum { FIR_IN_U8 = 0, FIR_IN_I16 = 1 } fir_in_dtype;
 typedef enum { FIR_OUT_U8_SAT = 0, FIR_OUT_I32 = 1 } fir_out_stage;
 
-/* Library / device queries. */
+/* Library / device queries.  fir_build_id: a hash of the sources the library was built from
+ * (csrc/, csrc/Makefile and this header); the Python loader refuses a library whose id differs
+ * from the sources beside it (a stale build). */
 int fir_abi_version(void);
+const char* fir_build_id(void);
 const char* fir_last_error(void);
 int fir_device_count(int* count);
 
@@ -188,14 +191,44 @@ int fir_restore_u8_dev(const double* a_dev, int64_t n, int policy, uint8_t* out_
  * fir_peer_access: *can = 1 when kernels on `device` may read the HBM of the GPU with PCI bus
  *   id `peer_bus_id` (the same GPU, or a peer visible to this process with peer access);
  *   0 when that GPU is not visible here or has no peer path.  Checked before any kernel
- *   reads a mapped neighbour (a mapping alone does not prove a kernel may read it). */
+ *   reads a mapped neighbour (a mapping alone does not prove a kernel may read it).
+ * fir_peer_atomics: *can = 1 when kernels on `device` may also perform atomics on that GPU's
+ *   HBM (the same GPU, or hipDevP2PAttrNativeAtomicSupported); the halo gate below needs it. */
 #define FIR_IPC_HANDLE_BYTES 64
 int fir_device_bus_id(int device, char* out, int len);
 int fir_peer_access(int device, const char* peer_bus_id, int* can);
+int fir_peer_atomics(int device, const char* peer_bus_id, int* can);
 int fir_ipc_export(const void* dev_ptr, void* handle_out, int64_t* offset_out);
 int fir_ipc_import(const void* handle, int64_t offset, int device, void** dev_ptr_out);
 int fir_ipc_close(void* dev_ptr);
 int fir_peek(const void* dev_ptr, void* host_out, int64_t bytes);
+
+/* ---- per-step ordering of the halo hand-off --------------------------
+ * When every rank's segment changes from step to step, rank r must read the neighbours'
+ * segments of THIS step.  Each rank owns a mailbox in its own HBM (zeroed once, exported with
+ * fir_ipc_export, mapped by both neighbours with fir_ipc_import); every step, on the rank's
+ * stream after the step's segment is written and before the FIR kernel that uses the halos,
+ * fir_halo_gate_dev runs ONE wave that
+ *   1. publishes the segment's first halo_right_bytes (its left neighbour's right halo) and
+ *      last halo_left_bytes (its right neighbour's left halo) with this step's epoch,
+ *   2. waits until both present neighbours have published the same epoch (at most timeout_s
+ *      seconds; on expiry *status_dev = FIR_GATE_TIMEOUT, the halos are zeroed, and every later
+ *      gate of this mailbox stops waiting and reports the same),
+ *   3. copies the left neighbour's published tail into halo_left_dev (halo_left_bytes) and the
+ *      right neighbour's published head into halo_right_dev (halo_right_bytes).
+ * A NULL neighbour mailbox is a global end (no wait, halo untouched).  Mailbox words are only
+ * touched by device atomics (performed at the memory side: coherent across XCDs and xGMI).
+ * All ranks of a ring must use the same halo sizes and call the gate once per step.
+ * fir_halo_mailbox_bytes: size of one mailbox; fir_halo_mailbox_init_dev: zero it on `stream`
+ * (before it is exported; every rank's init must complete before any neighbour's first gate).
+ * Mailboxes must be 128-byte aligned. */
+#define FIR_GATE_TIMEOUT 1
+int64_t fir_halo_mailbox_bytes(int64_t halo_left_bytes, int64_t halo_right_bytes);
+int fir_halo_mailbox_init_dev(void* mailbox_dev, int64_t bytes, void* stream);
+int fir_halo_gate_dev(const void* x_dev, int64_t seg_bytes, int64_t halo_left_bytes, int64_t halo_right_bytes,
+                      void* mailbox_dev, const void* left_mailbox_dev, const void* right_mailbox_dev,
+                      void* halo_left_dev, void* halo_right_dev, int32_t* status_dev, double timeout_s,
+                      void* stream);
 
 #ifdef __cplusplus
 }

@@ -168,26 +168,28 @@ def _xgmi_worker(rank, world, port, taps, ch, q):
         lo, hi = sharded.segment_bounds(n, world, rank)
         seg = torch.from_numpy(x[lo * ch:hi * ch].copy()).to(dev)
         y = torch.empty(seg.shape, dtype=torch.int32, device=dev)
+        y2 = torch.full(seg.shape, -7, dtype=torch.int32, device=dev)
         torch.cuda.synchronize()
         dist.barrier()  # every segment resident before it is mapped
         kind, src = sharded.make_halo_source(seg, len(taps), ch)
-        for _ in range(3):  # the mapping is reused step after step
+        for step in range(3):  # every segment changes every step; the gate orders the hand-off
+            seg.add_(step + 1)
+            src.gate()
             to.fir1d_fixed_rows_dev(seg, taps, 12, 32, fh.OUT_I32, ch, out=y)
             to.fir1d_fixed_edges_dev(seg, taps, y, *src.halos(), 12, 32, fh.OUT_I32, ch)
+            # the one-launch form reads the same received halos inside the register kernel
+            to.fir1d_fixed_segment_dev(seg, taps, *src.halos(), 12, 32, fh.OUT_I32, ch, out=y2)
         torch.cuda.synchronize()
+        src.check()
         parts = [None] * world
         dist.all_gather_object(parts, y.cpu().numpy())
-        # the one-launch form reads the same peer addresses inside the register kernel
-        y2 = torch.full(seg.shape, -7, dtype=torch.int32, device=dev)
-        to.fir1d_fixed_segment_dev(seg, taps, *src.halos(), 12, 32, fh.OUT_I32, ch, out=y2)
-        torch.cuda.synchronize()
-        same = bool(torch.equal(y, y2))
         flags = [None] * world
-        dist.all_gather_object(flags, same)
+        dist.all_gather_object(flags, bool(torch.equal(y, y2)))
         dist.barrier()  # nobody unmaps / frees before every rank is done reading
         src.close()
         if rank == 0:
-            full = co().fir1d_rows(x, taps, 12, 32, co().OUT_I32, channels=ch)
+            xf = (x.astype(np.int32) + 6).astype(np.int16)  # + 1 + 2 + 3, int16 wrap
+            full = co().fir1d_rows(xf, taps, 12, 32, co().OUT_I32, channels=ch)
             q.put((kind, bool(np.array_equal(np.concatenate(parts), full)) and all(flags)))
     finally:
         dist.destroy_process_group()
@@ -196,9 +198,10 @@ def _xgmi_worker(rank, world, port, taps, ch, q):
 @pytest.mark.parametrize("world,taps,ch", [(2, [-256, -1024, 6656, -1024, -256], 1), (3, [5, -7, 9, 11], 1),
                                            (4, [1024, 2048, 1024], 2)])
 def test_xgmi_peer_halos_across_processes(world, taps, ch):
-    """fir_hip.sharded.XgmiHalo: ranks (processes) map their neighbours' segments through the
-    C ABI's IPC entries and the edge kernel reads the halos from them.  On the one-GPU box the
-    ranks share device 0 (the same mapping path as across GPUs, minus the xGMI hop)."""
+    """fir_hip.sharded.XgmiHalo: ranks (processes) map their neighbours' mailboxes through the
+    C ABI's IPC entries and the halo gate hands the edges over every step while every segment
+    changes.  On the one-GPU box the ranks share device 0 (the same mapping and atomics path
+    as across GPUs, minus the xGMI hop)."""
     import socket
 
     import torch.multiprocessing as mp

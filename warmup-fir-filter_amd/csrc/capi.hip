@@ -304,6 +304,11 @@ extern "C" {
 
 int fir_abi_version(void) { return FIR_HIP_ABI_VERSION; }
 
+#ifndef FIR_BUILD_ID
+#define FIR_BUILD_ID "unknown"
+#endif
+const char* fir_build_id(void) { return FIR_BUILD_ID; }
+
 const char* fir_last_error(void) { return g_err.c_str(); }
 
 int fir_device_count(int* count) {
@@ -762,6 +767,59 @@ int fir_peer_access(int device, const char* peer_bus_id, int* can) {
         if (e != hipSuccess) return fail(FIR_EHIP, std::string("hipDeviceCanAccessPeer: ") + hipGetErrorString(e));
         *can = ok ? 1 : 0;
         return FIR_OK;
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int fir_peer_atomics(int device, const char* peer_bus_id, int* can) {
+    try {
+        if (!peer_bus_id || !can) return fail(FIR_EINVAL, "NULL argument");
+        *can = 0;
+        int peer = -1;
+        if (hipDeviceGetByPCIBusId(&peer, peer_bus_id) != hipSuccess || peer < 0) {
+            (void)hipGetLastError();
+            return FIR_OK;
+        }
+        if (peer == device) {
+            *can = 1;
+            return FIR_OK;
+        }
+        int ok = 0;
+        hipError_t e = hipDeviceGetP2PAttribute(&ok, hipDevP2PAttrNativeAtomicSupported, device, peer);
+        if (e != hipSuccess) return fail(FIR_EHIP, std::string("hipDeviceGetP2PAttribute: ") + hipGetErrorString(e));
+        *can = ok ? 1 : 0;
+        return FIR_OK;
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int64_t fir_halo_mailbox_bytes(int64_t halo_left_bytes, int64_t halo_right_bytes) {
+    if (halo_left_bytes < 0 || halo_right_bytes < 0) return -1;
+    return fir::halo_mailbox_bytes(halo_left_bytes, halo_right_bytes);
+}
+
+int fir_halo_mailbox_init_dev(void* mailbox_dev, int64_t bytes, void* stream) {
+    try {
+        std::string err;
+        int rc = fir::launch_halo_mailbox_init(mailbox_dev, bytes, (hipStream_t)stream, &err);
+        return rc ? fail(rc, err) : FIR_OK;
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int fir_halo_gate_dev(const void* x_dev, int64_t seg_bytes, int64_t halo_left_bytes, int64_t halo_right_bytes,
+                      void* mailbox_dev, const void* left_mailbox_dev, const void* right_mailbox_dev,
+                      void* halo_left_dev, void* halo_right_dev, int32_t* status_dev, double timeout_s,
+                      void* stream) {
+    try {
+        std::string err;
+        int rc = fir::launch_halo_gate(x_dev, seg_bytes, halo_left_bytes, halo_right_bytes, mailbox_dev,
+                                       left_mailbox_dev, right_mailbox_dev, halo_left_dev, halo_right_dev, status_dev,
+                                       timeout_s, (hipStream_t)stream, &err);
+        return rc ? fail(rc, err) : FIR_OK;
     } catch (...) {
         return fail(FIR_EHIP, "internal error");
     }

@@ -40,6 +40,15 @@ int launch_fir1d_segment(const void* x, int in_dtype, int64_t n, int ch, const i
                          int acc_bits, int stage, const void* halo_left, const void* halo_right, void* y,
                          hipStream_t stream, std::string* err);
 
+// Per-step halo ordering for sharded segments (halo_gate.hip): mailbox size, its zeroing, and
+// the one-wave gate kernel (publish own edges, wait for both neighbours' epoch, copy their
+// edges into the local halo buffers).
+int64_t halo_mailbox_bytes(int64_t hl_bytes, int64_t hr_bytes);
+int launch_halo_mailbox_init(void* mailbox, int64_t bytes, hipStream_t stream, std::string* err);
+int launch_halo_gate(const void* x, int64_t seg_bytes, int64_t hl_bytes, int64_t hr_bytes, void* mailbox,
+                     const void* left_mailbox, const void* right_mailbox, void* halo_left, void* halo_right,
+                     int32_t* status, double timeout_s, hipStream_t stream, std::string* err);
+
 // 2-D fixed FIR over `frames` uint8 frames of height x width stored back to back (one launch).
 // 2-D u8 -> sat-u8 frames on the int8 matrix cores (fir2d_mfma.hip); hipErrorNotSupported when
 // the shape, alignment or taps are outside its cover (the caller then takes fir2d_reg_kernel)

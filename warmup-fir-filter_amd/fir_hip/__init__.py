@@ -24,7 +24,8 @@ __all__ = [
     "FirHipError", "lib", "lib_path", "device_count", "fir1d_fixed_rows", "fir1d_fixed_rows_multi",
     "fir1d_fixed_rows_sharded", "fir2d_fixed", "fir1d_ideal_rows", "compare_metrics", "restore_u8", "IN_U8", "IN_I16",
     "OUT_U8_SAT", "OUT_I32", "RESTORE_CLIP", "RESTORE_NORMALIZE", "MAX_TAPS", "EXPORTS", "ipc_export", "ipc_import",
-    "ipc_close", "peek", "IPC_HANDLE_BYTES", "device_bus_id", "peer_access",
+    "ipc_close", "peek", "IPC_HANDLE_BYTES", "device_bus_id", "peer_access", "peer_atomics", "halo_mailbox_bytes",
+    "GATE_TIMEOUT", "build_id",
 ]
 
 IN_U8, IN_I16 = 0, 1
@@ -32,7 +33,8 @@ OUT_U8_SAT, OUT_I32 = 0, 1
 RESTORE_CLIP, RESTORE_NORMALIZE = 0, 1
 MAX_TAPS = 256
 IPC_HANDLE_BYTES = 64
-ABI_VERSION = 1
+ABI_VERSION = 2
+GATE_TIMEOUT = 1  # FIR_GATE_TIMEOUT
 
 _HERE = Path(__file__).resolve().parent
 
@@ -50,6 +52,7 @@ _i32, _i64, _vp = ctypes.c_int, ctypes.c_int64, ctypes.c_void_p
 # symbol -> (restype, argtypes); mirrors include/fir_hip.h one to one
 EXPORTS = {
     "fir_abi_version": (_i32, []),
+    "fir_build_id": (ctypes.c_char_p, []),
     "fir_last_error": (ctypes.c_char_p, []),
     "fir_device_count": (_i32, [ctypes.POINTER(_i32)]),
     "fir1d_fixed_rows": (_i32, [_vp, _i32, _i64, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _i32]),
@@ -77,6 +80,10 @@ EXPORTS = {
     "fir_peek": (_i32, [_vp, _vp, _i64]),
     "fir_device_bus_id": (_i32, [_i32, ctypes.c_char_p, _i32]),
     "fir_peer_access": (_i32, [_i32, ctypes.c_char_p, ctypes.POINTER(_i32)]),
+    "fir_peer_atomics": (_i32, [_i32, ctypes.c_char_p, ctypes.POINTER(_i32)]),
+    "fir_halo_mailbox_bytes": (_i64, [_i64, _i64]),
+    "fir_halo_mailbox_init_dev": (_i32, [_vp, _i64, _vp]),
+    "fir_halo_gate_dev": (_i32, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_double, _vp]),
 }
 
 _lib = None
@@ -107,6 +114,12 @@ def lib() -> ctypes.CDLL:
         ver = handle.fir_abi_version()
         if ver != ABI_VERSION:
             raise FirHipError(f"{path}: ABI version {ver}, expected {ABI_VERSION}")
+        from ._srcid import source_id
+
+        built, want = handle.fir_build_id().decode(), source_id()
+        if want is not None and built != want:
+            raise FirHipError(f"{path} was built from other sources (build id {built}, the sources beside it hash "
+                              f"to {want}): rebuild with `make -C warmup-fir-filter_amd/csrc`")
         _lib = handle
     return _lib
 
@@ -349,6 +362,27 @@ def peer_access(device: int, peer_bus_id: str) -> bool:
     can = _i32(0)
     _check(lib().fir_peer_access(int(device), peer_bus_id.encode(), ctypes.byref(can)), "fir_peer_access")
     return bool(can.value)
+
+
+def peer_atomics(device: int, peer_bus_id: str) -> bool:
+    """Whether kernels on ``device`` may perform atomics on the HBM of the GPU at ``peer_bus_id``
+    (the halo gate's mailbox protocol needs it)."""
+    can = _i32(0)
+    _check(lib().fir_peer_atomics(int(device), peer_bus_id.encode(), ctypes.byref(can)), "fir_peer_atomics")
+    return bool(can.value)
+
+
+def halo_mailbox_bytes(halo_left_bytes: int, halo_right_bytes: int) -> int:
+    """Bytes of one rank's halo-gate mailbox (fir_hip.h, fir_halo_gate_dev)."""
+    n = int(lib().fir_halo_mailbox_bytes(int(halo_left_bytes), int(halo_right_bytes)))
+    if n < 0:
+        raise FirHipError("halo byte counts must be >= 0")
+    return n
+
+
+def build_id() -> str:
+    """The source id the loaded library was built from (see fir_hip._srcid)."""
+    return lib().fir_build_id().decode()
 
 
 def peek(dev_ptr: int, nbytes: int) -> bytes:

@@ -8,9 +8,10 @@ left neighbour and the first ``HR = L//2`` samples of its right neighbour (times
 the only data that crosses GPUs.  Two sources:
 
 * :class:`XgmiHalo` (default, :func:`make_halo_source`): each rank maps its neighbours'
-  resident segments once (HIP IPC through the C ABI); every pass is then one launch of the
-  FIR kernel whose edge lanes read the halo from the neighbours' HBM over xGMI
-  (``torch_ops.fir1d_fixed_segment_dev``).
+  mailboxes once (HIP IPC through the C ABI); every pass is then a one-wave gate kernel that
+  hands the edges over through the mailboxes (device atomics over xGMI, ordered per step, so
+  segments may change every pass) followed by one launch of the FIR kernel reading the
+  received halos (``torch_ops.fir1d_fixed_segment_dev``).
 * :class:`HaloExchange` (fallback, ``FIR_HALO=rccl``): two point-to-point messages of a few
   bytes per neighbour pair every pass, one ``batch_isend_irecv`` group, overlapped with the
   bulk kernel; a one-block edge kernel then rewrites the HL + HR edge outputs
@@ -107,19 +108,31 @@ class HaloExchange:
 
 
 class XgmiHalo:
-    """Halos read straight from the neighbours' HBM over xGMI (the MI355X-native exchange).
+    """The halo hand-off over xGMI, ordered per step (the MI355X-native exchange).
 
-    Set up once, collectively: every rank exports the allocation holding its resident
-    segment (fir_hip.ipc_export), the handles are all-gathered over the process group, and
-    each rank maps its left and right neighbours' segments (fir_hip.ipc_import) at the
-    addresses of the HL / HR samples it needs.  A step then passes those addresses to the
-    edge kernel, which loads the 2 x (a few) bytes over xGMI itself: no message, no RCCL
-    kernel, no cross-stream event per step.  The mapping is checked once against the
-    samples the neighbour reports.  Valid while the neighbours' segments stay resident and
-    unchanged (a resident long vector filtered in place); ``close()`` unmaps."""
+    Set up once, collectively: every rank zeroes a small mailbox in its own HBM
+    (``fir_halo_mailbox_init_dev``), exports it (fir_hip.ipc_export), the handles are
+    all-gathered over the process group, and each rank maps its left and right neighbours'
+    mailboxes (fir_hip.ipc_import).  Every step, :meth:`gate` enqueues ONE wave on this rank's
+    stream (``fir_halo_gate_dev``, csrc/halo_gate.hip) after whatever wrote the step's segment:
+    it publishes the segment's first HR and last HL samples with the step's epoch, waits until
+    both neighbours have published the same epoch (device atomics over xGMI, no host round trip,
+    no RCCL kernel), and copies their samples into the local halo buffers :meth:`halos` returns,
+    which the FIR kernel then reads.  So the halos are those of THIS step even when every
+    segment changes each step, and no rank overwrites what a neighbour has yet to read (two
+    mailbox slots; the argument is in halo_gate.hip).  A wait is bounded (``timeout_s``); an
+    expired one is reported by :meth:`check` (the halos are then zero, not stale).
 
-    def __init__(self, seg: torch.Tensor, taps: int, channels: int = 1, group=None):
+    Requires peer access AND peer atomics to both neighbours' GPUs (checked before mapping;
+    :func:`make_halo_source` falls back to RCCL on every rank otherwise, or if the first gated
+    hand-off, checked against the edges every rank reported, does not arrive)."""
+
+    def __init__(self, seg: torch.Tensor, taps: int, channels: int = 1, group=None, timeout_s: float | None = None):
+        import os
+
         import fir_hip
+
+        from . import torch_ops
 
         seg = seg.reshape(-1)
         if not seg.is_cuda or not seg.is_contiguous():
@@ -129,46 +142,75 @@ class XgmiHalo:
         hl, hr = halo_sizes(taps, channels)
         if seg.numel() < max(hl, hr):
             raise ValueError("segment shorter than the filter halo")
+        self.seg, self.hl, self.hr = seg, hl, hr
+        self.timeout_s = float(timeout_s if timeout_s is not None else os.environ.get("FIR_GATE_TIMEOUT_S", 10.0))
+        elt = seg.element_size()
+        self.hl_bytes, self.hr_bytes = hl * elt, hr * elt
         dev = seg.device.index
-        handle, off = fir_hip.ipc_export(seg.data_ptr())
-        np_dtype = seg[:1].cpu().numpy().dtype
-        mine = {"handle": handle, "offset": off, "numel": seg.numel(), "elt": seg.element_size(),
-                "bus": fir_hip.device_bus_id(dev),
+        self.mailbox = torch.empty(fir_hip.halo_mailbox_bytes(self.hl_bytes, self.hr_bytes), dtype=torch.uint8,
+                                   device=seg.device)
+        torch_ops.halo_mailbox_init_dev(self.mailbox)
+        self.status = torch.zeros(1, dtype=torch.int32, device=seg.device)
+        self.left = torch.zeros(hl, dtype=seg.dtype, device=seg.device) if rank > 0 and hl else None
+        self.right = torch.zeros(hr, dtype=seg.dtype, device=seg.device) if rank < world - 1 and hr else None
+        torch.cuda.synchronize(seg.device)  # zeroed before any neighbour can map it
+        handle, off = fir_hip.ipc_export(self.mailbox.data_ptr())
+        mine = {"handle": handle, "offset": off, "bus": fir_hip.device_bus_id(dev),
                 "first": seg[:hr].cpu().numpy().tobytes(), "last": seg[seg.numel() - hl:].cpu().numpy().tobytes()}
         infos = [None] * world
         dist.all_gather_object(infos, mine, group=group)
-        self.left_ptr = self.right_ptr = None
-        self.left_host = self.right_host = None
+        self._expect = (infos[rank - 1]["last"] if rank > 0 else None, infos[rank + 1]["first"] if rank < world - 1 else None)
+        self.left_mb = self.right_mb = None
         self._mapped = []
-        # a kernel on this GPU will load from the neighbours' HBM: refuse (-> RCCL on every rank)
-        # unless this process sees that GPU with a peer path, before mapping anything
-        for r in ((rank - 1,) if rank > 0 and hl else ()) + ((rank + 1,) if rank < world - 1 and hr else ()):
-            if not fir_hip.peer_access(dev, infos[r]["bus"]):
-                raise RuntimeError(f"no peer access from device {dev} to rank {r}'s GPU {infos[r]['bus']}")
+        # the gate's kernel loads from and performs atomics on the neighbours' HBM: refuse (-> RCCL
+        # on every rank) unless this process sees both GPUs with peer access and peer atomics
+        for r in (rank - 1, rank + 1):
+            if 0 <= r < world:
+                bus = infos[r]["bus"]
+                if not (fir_hip.peer_access(dev, bus) and fir_hip.peer_atomics(dev, bus)):
+                    raise RuntimeError(f"no peer access / peer atomics from device {dev} to rank {r}'s GPU {bus}")
         try:
-            if rank > 0 and hl:
+            if rank > 0:
                 p = infos[rank - 1]
-                self.left_ptr = fir_hip.ipc_import(p["handle"], p["offset"] + (p["numel"] - hl) * p["elt"], dev)
-                self._mapped.append(self.left_ptr)
-                got = fir_hip.peek(self.left_ptr, hl * p["elt"])
-                if got != p["last"]:
-                    raise RuntimeError("left neighbour mapping reads the wrong samples")
-                self.left_host = np.frombuffer(got, dtype=np_dtype).copy()
-            if rank < world - 1 and hr:
+                self.left_mb = fir_hip.ipc_import(p["handle"], p["offset"], dev)
+                self._mapped.append(self.left_mb)
+            if rank < world - 1:
                 p = infos[rank + 1]
-                self.right_ptr = fir_hip.ipc_import(p["handle"], p["offset"], dev)
-                self._mapped.append(self.right_ptr)
-                got = fir_hip.peek(self.right_ptr, hr * p["elt"])
-                if got != p["first"]:
-                    raise RuntimeError("right neighbour mapping reads the wrong samples")
-                self.right_host = np.frombuffer(got, dtype=np_dtype).copy()
+                self.right_mb = fir_hip.ipc_import(p["handle"], p["offset"], dev)
+                self._mapped.append(self.right_mb)
         except Exception:
             self.close()
             raise
 
+    def gate(self, stream=None) -> None:
+        """Enqueue this step's ordered hand-off (after the step's segment is written)."""
+        from . import torch_ops
+
+        torch_ops.halo_gate_dev(self.seg, self.hl_bytes, self.hr_bytes, self.mailbox, self.left_mb, self.right_mb,
+                                self.left, self.right, self.status, self.timeout_s, stream)
+
     def halos(self):
-        """(left, right) device addresses for the edge kernel (None at the global ends)."""
-        return self.left_ptr, self.right_ptr
+        """(left, right) halo tensors of the last gate (None at the global ends)."""
+        return self.left, self.right
+
+    def check(self) -> None:
+        """Synchronising check of the gate's status (raises if any wait timed out)."""
+        import fir_hip
+
+        if int(self.status.item()) != 0:
+            raise fir_hip.FirHipError(f"halo gate: a neighbour's epoch did not arrive within {self.timeout_s} s")
+
+    def probe(self) -> bool:
+        """One gated hand-off of the resident segments (collective), checked against the edges the
+        neighbours reported at setup: True when the xGMI path delivered them."""
+        self.gate()
+        torch.cuda.synchronize(self.seg.device)
+        if int(self.status.item()) != 0:
+            return False
+        got = (None if self.left is None else self.left.cpu().numpy().tobytes(),
+               None if self.right is None else self.right.cpu().numpy().tobytes())
+        want = (self._expect[0] if self.left is not None else None, self._expect[1] if self.right is not None else None)
+        return got == want
 
     def close(self) -> None:
         import fir_hip
@@ -176,31 +218,44 @@ class XgmiHalo:
         for p in self._mapped:
             fir_hip.ipc_close(p)
         self._mapped = []
-        self.left_ptr = self.right_ptr = None
+        self.left_mb = self.right_mb = None
 
 
 def make_halo_source(seg: torch.Tensor, taps: int, channels: int = 1, group=None, prefer: str = "xgmi"):
     """The per-step halo source for a resident segment: XgmiHalo when every rank can map its
-    neighbours (decided collectively, so all ranks take the same path), else the RCCL
-    HaloExchange.  Returns (kind, source) with kind "xgmi" or "rccl"."""
-    ok, err = 0, None
-    src = None
+    neighbours and the first gated hand-off arrives intact on every rank (decided collectively,
+    so all ranks take the same path), else the RCCL HaloExchange.  Returns (kind, source) with
+    kind "xgmi" or "rccl"."""
+    world = dist.get_world_size(group)
+
+    def agree(ok: int) -> bool:
+        flags = [None] * world
+        dist.all_gather_object(flags, ok, group=group)
+        return all(flags)
+
+    src, err = None, None
     if prefer == "xgmi":
         try:
             src = XgmiHalo(seg, taps, channels, group)
-            ok = 1
         except Exception as e:  # noqa: BLE001 - any failure selects the RCCL path on every rank
             err = e
-        flags = [None] * dist.get_world_size(group)
-        dist.all_gather_object(flags, ok, group=group)
-        if all(flags):
-            return "xgmi", src
+        if agree(int(src is not None)):
+            ok = 0
+            try:
+                ok = int(src.probe())
+            except Exception as e:  # noqa: BLE001
+                err = e
+            if not ok and err is None:
+                err = RuntimeError("the first gated hand-off did not deliver the neighbours' edges")
+            if agree(ok):
+                return "xgmi", src
+        dist.barrier(group=group)  # every rank: no neighbour is still reading a mailbox
         if src is not None:
             src.close()
         if err is not None:
             import sys
 
-            print(f"fir_hip.sharded: xGMI halo mapping unavailable ({err}); using RCCL", file=sys.stderr)
+            print(f"fir_hip.sharded: xGMI halo path unavailable ({err}); using RCCL", file=sys.stderr)
     return "rccl", HaloExchange(seg, taps, channels, group)
 
 

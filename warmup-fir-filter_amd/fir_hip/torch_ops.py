@@ -152,6 +152,32 @@ def fir1d_fixed_segment_dev(x: torch.Tensor, hq, halo_left, halo_right, frac_bit
     return out
 
 
+def halo_mailbox_init_dev(mailbox: torch.Tensor, stream=None) -> torch.Tensor:
+    """Zero a halo-gate mailbox (a 128-byte-aligned uint8 device tensor) with device atomics."""
+    _check_dev(mailbox, "mailbox")
+    _check(lib().fir_halo_mailbox_init_dev(ctypes.c_void_p(mailbox.data_ptr()), mailbox.numel() * mailbox.element_size(),
+                                           _stream_ptr(mailbox, stream)), "fir_halo_mailbox_init_dev")
+    return mailbox
+
+
+def halo_gate_dev(seg: torch.Tensor, hl_bytes: int, hr_bytes: int, mailbox: torch.Tensor, left_mailbox: int | None,
+                  right_mailbox: int | None, halo_left: torch.Tensor | None, halo_right: torch.Tensor | None,
+                  status: torch.Tensor, timeout_s: float = 10.0, stream=None) -> None:
+    """One step's ordered halo hand-off (fir_hip.h, fir_halo_gate_dev): publish this segment's
+    edges, wait for both neighbours' (mapped mailbox addresses, None at a global end), copy
+    theirs into ``halo_left`` / ``halo_right``; ``status`` (int32 device scalar) receives 0 or
+    FIR_GATE_TIMEOUT."""
+    _check_dev(seg, "seg")
+    _check_dev(mailbox, "mailbox")
+    ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    _check(lib().fir_halo_gate_dev(ctypes.c_void_p(seg.data_ptr()), seg.numel() * seg.element_size(), int(hl_bytes),
+                                   int(hr_bytes), ctypes.c_void_p(mailbox.data_ptr()),
+                                   None if left_mailbox is None else ctypes.c_void_p(left_mailbox),
+                                   None if right_mailbox is None else ctypes.c_void_p(right_mailbox),
+                                   ptr(halo_left), ptr(halo_right), ptr(status), float(timeout_s),
+                                   _stream_ptr(seg, stream)), "fir_halo_gate_dev")
+
+
 def fir2d_fixed_dev(x: torch.Tensor, hq2, frac_bits: int = 12, acc_bits: int = 32, out_stage: int = OUT_U8_SAT,
                     out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
     """2-D fixed FIR of a uint8 device frame (H, W) or batch of frames (F, H, W), one launch."""
