@@ -17,7 +17,8 @@
  * see oracle/fir_oracle.py for their definitions.
  *
  * Index convention: y[n] = sum_k hq[k] * x[n - k + c], c = L/2.
- * Exact sums are int64 (|acc| < 2^52 for every supported input/tap width).
+ * Sums are accumulated mod 2^64 (uint64: exact for the wrap to acc_bits < 64, and the true
+ * sum for acc_bits >= 64 while |sum| < 2^63, which the library checks).
  */
 #include <stdint.h>
 #include <stddef.h>
@@ -33,8 +34,9 @@ static inline int64_t wrap_round(int64_t acc, int frac_bits, int acc_bits) {
         const int s = 64 - acc_bits;
         acc = (int64_t)((uint64_t)acc << s) >> s; /* gcc: arithmetic >> on signed */
     }
-    if (frac_bits > 62) return 0; /* |acc| < 2^52 <= 2^(f-1) */
-    return (acc + ((int64_t)1 << (frac_bits - 1))) >> frac_bits;
+    /* (v + 2^(f-1)) >> f on unbounded ints == (v >> f) + bit (f-1) of v; 0 for f >= 64, |v| < 2^63 */
+    if (frac_bits >= 64) return 0;
+    return (acc >> frac_bits) + ((acc >> (frac_bits - 1)) & 1);
 }
 
 static inline int64_t load_sample(const void* x, int in_dtype, int64_t i) {
@@ -104,7 +106,7 @@ int oracle_fir1d_rows(const void* x, int in_dtype, int64_t rows, int64_t width, 
                 continue;
             }
             for (int ch = 0; ch < channels; ++ch) {
-                int64_t acc = 0;
+                uint64_t acc = 0;
                 for (int k = 0; k < L; ++k) {
                     const int64_t idx = n - k + c;
                     int64_t v = 0;
@@ -115,7 +117,7 @@ int oracle_fir1d_rows(const void* x, int in_dtype, int64_t rows, int64_t width, 
                     } else if (idx >= width && halo_right) {
                         v = load_sample(halo_right, in_dtype, (idx - width) * channels + ch);
                     }
-                    acc += (int64_t)hq[k] * v;
+                    acc += (uint64_t)((int64_t)hq[k] * v);
                 }
                 store_out(y, out_stage, base + n * channels + ch, wrap_round(acc, frac_bits, acc_bits));
             }
@@ -137,14 +139,14 @@ int oracle_fir2d(const uint8_t* x, int64_t H, int64_t W, const int32_t* hq, int 
 #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < H; ++i) {
         for (int64_t j = 0; j < W; ++j) {
-            int64_t acc = 0;
+            uint64_t acc = 0;
             for (int m = 0; m < R; ++m) {
                 const int64_t ii = i - m + cr;
                 if (ii < 0 || ii >= H) continue;
                 for (int n = 0; n < C; ++n) {
                     const int64_t jj = j - n + cc;
                     if (jj < 0 || jj >= W) continue;
-                    acc += (int64_t)hq[m * C + n] * (int64_t)x[ii * W + jj];
+                    acc += (uint64_t)((int64_t)hq[m * C + n] * (int64_t)x[ii * W + jj]);
                 }
             }
             store_out(y, out_stage, i * W + j, wrap_round(acc, frac_bits, acc_bits));

@@ -71,15 +71,17 @@ def prep_x(x) -> np.ndarray:
 
 
 def wrap_round(acc: np.ndarray, frac_bits: int, acc_bits: int) -> np.ndarray:
-    """fir_1d_fixed_ref.py:94,110-120 on exact int64 sums (|acc| < 2^52 by construction)."""
+    """fir_1d_fixed_ref.py:94,110-120 on int64 sums: exact mod 2^64 (all the wrap to
+    acc_bits < 64 needs) or, for acc_bits >= 64, the exact sum (|acc| < 2^63).  The reference's
+    (v + 2^(f-1)) >> f on unbounded ints equals (v >> f) + bit (f-1) of v, which cannot
+    overflow; for f >= 64 it is 0 for every |v| < 2^63."""
     acc = np.asarray(acc, dtype=np.int64)
     if acc_bits < 64:
         s = np.uint64(64 - acc_bits)
         acc = ((acc.astype(np.uint64) << s).view(np.int64)) >> np.int64(64 - acc_bits)
-    if frac_bits > 62:
-        # |acc| < 2^52 <= 2^(f-1): (acc + 2^(f-1)) >> f == 0 for every reachable acc
+    if frac_bits >= 64:
         return np.zeros_like(acc)
-    return (acc + np.int64(1 << (frac_bits - 1))) >> np.int64(frac_bits)
+    return (acc >> np.int64(frac_bits)) + ((acc >> np.int64(frac_bits - 1)) & np.int64(1))
 
 
 def _stage(q: np.ndarray, out_stage: int) -> np.ndarray:
@@ -101,10 +103,11 @@ def _mac_rows(x2: np.ndarray, hq: np.ndarray, left: np.ndarray | None = None,
     rpad = np.zeros((rows, HR), np.int64) if right is None else np.asarray(right, np.int64).reshape(rows, HR)
     xp = np.concatenate([lpad, x2.astype(np.int64), rpad], axis=1)
     acc = np.zeros((rows, n), np.int64)
-    for k in range(L):
-        # x[n - k + c] sits at xp[n - k + c + HL] = xp[n + (L - 1) - k]
-        off = L - 1 - k
-        acc += np.int64(hq[k]) * xp[:, off:off + n]
+    with np.errstate(over="ignore"):  # int64 arithmetic wraps mod 2^64, which is what wrap_round needs
+        for k in range(L):
+            # x[n - k + c] sits at xp[n - k + c + HL] = xp[n + (L - 1) - k]
+            off = L - 1 - k
+            acc += np.int64(hq[k]) * xp[:, off:off + n]
     return acc
 
 

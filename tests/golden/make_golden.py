@@ -24,6 +24,8 @@ Files written:
   small_image_outputs.npz            full fixed/ideal outputs of the two 64x64 cases
   restore_u8.npz                     restore conversions (clip / normalize) of the 16 small
                                      ideal outputs and of edge-case arrays (ties, +-0, range ends)
+  long_taps.npz                      long filters (257 / 1000 / 2048 / 4099 taps, shorter and
+                                     longer than x): fir_1d_fixed_golden and fir_1d_ideal outputs
   meta.json                          generator environment
 
 Usage:  python tests/golden/make_golden.py [--jobs 8]
@@ -323,16 +325,66 @@ def gen_restore():
     return len(arrays)
 
 
+# (L, n, frac, acc, coeff, tap scale): every tap count the reference accepts is a legal input
+# (its loop runs over any len(h), fir_1d_fixed_ref.py:83-107; fir_1d_ref.py:49-63)
+LONG_FIXED = [(257, 3000, 12, 32, 16, 1e-2), (257, 50, 4, 32, 8, 1e-1), (1000, 2000, 20, 48, 32, 1e-3),
+              (1000, 999, 12, 24, 16, 1e-2), (1000, 1, 12, 32, 16, 1.0), (2048, 700, 12, 32, 16, 1e-2),
+              (4099, 1500, 12, 32, 16, 1e-3), (4099, 7, 12, 32, 16, 1e-1), (4099, 4099, 28, 64, 32, 1e-3),
+              (4099, 3000, 12, 20, 16, 1.0)]
+LONG_IDEAL = [(257, 3000, 1e-2), (1000, 1500, 1e-2), (2048, 600, 1.0), (4099, 1200, 1e-3), (4099, 5, 1e-1)]
+
+
+def gen_long_taps(fixed_ref, ideal_ref, seed=4099):
+    rng = np.random.default_rng(seed)
+    out = {}
+    xs, hs, ys, params = [], [], [], []
+    for L, n, frac, acc, coeff, scale in LONG_FIXED:
+        x = _rand_x(rng, n)
+        h = np.clip(_rand_h(rng, L, frac, coeff) * scale, -8.0, 8.0)
+        y = fixed_ref.fir_1d_fixed_golden(x.tolist(), h.tolist(), frac_bits=frac, acc_bits=acc, coeff_bits=coeff)
+        xs.append(x)
+        hs.append(h)
+        ys.append(np.asarray(y, dtype=np.uint8))
+        params.append((frac, acc, coeff))
+    for k, v in zip(("x", "x_off", "h", "h_off", "y", "y_off"), _ragged(xs, hs, ys)):
+        out["fixed_" + k] = v
+    out["fixed_params"] = np.array(params, dtype=np.int64)
+    xs, hs, ys = [], [], []
+    for L, n, scale in LONG_IDEAL:
+        x = _rand_x(rng, n)
+        h = rng.uniform(-8.0, 8.0, L) * scale
+        xs.append(x)
+        hs.append(h)
+        ys.append(np.asarray(ideal_ref.fir_1d_ideal(x.tolist(), h.tolist()), dtype=np.float64))
+    for k, v in zip(("x", "x_off", "h", "h_off", "y", "y_off"), _ragged(xs, hs, ys)):
+        out["ideal_" + k] = v
+    np.savez_compressed(OUT / "long_taps.npz", **out)
+    return len(LONG_FIXED) + len(LONG_IDEAL)
+
+
+def _ragged(xs, hs, ys):
+    def cat(parts, dtype):
+        off = np.zeros(len(parts) + 1, dtype=np.int64)
+        off[1:] = np.cumsum([len(p) for p in parts])
+        return np.concatenate(parts).astype(dtype), off
+
+    return (*cat(xs, np.float64), *cat(hs, np.float64), *cat(ys, ys[0].dtype))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("--skip-images", action="store_true")
     ap.add_argument("--only-restore", action="store_true")
+    ap.add_argument("--only-long", action="store_true")
     args = ap.parse_args()
     if args.only_restore:
         print("restore", gen_restore())
         return
     fixed_ref, ideal_ref, *_ = _ref_imports()
+    if args.only_long:
+        print("long_taps", gen_long_taps(fixed_ref, ideal_ref))
+        return
     import PIL
     meta = {"reference": str(REF), "numpy": np.__version__, "pillow": PIL.__version__,
             "python": sys.version.split()[0]}
@@ -342,6 +394,7 @@ def main():
     if not args.skip_images:
         print("images", gen_images(args.jobs))
     print("restore", gen_restore())
+    print("long_taps", gen_long_taps(fixed_ref, ideal_ref))
     (OUT / "meta.json").write_text(json.dumps(meta, indent=1) + "\n")
 
 

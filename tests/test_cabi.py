@@ -61,7 +61,8 @@ def test_errors_surface_as_firhiperror():
     with pytest.raises(fir_hip.FirHipError):
         fir_hip._taps_i32([])
     with pytest.raises(fir_hip.FirHipError):
-        fir_hip._taps_i32(list(range(fir_hip.MAX_TAPS + 1)))
+        fir_hip._taps_i32(np.ones(fir_hip.MAX_TAPS + 1, np.int64))
+    assert fir_hip._taps_i32(np.ones(4099, np.int64)).size == 4099  # long filters are legal
 
 
 def test_sharded_and_restore_argument_checks_without_device(lib):
@@ -118,3 +119,34 @@ def test_out_argument_is_checked_before_any_call():
     x16 = np.zeros(128, np.int16)
     with pytest.raises(fir_hip.FirHipError, match="overlap"):  # partial overlap via a view
         fir_hip.fir1d_fixed_rows(x16[:64].view(np.uint8), h, out=x16.view(np.uint8)[64:192])
+
+
+def test_stale_library_is_refused(tmp_path):
+    """The library carries the id of the sources it was built from (fir_build_id); the loader
+    refuses it when the sources beside it differ — one flipped source byte, no rebuild."""
+    import os
+    import shutil
+    import subprocess
+    import sys
+
+    pkg = Path(fir_hip.__file__).resolve().parents[1]  # warmup-fir-filter_amd/
+    dst = tmp_path / "tree" / pkg.name
+    shutil.copytree(pkg / "fir_hip", dst / "fir_hip", ignore=shutil.ignore_patterns("__pycache__"))
+    shutil.copytree(pkg / "csrc", dst / "csrc", ignore=shutil.ignore_patterns("build"))
+    (dst.parent / "include").mkdir()
+    shutil.copy(HEADER, dst.parent / "include" / HEADER.name)
+    env = {k: v for k, v in os.environ.items() if k != "FIR_HIP_LIB"}
+    probe = f"import sys; sys.path.insert(0, {str(dst)!r}); import fir_hip; fir_hip.lib(); print(fir_hip.build_id())"
+
+    ok = subprocess.run([sys.executable, "-c", probe], env=env, capture_output=True, text=True)
+    assert ok.returncode == 0, ok.stderr
+    assert ok.stdout.strip() == fir_hip.build_id()
+
+    src = dst / "csrc" / "fir1d.hip"
+    data = bytearray(src.read_bytes())
+    i = data.index(b"gfx950")
+    data[i] ^= 0x20  # 'g' -> 'G' inside a comment: the compiled code would not even change
+    src.write_bytes(bytes(data))
+    bad = subprocess.run([sys.executable, "-c", probe], env=env, capture_output=True, text=True)
+    assert bad.returncode != 0
+    assert "built from other sources" in bad.stderr

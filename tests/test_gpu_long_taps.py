@@ -1,0 +1,150 @@
+"""GPU: filters of any length, as the reference accepts them (its MAC loop runs over any
+len(h): fir_1d/model/python/fir_1d_fixed_ref.py:83-107, fir_1d/model/python/fir_1d_ref.py:49-63).
+
+* the drop-in API (fir_1d_fixed_golden, fir_1d_ideal) with 257 / 1000 / 2048 / 4099 taps against
+  the reference's own outputs (tests/golden/long_taps.npz, made by make_golden.py), x shorter
+  and longer than h;
+* the library entries past the old 256-tap / (L-1)*channels <= 1024 limits against the C
+  oracle: L = 1000 over 2^24 int16 samples, long u8 rows, complex and many-channel signals,
+  long-halo segments, fused banks, the f64 ideal rows and 2-D kernels of 17x17 and 300 taps;
+* acc_bits >= 64 with a sum that could exceed 64 bits is refused, not wrapped.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+import fir_hip
+from conftest import GOLDEN
+from fir_1d.model.python.fir_1d_fixed_ref import fir_1d_fixed_golden
+from fir_1d.model.python.fir_1d_ref import fir_1d_ideal
+from fir_hip import torch_ops
+from oracle import c_oracle, fir_oracle as fo
+
+DEV = torch.device("cuda:0")
+
+
+def _long_cases(kind: str):
+    with np.load(GOLDEN / "long_taps.npz") as d:
+        xo, ho, yo = d[kind + "_x_off"], d[kind + "_h_off"], d[kind + "_y_off"]
+        params = d["fixed_params"] if kind == "fixed" else None
+        for i in range(len(xo) - 1):
+            p = tuple(int(v) for v in params[i]) if params is not None else ()
+            yield (d[kind + "_x"][xo[i]:xo[i + 1]], d[kind + "_h"][ho[i]:ho[i + 1]], p,
+                   d[kind + "_y"][yo[i]:yo[i + 1]])
+
+
+def test_fixed_golden_long_filters_reference_outputs():
+    n = 0
+    for x, h, (f, a, c), y in _long_cases("fixed"):
+        got = fir_1d_fixed_golden(x.tolist(), h.tolist(), frac_bits=f, acc_bits=a, coeff_bits=c)
+        assert np.array_equal(got, y), (len(h), len(x), f, a, c)
+        n += 1
+    assert n == 10
+
+
+def test_ideal_long_filters_reference_outputs():
+    n = 0
+    for x, h, _, y in _long_cases("ideal"):
+        got = np.asarray(fir_1d_ideal(x.tolist(), h.tolist()), dtype=np.float64)
+        assert got.tobytes() == y.tobytes(), (len(h), len(x))
+        n += 1
+    assert n == 5
+
+
+@pytest.mark.parametrize("L", [65, 257, 1000])
+def test_int16_2p24_long_filter_vs_c_oracle(L):
+    """L = 1000 over 2^24 int16 -> int32 (and the 64-tap boundary past it)."""
+    rng = np.random.default_rng(L)
+    x = rng.integers(-32768, 32768, 1 << 24, dtype=np.int16)
+    hq = rng.integers(-3000, 3000, L)
+    co = c_oracle()
+    got = fir_hip.fir1d_fixed_rows(x, hq, 12, 32, fir_hip.OUT_I32)
+    assert np.array_equal(got, co.fir1d_rows(x, hq, 12, 32, co.OUT_I32))
+
+
+@pytest.mark.parametrize("L,shape,stage,dtype", [
+    (257, (64, 4096), fir_hip.OUT_U8_SAT, np.uint8), (1000, (33, 1031), fir_hip.OUT_U8_SAT, np.uint8),
+    (300, (17, 4096), fir_hip.OUT_I32, np.int16), (4099, (3, 5000), fir_hip.OUT_I32, np.int16),
+    (513, (1, 777), fir_hip.OUT_U8_SAT, np.uint8), (4099, (2, 100), fir_hip.OUT_I32, np.int16)])
+def test_long_filter_rows_vs_oracle(L, shape, stage, dtype):
+    rng = np.random.default_rng(L + shape[1])
+    lo, hi = (0, 256) if dtype == np.uint8 else (-32768, 32768)
+    x = rng.integers(lo, hi, shape, dtype=dtype)
+    hq = rng.integers(-400, 400, L)
+    co = c_oracle()
+    for frac, acc in ((12, 32), (16, 24), (20, 48)):
+        got = fir_hip.fir1d_fixed_rows(x, hq, frac, acc, stage)
+        assert np.array_equal(got, co.fir1d_rows(x, hq, frac, acc, stage)), (frac, acc)
+
+
+@pytest.mark.parametrize("L,ch", [(700, 2), (3, 5000), (40, 64), (129, 16)])
+def test_long_halo_channels_vs_oracle(L, ch):
+    """(L-1) * channels far past the old 1024-sample halo limit."""
+    rng = np.random.default_rng(L * ch)
+    x = rng.integers(-32768, 32768, (3, 37 * ch), dtype=np.int16)
+    hq = rng.integers(-2000, 2000, L)
+    got = fir_hip.fir1d_fixed_rows(x, hq, 12, 32, fir_hip.OUT_I32, channels=ch)
+    assert np.array_equal(got, fo.fir1d_rows(x, hq, 12, 32, fo.OUT_I32, channels=ch))
+
+
+@pytest.mark.parametrize("L", [301, 1024])
+def test_long_halo_segment_vs_oracle(L):
+    """A sharded segment whose halos are hundreds of samples (fir1d_fixed_segment_dev)."""
+    rng = np.random.default_rng(L)
+    n = 20_000
+    x = rng.integers(-32768, 32768, n, dtype=np.int16)
+    hq = rng.integers(-2000, 2000, L)
+    hl_n, hr_n = fo.halo_sizes(L)
+    hlv = rng.integers(-32768, 32768, hl_n, dtype=np.int16)
+    hrv = rng.integers(-32768, 32768, hr_n, dtype=np.int16)
+    y = torch_ops.fir1d_fixed_segment_dev(torch.from_numpy(x).to(DEV), hq, torch.from_numpy(hlv).to(DEV),
+                                          torch.from_numpy(hrv).to(DEV), 12, 32, fir_hip.OUT_I32)
+    want = c_oracle().fir1d_rows(x, hq, 12, 32, c_oracle().OUT_I32, halo_left=hlv, halo_right=hrv)
+    assert np.array_equal(y.cpu().numpy(), want)
+
+
+def test_long_filter_bank_and_sharded_entries():
+    rng = np.random.default_rng(5)
+    x = rng.integers(0, 256, (9, 2048), dtype=np.uint8)
+    bank = rng.integers(-300, 300, (3, 333))
+    got = fir_hip.fir1d_fixed_rows_multi(x, bank, 12, 32, fir_hip.OUT_U8_SAT)
+    for f in range(3):
+        assert np.array_equal(got[f], fo.fir1d_rows(x, bank[f], 12, 32, fo.OUT_U8_SAT)), f
+    x1 = rng.integers(-32768, 32768, 100_003, dtype=np.int16)
+    hq = rng.integers(-2000, 2000, 999)
+    got = fir_hip.fir1d_fixed_rows_sharded(x1, hq, 12, 32, fir_hip.OUT_I32, devices=[0, 0, 0])
+    assert np.array_equal(got, c_oracle().fir1d_rows(x1, hq, 12, 32, c_oracle().OUT_I32))
+
+
+@pytest.mark.parametrize("L", [10, 257, 1025, 4099])
+def test_ideal_long_rows_vs_oracle(L):
+    rng = np.random.default_rng(L)
+    x = rng.integers(0, 256, (7, 3001), dtype=np.uint8)
+    h = rng.uniform(-1.0, 1.0, L)
+    got = fir_hip.fir1d_ideal_rows(x, h)
+    assert got.tobytes() == c_oracle().fir1d_ideal_rows(x, h).tobytes()
+
+
+@pytest.mark.parametrize("R,C,shape", [(17, 17, (300, 517)), (5, 60, (77, 256)), (33, 9, (70000, 16)),
+                                       (1, 300, (40, 1000))])
+def test_fir2d_many_taps_vs_oracle(R, C, shape):
+    """2-D kernels past the old R*C <= 256 limit, and a frame taller than 65535 rows."""
+    rng = np.random.default_rng(R * C)
+    x = rng.integers(0, 256, shape, dtype=np.uint8)
+    hq = rng.integers(-200, 200, (R, C))
+    co = c_oracle()
+    for stage in (fir_hip.OUT_U8_SAT, fir_hip.OUT_I32):
+        got = fir_hip.fir2d_fixed(x, hq, 12, 32, stage)
+        assert np.array_equal(got, co.fir2d(x, hq, 12, 32, stage)), stage
+
+
+def test_acc64_overflow_is_refused():
+    """acc_bits >= 64 promises the exact sum: refused when it could exceed 64 bits."""
+    x = np.zeros(16, np.int16)
+    hq = np.full((1 << 17) + 1000, (1 << 31) - 1, np.int64)
+    with pytest.raises(fir_hip.FirHipError, match="exceeds 64 bits"):
+        fir_hip.fir1d_fixed_rows(x, hq, 12, 64, fir_hip.OUT_I32)
+    # the same taps with a wrap to 64 - 1 bits are exact mod 2^64 and accepted
+    assert fir_hip.fir1d_fixed_rows(x, hq, 12, 63, fir_hip.OUT_I32).tolist() == [0] * 16

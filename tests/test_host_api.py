@@ -91,7 +91,24 @@ def test_quantization_matches_oracle_on_random_sweep():
 
 
 def test_device_bits_clamp_is_result_preserving():
-    acc = np.array([-(1 << 51), -5, 0, 7, (1 << 51) - 1], dtype=np.int64)
-    for f, a in ((12, 70), (12, 64), (70, 32), (63, 40), (62, 100)):
+    acc = np.array([-(1 << 63), -(1 << 62) - 1, -(1 << 51), -5, -1, 0, 7, (1 << 51) - 1, (1 << 63) - 1], dtype=np.int64)
+    for f, a in ((12, 70), (12, 64), (70, 32), (63, 40), (62, 100), (64, 64), (65, 64), (200, 200), (63, 64)):
         fd, ad = device_bits(f, a)
         assert np.array_equal(fo.wrap_round(acc, f, a), fo.wrap_round(acc, fd, ad))
+
+
+def test_wrap_round_equals_unbounded_reference_arithmetic():
+    """fir_1d_fixed_ref.py:110-120 on Python ints vs the oracle's overflow-free int64 form, for
+    sums up to the full int64 range (long filters) and every frac / acc width class."""
+    rng = np.random.default_rng(63)
+    acc = np.concatenate([rng.integers(-(1 << 63), (1 << 63) - 1, 400, dtype=np.int64),
+                          np.array([-(1 << 63), (1 << 63) - 1, -1, 0, 1], dtype=np.int64)])
+    for f in (1, 2, 12, 31, 32, 52, 62, 63, 64, 65, 90):
+        for a in (1, 8, 32, 33, 63, 64, 70):
+            got = fo.wrap_round(acc, f, a)
+            for v, g in zip(acc.tolist(), got.tolist()):
+                if a < 64:  # the reference's mask + sign restore
+                    v &= (1 << a) - 1
+                    if v & (1 << (a - 1)):
+                        v -= 1 << a
+                assert g == (v + (1 << (f - 1))) >> f, (v, f, a)

@@ -16,9 +16,9 @@
 //    1 KiB rows.  Rows that are a whole number of vectors zero the out-of-row halo and
 //    stay on the unmasked path; other widths mask the vectors that straddle a row edge.
 //  * fir1d_generic_kernel — every other configuration (any tap count up to FIR_MAX_TAPS,
-//    any acc_bits / frac_bits, unaligned buffers, narrow rows, halo segments): a
-//    workgroup stages an LDS sliding-window tile of 1024 outputs + (L-1)*channels halo
-//    samples, then every thread forms its outputs from LDS with an exact int64 sum.
+//    any channel count, any acc_bits / frac_bits, unaligned buffers, narrow rows, halo
+//    segments): a workgroup owns 1024 outputs and walks the taps (read from HBM) in chunks,
+//    staging each chunk's taps and window in LDS; exact 64-bit sums.
 #include <algorithm>
 #include <string>
 
@@ -42,86 +42,98 @@
 namespace fir {
 
 // ---------------------------------------------------------------------------------------
-// Generic LDS sliding-window kernel.
+// Generic LDS sliding-window kernel: any tap count, any channel count.  A workgroup owns
+// kGenTile consecutive outputs; the taps (device memory) are taken kc at a time: each chunk
+// stages its kc taps and the kGenTile + (kc-1)*ch samples they touch in LDS, and every thread
+// adds the chunk's products to its outputs' sums (uint64: exact mod 2^64, which is all the
+// wrap to acc_bits <= 64 needs, and the exact value while |sum| < 2^63, host-checked).
 constexpr int kGenTile = 1024;
-constexpr int kGenMaxHalo = 1024;  // (L-1) * channels
+constexpr int kGenWin = 4096;       // LDS window samples
+constexpr int kGenTapChunk = 1024;  // taps per LDS chunk
+constexpr int kGenPer = kGenTile / kBlock;
 
-struct TapsG {
-    int32_t h[FIR_MAX_TAPS];
-};
+// taps per chunk for `ch` interleaved channels: the window kGenTile + (kc-1)*ch fits kGenWin
+static int gen_tap_chunk(int L, int64_t ch) {
+    const int64_t kc = (kGenWin - kGenTile) / ch + 1;
+    return (int)std::min<int64_t>(std::min<int64_t>(kc, kGenTapChunk), L);
+}
+
+// sample gi of a segment [0, total) with optional halos before / after it (zeros otherwise)
+template <typename InT>
+__device__ __forceinline__ int32_t seg_sample(const InT* __restrict__ x, int64_t gi, int64_t total,
+                                              const InT* __restrict__ halo_l, int64_t hle,
+                                              const InT* __restrict__ halo_r, int64_t hre) {
+    if (gi >= 0 && gi < total) return (int32_t)x[gi];
+    if (gi < 0) return halo_l && gi >= -hle ? (int32_t)halo_l[hle + gi] : 0;
+    return halo_r && gi < total + hre ? (int32_t)halo_r[gi - total] : 0;
+}
 
 template <typename InT, int STAGE>
 __global__ __launch_bounds__(kBlock) void fir1d_generic_kernel(const InT* __restrict__ x,
                                                                typename OutTraits<STAGE>::T* __restrict__ y,
                                                                int64_t start, int64_t end, int64_t total,
-                                                               int64_t rowlen, int multi_row, int ch,
+                                                               int64_t rowlen, int multi_row, int64_t ch,
                                                                const InT* __restrict__ halo_l,
-                                                               const InT* __restrict__ halo_r, TapsG taps, int L,
+                                                               const InT* __restrict__ halo_r,
+                                                               const int32_t* __restrict__ taps, int L, int KC,
                                                                int frac, int acc_bits) {
-    __shared__ int32_t s_taps[FIR_MAX_TAPS];
-    __shared__ int32_t s_x[kGenTile + kGenMaxHalo];
+    __shared__ int32_t s_taps[kGenTapChunk];
+    __shared__ int32_t s_x[kGenWin];
     const int c = L / 2;
-    const int HLE = (L - 1 - c) * ch;
-    const int HRE = c * ch;
+    const int64_t HLE = (int64_t)(L - 1 - c) * ch, HRE = (int64_t)c * ch;
     const int64_t t0 = start + (int64_t)blockIdx.x * kGenTile;
-    const int span = kGenTile + HLE + HRE;
+    uint64_t acc[kGenPer] = {};
+    int64_t col[kGenPer];
+#pragma unroll
+    for (int j = 0; j < kGenPer; ++j) col[j] = multi_row ? (t0 + threadIdx.x + j * kBlock) % rowlen : 0;
 
-    for (int k = threadIdx.x; k < L; k += kBlock) s_taps[k] = taps.h[k];
-    for (int i = threadIdx.x; i < span; i += kBlock) {
-        const int64_t gi = t0 - HLE + i;
-        int32_t val = 0;
-        if (gi >= 0 && gi < total) {
-            val = (int32_t)x[gi];
-        } else if (gi < 0) {
-            if (halo_l && gi >= -HLE) val = (int32_t)halo_l[HLE + gi];
-        } else if (halo_r && gi < total + HRE) {
-            val = (int32_t)halo_r[gi - total];
+    for (int k0 = 0; k0 < L; k0 += KC) {
+        const int kc = min(KC, L - k0);
+        // outputs t0 + i use samples t0 + i + (c - k) * ch, k in [k0, k0 + kc): window from
+        // w0 = t0 + (c - k0 - kc + 1) * ch, output i's tap k at window index i + (kc - 1 - (k - k0)) * ch
+        const int64_t w0 = t0 + (int64_t)(c - k0 - kc + 1) * ch;
+        const int span = kGenTile + (kc - 1) * (int)ch;
+        __syncthreads();  // the previous chunk's reads are done
+        for (int k = threadIdx.x; k < kc; k += kBlock) s_taps[k] = taps[k0 + k];
+        for (int i = threadIdx.x; i < span; i += kBlock) s_x[i] = seg_sample(x, w0 + i, total, halo_l, HLE, halo_r, HRE);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kGenPer; ++j) {
+            const int i = threadIdx.x + j * kBlock;
+            for (int k = 0; k < kc; ++k) {
+                int32_t xv = s_x[i + (kc - 1 - k) * (int)ch];
+                if (multi_row) {
+                    const int64_t d = (int64_t)(c - k0 - k) * ch;
+                    if (col[j] + d < 0 || col[j] + d >= rowlen) xv = 0;
+                }
+                acc[j] += (uint64_t)((int64_t)s_taps[k] * xv);
+            }
         }
-        s_x[i] = val;
     }
-    __syncthreads();
-
-    for (int i = threadIdx.x; i < kGenTile; i += kBlock) {
-        const int64_t gi = t0 + i;
-        if (gi >= end) break;
-        const int64_t col = multi_row ? gi % rowlen : 0;
-        int64_t acc = 0;
-        for (int k = 0; k < L; ++k) {
-            const int d = (c - k) * ch;
-            int32_t xv = s_x[HLE + i + d];
-            if (multi_row && (col + d < 0 || col + d >= rowlen)) xv = 0;
-            acc += (int64_t)s_taps[k] * xv;
-        }
-        y[gi] = stage_out<STAGE>(round64(acc, frac, acc_bits));
+#pragma unroll
+    for (int j = 0; j < kGenPer; ++j) {
+        const int64_t gi = t0 + threadIdx.x + j * kBlock;
+        if (gi < end) y[gi] = stage_out<STAGE>(round64((int64_t)acc[j], frac, acc_bits));
     }
 }
 
 // Both edges of a single-row segment in one launch (multi-GPU step): output j < hle is the
 // left edge, j >= hle maps to the right edge total - hre + (j - hle).  Samples left of the
-// segment come from halo_l, right of it from halo_r (zeros when NULL).  Exact int64 sums.
+// segment come from halo_l, right of it from halo_r (zeros when NULL).  Exact 64-bit sums.
 template <typename InT, int STAGE>
 __global__ __launch_bounds__(kBlock) void fir1d_edges_kernel(const InT* __restrict__ x,
                                                              typename OutTraits<STAGE>::T* __restrict__ y,
-                                                             int64_t total, int ch, const InT* __restrict__ halo_l,
-                                                             const InT* __restrict__ halo_r, TapsG taps, int L,
-                                                             int hle, int hre, int frac, int acc_bits) {
+                                                             int64_t total, int64_t ch, const InT* __restrict__ halo_l,
+                                                             const InT* __restrict__ halo_r,
+                                                             const int32_t* __restrict__ taps, int L, int64_t hle,
+                                                             int64_t hre, int frac, int acc_bits) {
     const int c = L / 2;
-    for (int j = threadIdx.x; j < hle + hre; j += kBlock) {
+    for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < hle + hre; j += (int64_t)gridDim.x * kBlock) {
         const int64_t gi = j < hle ? j : total - hre + (j - hle);
-        int64_t acc = 0;
-        for (int k = 0; k < L; ++k) {
-            const int64_t si = gi + (int64_t)(c - k) * ch;
-            int32_t v = 0;
-            if (si >= 0 && si < total) {
-                v = (int32_t)x[si];
-            } else if (si < 0) {
-                if (halo_l) v = (int32_t)halo_l[hle + si];
-            } else if (halo_r) {
-                v = (int32_t)halo_r[si - total];
-            }
-            acc += (int64_t)taps.h[k] * v;
-        }
-        y[gi] = stage_out<STAGE>(round64(acc, frac, acc_bits));
+        uint64_t acc = 0;
+        for (int k = 0; k < L; ++k)
+            acc += (uint64_t)((int64_t)taps[k] * seg_sample(x, gi + (int64_t)(c - k) * ch, total, halo_l, hle, halo_r, hre));
+        y[gi] = stage_out<STAGE>(round64((int64_t)acc, frac, acc_bits));
     }
 }
 
@@ -134,13 +146,14 @@ static hipError_t launch_generic(const void* x, void* y, int64_t start, int64_t 
                                  const int32_t* hq, int L, int frac, int acc_bits, hipStream_t stream) {
     using OutT = typename OutTraits<STAGE>::T;
     if (end <= start) return hipSuccess;
-    TapsG t;
-    for (int k = 0; k < L; ++k) t.h[k] = hq[k];
-    for (int k = L; k < FIR_MAX_TAPS; ++k) t.h[k] = 0;
+    std::string err;
+    const int32_t* td = (const int32_t*)device_table(hq, sizeof(int32_t) * (size_t)L, &err);
+    if (!td) return hipErrorOutOfMemory;
     const int64_t blocks = (end - start + kGenTile - 1) / kGenTile;
+    if (blocks >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
     hipLaunchKernelGGL((fir1d_generic_kernel<InT, STAGE>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
-                       (const InT*)x, (OutT*)y, start, end, total, rowlen, multi_row ? 1 : 0, ch, (const InT*)hl,
-                       (const InT*)hr, t, L, frac, acc_bits);
+                       (const InT*)x, (OutT*)y, start, end, total, rowlen, multi_row ? 1 : 0, (int64_t)ch,
+                       (const InT*)hl, (const InT*)hr, td, L, gen_tap_chunk(L, ch), frac, acc_bits);
     return hipGetLastError();
 }
 
@@ -164,11 +177,12 @@ static hipError_t dispatch_generic(int in_dtype, int stage, const void* x, void*
 
 template <typename InT, int STAGE>
 static hipError_t launch_edges(const void* x, void* y, int64_t total, int ch, const void* hl, const void* hr,
-                               const TapsG& t, int L, int64_t hle, int64_t hre, int frac, int acc_bits,
+                               const int32_t* td, int L, int64_t hle, int64_t hre, int frac, int acc_bits,
                                hipStream_t stream) {
-    hipLaunchKernelGGL((fir1d_edges_kernel<InT, STAGE>), dim3(1), dim3(kBlock), 0, stream, (const InT*)x,
-                       (typename OutTraits<STAGE>::T*)y, total, ch, (const InT*)hl, (const InT*)hr, t, L, (int)hle,
-                       (int)hre, frac, acc_bits);
+    const int64_t blocks = std::min<int64_t>((hle + hre + kBlock - 1) / kBlock, 1024);
+    hipLaunchKernelGGL((fir1d_edges_kernel<InT, STAGE>), dim3((unsigned)blocks), dim3(kBlock), 0, stream, (const InT*)x,
+                       (typename OutTraits<STAGE>::T*)y, total, (int64_t)ch, (const InT*)hl, (const InT*)hr, td, L,
+                       hle, hre, frac, acc_bits);
     return hipGetLastError();
 }
 
@@ -180,8 +194,14 @@ static int check_common(int in_dtype, int64_t rows, int64_t width, int ch, const
     if (ch < 1) return *err = "channels must be >= 1", FIR_EINVAL;
     if (!hq) return *err = "hq must not be NULL", FIR_EINVAL;
     if (L < 1 || L > FIR_MAX_TAPS) return *err = "taps must be in [1, " + std::to_string(FIR_MAX_TAPS) + "]", FIR_EINVAL;
-    if ((int64_t)(L - 1) * ch > kGenMaxHalo) return *err = "(taps-1)*channels exceeds 1024", FIR_EINVAL;
     if (frac < 1 || acc_bits < 1) return *err = "frac_bits and acc_bits must be >= 1", FIR_EINVAL;
+    if (acc_bits >= 64) {  // no wrap: the 64-bit sum must be the exact one
+        int64_t habs = 0;
+        for (int k = 0; k < L; ++k) habs += hq[k] < 0 ? -(int64_t)hq[k] : hq[k];
+        const int64_t xmax = in_dtype == FIR_IN_U8 ? 255 : 32768;
+        if (habs > (INT64_MAX - 1) / xmax)
+            return *err = "acc_bits >= 64 with sum|hq| * max|x| >= 2^63: the sum exceeds 64 bits", FIR_EINVAL;
+    }
     return FIR_OK;
 }
 
@@ -327,16 +347,16 @@ int launch_fir1d_edges(const void* x, int in_dtype, int64_t n, int ch, const int
         e = dispatch_generic(in_dtype, stage, x, y, 0, total, total, total, false, ch, hl, hr, hq, L, frac, acc_bits,
                              stream);
     } else if (hle + hre > 0) {  // both edges, one launch
-        TapsG t;
-        for (int k = 0; k < FIR_MAX_TAPS; ++k) t.h[k] = k < L ? hq[k] : 0;
+        const int32_t* td = (const int32_t*)device_table(hq, sizeof(int32_t) * (size_t)L, err);
+        if (!td) return FIR_ENOMEM;
         if (in_dtype == FIR_IN_U8)
             e = stage == FIR_OUT_U8_SAT
-                    ? launch_edges<uint8_t, FIR_OUT_U8_SAT>(x, y, total, ch, hl, hr, t, L, hle, hre, frac, acc_bits, stream)
-                    : launch_edges<uint8_t, FIR_OUT_I32>(x, y, total, ch, hl, hr, t, L, hle, hre, frac, acc_bits, stream);
+                    ? launch_edges<uint8_t, FIR_OUT_U8_SAT>(x, y, total, ch, hl, hr, td, L, hle, hre, frac, acc_bits, stream)
+                    : launch_edges<uint8_t, FIR_OUT_I32>(x, y, total, ch, hl, hr, td, L, hle, hre, frac, acc_bits, stream);
         else
             e = stage == FIR_OUT_U8_SAT
-                    ? launch_edges<int16_t, FIR_OUT_U8_SAT>(x, y, total, ch, hl, hr, t, L, hle, hre, frac, acc_bits, stream)
-                    : launch_edges<int16_t, FIR_OUT_I32>(x, y, total, ch, hl, hr, t, L, hle, hre, frac, acc_bits, stream);
+                    ? launch_edges<int16_t, FIR_OUT_U8_SAT>(x, y, total, ch, hl, hr, td, L, hle, hre, frac, acc_bits, stream)
+                    : launch_edges<int16_t, FIR_OUT_I32>(x, y, total, ch, hl, hr, td, L, hle, hre, frac, acc_bits, stream);
     }
     if (e != hipSuccess) return *err = std::string("fir1d edge launch failed: ") + hipGetErrorString(e), FIR_EHIP;
     return FIR_OK;

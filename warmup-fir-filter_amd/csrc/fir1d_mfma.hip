@@ -1,4 +1,4 @@
-// fir1d_mfma.hip — long 1-D fixed-point filters (10..64 taps) on the matrix cores, SURVEY §8 a1/a6.
+// fir1d_mfma.hip — long 1-D fixed-point filters (10 taps and up) on the matrix cores, SURVEY §8 a1/a6.
 //
 // Arithmetic: fir_1d/model/python/fir_1d_fixed_ref.py:95-126 (reference root): y[n] =
 // sum_t h[t] x[n - t + L/2] wrapped to acc_bits, rounded, staged (u8 saturate or int32).
@@ -25,6 +25,7 @@
 // loop.  Outputs go back through the same LDS as whole 1 KiB rows.  Rows (images) whose length
 // is a multiple of 8 are tiled row by row, samples of other rows zeroed while staging.
 #include <string>
+#include <vector>
 
 #include "fir_common.h"
 #include "fir_launch.h"
@@ -79,8 +80,8 @@ struct MfTile {
     int64_t rs, re, ts;
 };
 
-// tile -> row bounds and start; tile and tiles_per_row are wave-uniform and below 2^32 (total <
-// 2^40 samples), so this is one 32-bit scalar division per tile, not a 64-bit VALU one
+// tile -> row bounds and start; tile and tiles_per_row are wave-uniform and the tile count is
+// below 2^32 (mfma_path_ok), so this is one 32-bit scalar division per tile, not a 64-bit VALU one
 __device__ __forceinline__ MfTile mf_tile(uint32_t tile, int64_t rowlen, uint32_t tiles_per_row) {
     const uint32_t row = __builtin_amdgcn_readfirstlane(tile / tiles_per_row);
     const uint32_t tr = __builtin_amdgcn_readfirstlane(tile - row * tiles_per_row);
@@ -127,7 +128,8 @@ __global__ __launch_bounds__(kBlock, FIR_MFMA_MINB) void fir1d_mfma_kernel(const
         a_lo[s] = mf_i32x4{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3]};
         a_hi[s] = mf_i32x4{(int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
     }
-    const int32_t sat_hi = (256 << frac) - 1;  // FAST u8 stage: clamp the biased sum, then shift
+    // FAST u8 stage: clamp the biased sum, then shift (FAST implies frac <= 22; unused otherwise)
+    const int32_t sat_hi = FAST ? (int32_t)((256u << (frac & 31)) - 1u) : 0;
 
     const uint32_t step = gridDim.x * kMfWaves, nt32 = (uint32_t)ntiles, tpr = (uint32_t)tiles_per_row;
     uint32_t tile = blockIdx.x * kMfWaves + wv;
@@ -295,6 +297,193 @@ __global__ __launch_bounds__(kBlock, FIR_MFMA_MINB) void fir1d_mfma_kernel(const
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Filters longer than kMfMaxTaps (any length): the same Toeplitz product with K = 32 + L/2 + P
+// split into chunks of kMlChunk k-steps.  Per tile and chunk the wave stages the chunk's window
+// (992 + 32 * steps samples) as byte planes in its LDS, then runs the chunk's k-steps with the
+// accumulators carried over: the tap fragments no longer fit VGPRs, so each k-step's A fragments
+// come from a table in HBM (frag[s][plane][lane], 16 bytes per lane: one coalesced 1 KiB load per
+// plane, the same for every tile, so L2-resident).
+constexpr int kMlChunk = 16;                          // k-steps per staged window
+constexpr int kMlWin = 32 * 31 + 32 * kMlChunk;       // window samples per chunk (1504)
+constexpr int kMlNV = kMlWin / 8;                     // 8-sample vectors
+constexpr int kMlNIT = (kMlNV + kWave - 1) / kWave;   // per lane
+constexpr int kMlPlane = mf_pos(kMlWin);
+
+template <typename InT, int STAGE, bool ACC32, bool FAST>
+__global__ __launch_bounds__(kBlock) void fir1d_mfma_long_kernel(const InT* __restrict__ x,
+                                                                 typename OutTraits<STAGE>::T* __restrict__ y,
+                                                                 int64_t rowlen, int64_t tiles_per_row, int64_t ntiles,
+                                                                 const mf_i32x4* __restrict__ frag, int KS, int P,
+                                                                 uint32_t bias, int shl, int frac) {
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+    constexpr bool I16 = sizeof(InT) == 2;
+    constexpr int WBYTES = (I16 ? 2 * kMlPlane : kMlPlane) > 4608 ? (I16 ? 2 * kMlPlane : kMlPlane) : 4608;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kMfWaves][WBYTES];
+
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & 31, hf = lane >> 5;
+    uint8_t* pl = lds[wv];
+    uint8_t* ph = lds[wv] + kMlPlane;
+    const int32_t sat_hi = FAST ? (int32_t)((256u << (frac & 31)) - 1u) : 0;
+    const uint32_t step = gridDim.x * kMfWaves, nt32 = (uint32_t)ntiles, tpr = (uint32_t)tiles_per_row;
+
+    for (uint32_t tile = blockIdx.x * kMfWaves + wv; tile < nt32; tile += step) {
+        const MfTile t = mf_tile(tile, rowlen, tpr);
+        const int m = (int)min((int64_t)kMfTile, t.re - t.ts);
+        mf_i32x16 acc_ll = {}, acc_mid = {}, acc_m2 = {}, acc_hh = {};
+        for (int s0 = 0; s0 < KS; s0 += kMlChunk) {
+            const int steps = min(kMlChunk, KS - s0);
+            const int nv = (32 * 31 + 32 * steps) / 8;
+            // ---- the chunk's window [w0, w0 + 8 nv) through a descriptor over this row's part of it
+            const int64_t w0 = t.ts - P + 32 * (int64_t)s0, base = w0 > t.rs ? w0 : t.rs;
+            const int64_t end = t.re < w0 + 8 * nv ? t.re : w0 + 8 * nv;
+            const __amdgpu_buffer_rsrc_t rs = mf_rsrc(x + base, (uint32_t)(end > base ? (end - base) * (int64_t)sizeof(InT) : 0));
+            uint32_t raw[kMlNIT][4];
+#pragma unroll
+            for (int it = 0; it < kMlNIT; ++it) {
+                const int v = min(it * kWave + lane, nv - 1);
+                const int64_t g = w0 + 8 * v;
+                const uint32_t off = g >= base ? (uint32_t)((g - base) * (int64_t)sizeof(InT)) : kMfOff;
+                if constexpr (I16) {
+                    const mf_i32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+                    raw[it][0] = q.x, raw[it][1] = q.y, raw[it][2] = q.z, raw[it][3] = q.w;
+                } else {
+                    typedef int i32x2 __attribute__((ext_vector_type(2)));
+                    const i32x2 q = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+                    raw[it][0] = q.x, raw[it][1] = q.y, raw[it][2] = 0u, raw[it][3] = 0u;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();  // the previous chunk's B reads are done
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int it = 0; it < kMlNIT; ++it) {
+                const int v = it * kWave + lane;
+                if (v < nv) {
+                    const uint32_t* d = raw[it];
+                    if constexpr (I16) {
+                        *reinterpret_cast<u2*>(&ph[mf_pos(8 * v)]) =
+                            u2{__builtin_amdgcn_perm(d[1], d[0], 0x07050301u), __builtin_amdgcn_perm(d[3], d[2], 0x07050301u)};
+                        *reinterpret_cast<u2*>(&pl[mf_pos(8 * v)]) =
+                            u2{__builtin_amdgcn_perm(d[1], d[0], 0x06040200u) ^ 0x80808080u,
+                               __builtin_amdgcn_perm(d[3], d[2], 0x06040200u) ^ 0x80808080u};
+                    } else {
+                        *reinterpret_cast<u2*>(&pl[mf_pos(8 * v)]) = u2{d[0] ^ 0x80808080u, d[1] ^ 0x80808080u};
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            // ---- the chunk's k-steps: A from the fragment table, B from the planes
+            const mf_i32x4* fa = frag + (int64_t)s0 * 2 * kWave + lane;
+            for (int s = 0; s < steps; ++s) {
+                const mf_i32x4 a_lo = fa[(2 * s) * kWave], a_hi = fa[(2 * s + 1) * kWave];
+                const int i = mf_pos(32 * r + 32 * s + 16 * hf);
+                const mf_i32x4 b_l = *reinterpret_cast<const mf_i32x4*>(&pl[i]);
+                acc_ll = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_lo, b_l, acc_ll, 0, 0, 0);
+                acc_mid = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_hi, b_l, acc_mid, 0, 0, 0);
+                if constexpr (I16) {
+                    const mf_i32x4 b_h = *reinterpret_cast<const mf_i32x4*>(&ph[i]);
+                    acc_m2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_lo, b_h, acc_m2, 0, 0, 0);
+                    acc_hh = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_hi, b_h, acc_hh, 0, 0, 0);
+                }
+            }
+        }
+        // ---- combine, wrap, round, stage; outputs through LDS as whole 1 KiB rows (as above)
+        int32_t q[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            uint32_t a;
+            if constexpr (I16)
+                a = ((uint32_t)(acc_mid[i] + acc_m2[i]) << 8) + (uint32_t)acc_ll[i] + ((uint32_t)acc_hh[i] << 16) + bias;
+            else
+                a = ((uint32_t)acc_mid[i] << 8) + (uint32_t)acc_ll[i] + bias;
+            if constexpr (FAST)
+                q[i] = STAGE == FIR_OUT_U8_SAT ? min(max((int32_t)a, 0), sat_hi) : (int32_t)a >> frac;
+            else
+                q[i] = round_acc<ACC32>(a, shl, frac);
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        if constexpr (STAGE == FIR_OUT_I32) {
+            uint32_t* ob = reinterpret_cast<uint32_t*>(lds[wv]);
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4)
+                *reinterpret_cast<u4*>(&ob[36 * r + 8 * g4 + 4 * hf]) =
+                    u4{(uint32_t)q[4 * g4], (uint32_t)q[4 * g4 + 1], (uint32_t)q[4 * g4 + 2], (uint32_t)q[4 * g4 + 3]};
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            const __amdgpu_buffer_rsrc_t rd = mf_rsrc(y + t.ts, (uint32_t)m * 4u);
+#pragma unroll
+            for (int rho = 0; rho < 4; ++rho) {
+                const int o = 256 * rho + 4 * lane;
+                __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const mf_i32x4*>(&ob[36 * (o >> 5) + (o & 31)]), rd,
+                                                       (uint32_t)(256 * rho + 4 * lane) * 4u, 0, kMfAuxNt);
+            }
+        } else {
+            uint8_t* ob = lds[wv];
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                uint32_t w;
+                if constexpr (FAST) {
+                    w = (uint32_t)q[4 * g4] >> frac;
+                    w |= ((uint32_t)q[4 * g4 + 1] >> frac) << 8;
+                    w |= ((uint32_t)q[4 * g4 + 2] >> frac) << 16;
+                    w |= ((uint32_t)q[4 * g4 + 3] >> frac) << 24;
+                } else {
+                    w = (uint32_t)stage_out32<STAGE>(q[4 * g4]) | ((uint32_t)stage_out32<STAGE>(q[4 * g4 + 1]) << 8) |
+                        ((uint32_t)stage_out32<STAGE>(q[4 * g4 + 2]) << 16) |
+                        ((uint32_t)stage_out32<STAGE>(q[4 * g4 + 3]) << 24);
+                }
+                *reinterpret_cast<uint32_t*>(&ob[48 * r + 8 * g4 + 4 * hf]) = w;
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            const int o = 16 * lane;
+            __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const mf_i32x4*>(&ob[48 * (o >> 5) + (o & 31)]),
+                                                   mf_rsrc(y + t.ts, (uint32_t)m), (uint32_t)(16 * lane), 0, kMfAuxNt);
+        }
+        __builtin_amdgcn_wave_barrier();  // the output reads are done before the next tile's staging
+        asm volatile("" ::: "memory");
+    }
+}
+
+template <typename InT, int STAGE>
+static hipError_t launch_mfma_long(const void* x, void* y, int64_t rl, int64_t tpr, int64_t ntiles, const int32_t* hq,
+                                   int L, int P, int KS, uint32_t bias, bool fast, int frac, int acc_bits, hipStream_t s) {
+    using OutT = typename OutTraits<STAGE>::T;
+    // frag[s][p][lane] = bytes j = 0..15 of plane p's diagonal entries e = 31 - r + 32 s + 16 hf + j
+    const int c = L / 2;
+    std::vector<int8_t> tab((size_t)KS * 2 * kWave * 16);
+    for (int st = 0; st < KS; ++st)
+        for (int lane = 0; lane < kWave; ++lane)
+            for (int j = 0; j < 16; ++j) {
+                const int e = 31 - (lane & 31) + 32 * st + 16 * (lane >> 5) + j;
+                const int tap = 31 - e + c + P;
+                const int v = tap >= 0 && tap < L ? hq[tap] : 0;
+                const int lo = ((v + 128) & 255) - 128;
+                tab[(((size_t)st * 2 + 0) * kWave + lane) * 16 + j] = (int8_t)lo;
+                tab[(((size_t)st * 2 + 1) * kWave + lane) * 16 + j] = (int8_t)((v - lo) / 256);
+            }
+    std::string err;
+    const mf_i32x4* fr = (const mf_i32x4*)device_table(tab.data(), tab.size(), &err);
+    if (!fr) return hipErrorOutOfMemory;
+    const int64_t want = (ntiles + kMfWaves - 1) / kMfWaves;
+    const unsigned blocks = (unsigned)(want < kMfMaxBlocks ? want : kMfMaxBlocks);
+    if (fast)
+        hipLaunchKernelGGL((fir1d_mfma_long_kernel<InT, STAGE, true, true>), dim3(blocks), dim3(kBlock), 0, s,
+                           (const InT*)x, (OutT*)y, rl, tpr, ntiles, fr, KS, P, bias, 0, frac);
+    else if (acc_bits == 32)
+        hipLaunchKernelGGL((fir1d_mfma_long_kernel<InT, STAGE, true, false>), dim3(blocks), dim3(kBlock), 0, s,
+                           (const InT*)x, (OutT*)y, rl, tpr, ntiles, fr, KS, P, bias, 0, frac);
+    else
+        hipLaunchKernelGGL((fir1d_mfma_long_kernel<InT, STAGE, false, false>), dim3(blocks), dim3(kBlock), 0, s,
+                           (const InT*)x, (OutT*)y, rl, tpr, ntiles, fr, KS, P, bias, 32 - acc_bits, frac);
+    return hipGetLastError();
+}
+
 template <typename InT, int STAGE, int KS>
 static hipError_t launch_mfma_ks(const void* x, void* y, int64_t rowlen, int64_t tpr, int64_t ntiles, const MfmaTaps& t,
                                  int P, uint32_t bias, bool fast, int frac, int acc_bits, hipStream_t s) {
@@ -318,15 +507,7 @@ static hipError_t launch_mfma_t(const void* x, void* y, int64_t rows, int64_t ro
                                 int L, int frac, int acc_bits, hipStream_t s) {
     const int c = L / 2, hl = L - 1 - c;
     const int P = (hl + 7) & ~7;
-    const int K = 32 + c + P, KS = (K + 31) / 32;  // 2..3
-    MfmaTaps t;
-    for (int e = 0; e < 128; ++e) {
-        const int tap = 31 - e + c + P;
-        const int v = tap >= 0 && tap < L ? hq[tap] : 0;
-        const int lo = ((v + 128) & 255) - 128;  // balanced split: v = 256 hi + lo
-        t.lo[e] = (int8_t)lo;
-        t.hi[e] = (int8_t)((v - lo) / 256);
-    }
+    const int K = 32 + c + P, KS = (K + 31) / 32;  // 2..3 up to kMfMaxTaps taps
     int64_t hsum = 0, habs = 0;
     for (int k = 0; k < L; ++k) hsum += hq[k], habs += hq[k] < 0 ? -(int64_t)hq[k] : hq[k];
     uint32_t bias = (uint32_t)(128 * hsum);  // mod 2^32
@@ -337,6 +518,15 @@ static hipError_t launch_mfma_t(const void* x, void* y, int64_t rows, int64_t ro
     const int64_t rl = rows > 1 ? rowlen : total;
     const int64_t tpr = (rl + kMfTile - 1) / kMfTile;
     const int64_t ntiles = (rows > 1 ? rows : 1) * tpr;
+    if (L > kMfMaxTaps) return launch_mfma_long<InT, STAGE>(x, y, rl, tpr, ntiles, hq, L, P, KS, bias, fast, frac, acc_bits, s);
+    MfmaTaps t;
+    for (int e = 0; e < 128; ++e) {
+        const int tap = 31 - e + c + P;
+        const int v = tap >= 0 && tap < L ? hq[tap] : 0;
+        const int lo = ((v + 128) & 255) - 128;  // balanced split: v = 256 hi + lo
+        t.lo[e] = (int8_t)lo;
+        t.hi[e] = (int8_t)((v - lo) / 256);
+    }
     if (KS == 2) return launch_mfma_ks<InT, STAGE, 2>(x, y, rl, tpr, ntiles, t, P, bias, fast, frac, acc_bits, s);
     return launch_mfma_ks<InT, STAGE, 3>(x, y, rl, tpr, ntiles, t, P, bias, fast, frac, acc_bits, s);
 }
@@ -345,10 +535,12 @@ bool mfma_path_ok(const void* x, const void* y, int in_dtype, int64_t rows, int6
                   const int32_t* hq, int L, int frac, int acc_bits) {
     bool taps_ok = true;  // the high byte of the balanced split must be a signed byte
     for (int k = 0; k < L; ++k) taps_ok &= hq[k] >= -32768 && hq[k] <= 32639;
-    return L >= 2 && L <= kMfMaxTaps && ch == 1 && taps_ok && acc_bits <= 32 && frac <= 31 &&
+    // the tile index is a uint32 (one tile = 1024 outputs of one row)
+    const int64_t ntiles = rows > 1 ? rows * ((rowlen + kMfTile - 1) / kMfTile) : (total + kMfTile - 1) / kMfTile;
+    return L >= 2 && ch == 1 && taps_ok && acc_bits <= 32 && frac <= 31 &&
            (rows == 1 ? total : rowlen) % 8 == 0 &&  // row and tile edges on 8-sample vectors
            (uintptr_t)x % (in_dtype == FIR_IN_U8 ? 8 : 16) == 0 && (uintptr_t)y % 16 == 0 && total >= 8 &&
-           total < ((int64_t)1 << 40);
+           total < ((int64_t)1 << 40) && ntiles < ((int64_t)1 << 32) - kMfMaxBlocks * kMfWaves;
 }
 
 hipError_t launch_fir1d_mfma(const void* x, int in_dtype, int64_t rows, int64_t rowlen, int64_t total,

@@ -9,6 +9,7 @@
 // DPP wave shifts, and the vertical (R-1)-row halo is carried in a register ring of R
 // partial-output rows (input-stationary, no LDS, no re-read inside a strip).
 // fir2d_generic_kernel handles every other shape/width/alignment.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -53,33 +54,31 @@ constexpr int kStrip2dPkGen = FIR2D_PKG_STRIP;
 template <int R, int C>
 constexpr int pd_pk_gen() { return FIR2D_PKG_PD ? FIR2D_PKG_PD : (R * C >= 20 ? 2 : 3); }
 
-// Generic: one output per thread, exact int64 sum, global loads (L1/L2 absorb the reuse).
-struct Taps2G {
-    int32_t h[FIR_MAX_TAPS];
-};
-
+// Generic: one output per thread, exact 64-bit sum (mod 2^64, see round64), global loads (L1/L2
+// absorb the reuse), taps of any count from HBM; rows grid-strided (any height).
 template <int STAGE>
 __global__ __launch_bounds__(kBlock) void fir2d_generic_kernel(const uint8_t* __restrict__ x,
                                                                typename OutTraits<STAGE>::T* __restrict__ y,
-                                                               int64_t H, int64_t W, Taps2G taps, int R, int C,
-                                                               int frac, int acc_bits) {
+                                                               int64_t H, int64_t W, const int32_t* __restrict__ taps,
+                                                               int R, int C, int frac, int acc_bits) {
     const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int64_t i = blockIdx.y;
     if (j >= W) return;
     x += (int64_t)blockIdx.z * H * W;  // frame blockIdx.z of a batch stored back to back
     y += (int64_t)blockIdx.z * H * W;
     const int cr = R / 2, cc = C / 2;
-    int64_t acc = 0;
-    for (int m = 0; m < R; ++m) {
-        const int64_t ii = i - m + cr;
-        if (ii < 0 || ii >= H) continue;
-        for (int n = 0; n < C; ++n) {
-            const int64_t jj = j - n + cc;
-            if (jj < 0 || jj >= W) continue;
-            acc += (int64_t)taps.h[m * C + n] * (int64_t)x[ii * W + jj];
+    for (int64_t i = blockIdx.y; i < H; i += gridDim.y) {
+        uint64_t acc = 0;
+        for (int m = 0; m < R; ++m) {
+            const int64_t ii = i - m + cr;
+            if (ii < 0 || ii >= H) continue;
+            for (int n = 0; n < C; ++n) {
+                const int64_t jj = j - n + cc;
+                if (jj < 0 || jj >= W) continue;
+                acc += (uint64_t)((int64_t)taps[(int64_t)m * C + n] * (int64_t)x[ii * W + jj]);
+            }
         }
+        y[i * W + j] = stage_out<STAGE>(round64((int64_t)acc, frac, acc_bits));
     }
-    y[i * W + j] = stage_out<STAGE>(round64(acc, frac, acc_bits));
 }
 
 // Exact integer rank-1 factorisation h[m][n] == col[m] * row[n] (row taps int16), if any.
@@ -235,10 +234,13 @@ static hipError_t launch2d_reg_shape(int R, int C, const uint8_t* x, void* y, in
     return hipErrorInvalidValue;
 }
 
+static bool reg2d_shape(int R, int C) { return (R == 1 || R == 3 || R == 5) && (C == 1 || C == 3 || C == 5); }
+
 // rank-1 kernels have a register form with R + C/2 MACs per pixel; measured against the MFMA path
 // in profiles/r02 (the default dispatch keeps the faster one)
 static bool sep2d_register_form(const int32_t* hq, int R, int C) {
-    int32_t col[FIR_MAX_TAPS], row[FIR_MAX_TAPS];
+    if (!reg2d_shape(R, C)) return false;
+    int32_t col[5], row[5];
     return R > 1 && C > 1 && rank1_factor(hq, R, C, col, row);
 }
 
@@ -259,23 +261,29 @@ static bool small_pk16_form(const int32_t* hq, int R, int C, int frac, int acc_b
     return false;
 }
 
-static bool reg2d_shape(int R, int C) { return (R == 1 || R == 3 || R == 5) && (C == 1 || C == 3 || C == 5); }
-
 int launch_fir2d(const uint8_t* x, int64_t frames, int64_t H, int64_t W, const int32_t* hq, int R, int C, int frac,
                  int acc_bits, int stage, void* y, hipStream_t stream, std::string* err) {
     if (stage != FIR_OUT_U8_SAT && stage != FIR_OUT_I32) return *err = "out_stage must be FIR_OUT_U8_SAT or FIR_OUT_I32", FIR_EINVAL;
     if (H < 0 || W < 0 || frames < 0) return *err = "frames, height and width must be >= 0", FIR_EINVAL;
     if (frames > 65535) return *err = "frames must be <= 65535 per call", FIR_EINVAL;
     if (!hq) return *err = "hq must not be NULL", FIR_EINVAL;
-    if (R < 1 || C < 1 || (int64_t)R * C > FIR_MAX_TAPS) return *err = "tap_rows*tap_cols must be in [1, 256]", FIR_EINVAL;
+    if (R < 1 || C < 1 || (int64_t)R * C > FIR_MAX_TAPS)
+        return *err = "tap_rows*tap_cols must be in [1, " + std::to_string(FIR_MAX_TAPS) + "]", FIR_EINVAL;
     if (frac < 1 || acc_bits < 1) return *err = "frac_bits and acc_bits must be >= 1", FIR_EINVAL;
+    const int64_t ntaps = (int64_t)R * C;
+    if (acc_bits >= 64) {  // no wrap: the 64-bit sum must be the exact one
+        int64_t habs = 0;
+        for (int64_t k = 0; k < ntaps; ++k) habs += hq[k] < 0 ? -(int64_t)hq[k] : hq[k];
+        if (habs > (INT64_MAX - 1) / 255)
+            return *err = "acc_bits >= 64 with sum|hq| * 255 >= 2^63: the sum exceeds 64 bits", FIR_EINVAL;
+    }
     if (H == 0 || W == 0 || frames == 0) return FIR_OK;
     if (!x || !y) return *err = "x and y must not be NULL", FIR_EINVAL;
-    if (H > 65535 * (int64_t)kStrip2dSep) return *err = "height too large", FIR_EINVAL;
     bool taps16 = true;  // the register kernel multiplies on v_dot2_i32_i16
-    for (int k = 0; k < R * C; ++k) taps16 &= (hq[k] >= -32768 && hq[k] <= 32767);
+    for (int64_t k = 0; k < ntaps && taps16; ++k) taps16 &= (hq[k] >= -32768 && hq[k] <= 32767);
+    // the register kernel's grid holds a strip of rows per blockIdx.y
     const bool fast = reg2d_shape(R, C) && W % kVec2d == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)y % 16 == 0 &&
-                      acc_bits <= 32 && frac <= 31 && taps16 && W >= kVec2d;
+                      acc_bits <= 32 && frac <= 31 && taps16 && W >= kVec2d && H <= 65535 * (int64_t)kStrip2dSep;
     hipError_t e = hipErrorNotSupported;
     // matrix-core path (fir2d_mfma.hip) unless FIR2D_PATH=reg; rank-1 kernels and <= 3x3 kernels
     // with a packed-16 register form keep the register kernels by default (faster there:
@@ -291,16 +299,16 @@ int launch_fir2d(const uint8_t* x, int64_t frames, int64_t H, int64_t W, const i
         e = stage == FIR_OUT_U8_SAT ? launch2d_reg_shape<FIR_OUT_U8_SAT>(R, C, x, y, frames, H, W, hq, frac, acc_bits, stream)
                                     : launch2d_reg_shape<FIR_OUT_I32>(R, C, x, y, frames, H, W, hq, frac, acc_bits, stream);
     } else {
-        if (H > 65535) return *err = "height > 65535 needs the fast path (W % 16 == 0)", FIR_EINVAL;
-        Taps2G t;
-        for (int k = 0; k < FIR_MAX_TAPS; ++k) t.h[k] = k < R * C ? hq[k] : 0;
-        dim3 grid((unsigned)((W + kBlock - 1) / kBlock), (unsigned)H, (unsigned)frames);
+        if ((W + kBlock - 1) / kBlock >= ((int64_t)1 << 31)) return *err = "width too large", FIR_EINVAL;
+        const int32_t* td = (const int32_t*)device_table(hq, sizeof(int32_t) * (size_t)ntaps, err);
+        if (!td) return FIR_ENOMEM;
+        dim3 grid((unsigned)((W + kBlock - 1) / kBlock), (unsigned)std::min<int64_t>(H, 65535), (unsigned)frames);
         if (stage == FIR_OUT_U8_SAT)
             hipLaunchKernelGGL((fir2d_generic_kernel<FIR_OUT_U8_SAT>), grid, dim3(kBlock), 0, stream, x, (uint8_t*)y, H,
-                               W, t, R, C, frac, acc_bits);
+                               W, td, R, C, frac, acc_bits);
         else
             hipLaunchKernelGGL((fir2d_generic_kernel<FIR_OUT_I32>), grid, dim3(kBlock), 0, stream, x, (int32_t*)y, H,
-                               W, t, R, C, frac, acc_bits);
+                               W, td, R, C, frac, acc_bits);
         e = hipGetLastError();
     }
     if (e != hipSuccess) return *err = std::string("fir2d launch failed: ") + hipGetErrorString(e), FIR_EHIP;

@@ -27,6 +27,7 @@
 // 32n + 8g + 4h + 0..3; two v_permlane32_swap give every lane 16 contiguous output bytes, so each
 // output row leaves as one 1 KiB store instruction (non-temporal).
 #include <cstdlib>
+#include <atomic>
 #include <string>
 
 #include "fir_common.h"
@@ -319,24 +320,31 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
 // resident waves (occupancy x CUs x 4), which removes the partial last round of fixed strips;
 // FIR2D_MFMA_ROWS=n forces n (rounded up to the unrolled turn; A/B).
 template <int R, int NP, bool FAST, bool ACC32>
-static int m2_rows_per_strip(int64_t frames, int64_t ncol, int64_t H) {
+static int m2_rows_per_strip(int64_t frames, int64_t ncol, int64_t H, hipStream_t s) {
     constexpr int UN = (M2Geom<R>::RING & 1) ? 2 * M2Geom<R>::RING : M2Geom<R>::RING;
     int64_t rows;
     const char* env = getenv("FIR2D_MFMA_ROWS");
     if (env && atoi(env) > 0) {
         rows = atoi(env);
     } else {
-        static int resident = 0;  // waves of this instantiation resident on the device at once
+        // waves of this instantiation resident at once on the stream's device, cached per device
+        // (a benign race: concurrent first calls compute the same value)
+        constexpr int kMaxDev = 64;
+        static std::atomic<int> resident_by_dev[kMaxDev];
+        int dev = 0;
+        if (hipStreamGetDevice(s, &dev) != hipSuccess && hipGetDevice(&dev) != hipSuccess) dev = 0;
+        (void)hipGetLastError();
+        int resident = dev >= 0 && dev < kMaxDev ? resident_by_dev[dev].load(std::memory_order_relaxed) : 0;
         if (!resident) {
-            int dev = 0, cus = 0, nb = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            int cus = 0, nb = 0;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
                 hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fir2d_mfma_kernel<R, NP, FAST, ACC32>, kBlock, 0) !=
                     hipSuccess || cus <= 0 || nb <= 0) {
                 (void)hipGetLastError();
                 cus = 256, nb = 3;
             }
             resident = cus * nb * (kBlock / kWave);
+            if (dev >= 0 && dev < kMaxDev) resident_by_dev[dev].store(resident, std::memory_order_relaxed);
         }
         const int64_t per = frames * ncol, strips = resident / per > 1 ? resident / per : 1;
         rows = (H + strips - 1) / strips;
@@ -350,7 +358,7 @@ template <int R, int NP, bool FAST, bool ACC32>
 static hipError_t launch_m2v(const uint8_t* x, uint8_t* y, int64_t frames, int64_t H, int64_t W, const Mfma2Taps& t,
                              uint32_t bias, int sh, int acc_bits, int frac, hipStream_t s) {
     const int64_t ncol = (W + kM2Tile - 1) / kM2Tile;
-    const int rows = m2_rows_per_strip<R, NP, FAST, ACC32>(frames, ncol, H);
+    const int rows = m2_rows_per_strip<R, NP, FAST, ACC32>(frames, ncol, H, s);
     const int64_t nstrip = (H + rows - 1) / rows, nw = frames * ncol * nstrip;
     if (nw >= ((int64_t)1 << 31)) return hipErrorNotSupported;
     const unsigned blocks = (unsigned)((nw + (kBlock / kWave) - 1) / (kBlock / kWave));

@@ -8,6 +8,12 @@
 
 namespace fir {
 
+// Device copy of a host table (long tap sets, matrix-core tap fragments) on the current device,
+// cached by content: uploaded once (complete before this returns), kept for the process life
+// (dev_tables.hip).  nullptr + *err on failure.  The first use of a table cannot be captured
+// in a hipGraph (warm up before capturing).
+const void* device_table(const void* host, size_t bytes, std::string* err);
+
 // Enqueue the row-wise 1-D fixed FIR on `stream`; device pointers.  Returns fir_status.
 int launch_fir1d_rows(const void* x, int in_dtype, int64_t rows, int64_t width, int ch, const int32_t* hq, int L,
                       int frac, int acc_bits, int stage, void* y, hipStream_t stream, std::string* err);

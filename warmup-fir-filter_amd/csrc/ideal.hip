@@ -9,7 +9,8 @@
 // them: the running sum is never -0.0 because samples are >= 0).
 //
 // fir1d_ideal_reg_kernel (ideal_reg.h; L <= 9, aligned buffers): register/DPP layout.
-// fir1d_ideal_kernel (any L, any alignment): LDS tile of 1024 outputs plus the halo.
+// fir1d_ideal_kernel (any L, any alignment): 1024 outputs per workgroup, the taps walked in
+// LDS chunks of 1024 (taps in HBM) with each output's running sum kept across chunks.
 #include <string>
 
 #include "fir_common.h"
@@ -19,39 +20,55 @@
 namespace fir {
 
 constexpr int kIdealTile = 1024;
+constexpr int kIdealChunk = 1024;  // taps (and window halo) per LDS chunk
+constexpr int kIdealPer = kIdealTile / kBlock;
 
-struct TapsF64 {
-    double h[FIR_MAX_TAPS];
-};
-
+// Any L: the taps (device memory) are walked in chunks of kIdealChunk; each chunk stages its
+// taps and the kIdealTile + kc - 1 samples they touch in LDS, and each thread carries its
+// outputs' running sums across the chunks, so every sum is still formed in k order.
 __global__ __launch_bounds__(kBlock) void fir1d_ideal_kernel(const uint8_t* __restrict__ x, double* __restrict__ y,
                                                              int64_t total, int64_t rowlen, int multi_row,
-                                                             TapsF64 taps, int L) {
-    __shared__ double s_h[FIR_MAX_TAPS];
-    __shared__ int32_t s_x[kIdealTile + FIR_MAX_TAPS];
+                                                             const double* __restrict__ taps, int L) {
+    __shared__ double s_h[kIdealChunk];
+    __shared__ int32_t s_x[kIdealTile + kIdealChunk];
     const int c = L / 2;
-    const int HLE = L - 1 - c, HRE = c;
     const int64_t t0 = (int64_t)blockIdx.x * kIdealTile;
-    const int span = kIdealTile + HLE + HRE;
-    for (int k = threadIdx.x; k < L; k += kBlock) s_h[k] = taps.h[k];
-    for (int i = threadIdx.x; i < span; i += kBlock) {
-        const int64_t gi = t0 - HLE + i;
-        s_x[i] = (gi >= 0 && gi < total) ? (int32_t)x[gi] : 0;
+    const int64_t rl = multi_row ? rowlen : total;
+    double acc[kIdealPer];
+    int64_t col[kIdealPer];
+#pragma unroll
+    for (int j = 0; j < kIdealPer; ++j) {
+        acc[j] = 0.0;
+        const int64_t gi = t0 + threadIdx.x + j * kBlock;
+        col[j] = multi_row ? gi % rowlen : gi;
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < kIdealTile; i += kBlock) {
-        const int64_t gi = t0 + i;
-        if (gi >= total) break;
-        const int64_t col = multi_row ? gi % rowlen : gi;
-        const int64_t rl = multi_row ? rowlen : total;
-        double acc = 0.0;
-        for (int k = 0; k < L; ++k) {
-            const int d = c - k;
-            const bool ok = col + d >= 0 && col + d < rl;
-            const double xv = ok ? (double)s_x[HLE + i + d] : 0.0;
-            acc = __dadd_rn(acc, __dmul_rn(s_h[k], xv));
+    for (int k0 = 0; k0 < L; k0 += kIdealChunk) {
+        const int kc = min(kIdealChunk, L - k0);
+        const int64_t w0 = t0 + (c - k0 - kc + 1);  // output i's tap k at window index i + kc - 1 - (k - k0)
+        __syncthreads();
+        for (int k = threadIdx.x; k < kc; k += kBlock) s_h[k] = taps[k0 + k];
+        for (int i = threadIdx.x; i < kIdealTile + kc - 1; i += kBlock) {
+            const int64_t gi = w0 + i;
+            s_x[i] = (gi >= 0 && gi < total) ? (int32_t)x[gi] : 0;
         }
-        y[gi] = acc;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kIdealPer; ++j) {
+            const int i = threadIdx.x + j * kBlock;
+            double a = acc[j];
+            for (int k = 0; k < kc; ++k) {
+                const int64_t d = c - k0 - k;
+                const bool ok = col[j] + d >= 0 && col[j] + d < rl;
+                const double xv = ok ? (double)s_x[i + kc - 1 - k] : 0.0;
+                a = __dadd_rn(a, __dmul_rn(s_h[k], xv));
+            }
+            acc[j] = a;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kIdealPer; ++j) {
+        const int64_t gi = t0 + threadIdx.x + j * kBlock;
+        if (gi < total) y[gi] = acc[j];
     }
 }
 
@@ -80,7 +97,7 @@ int launch_fir1d_ideal(const uint8_t* x, int64_t rows, int64_t width, const doub
                        hipStream_t stream, std::string* err) {
     if (rows < 0 || width < 0) return *err = "rows and width must be >= 0", FIR_EINVAL;
     if (!h) return *err = "h must not be NULL", FIR_EINVAL;
-    if (L < 1 || L > FIR_MAX_TAPS) return *err = "taps must be in [1, 256]", FIR_EINVAL;
+    if (L < 1 || L > FIR_MAX_TAPS) return *err = "taps must be in [1, " + std::to_string(FIR_MAX_TAPS) + "]", FIR_EINVAL;
     const int64_t total = rows * width;
     if (total == 0) return FIR_OK;
     if (!x || !y) return *err = "x and y must not be NULL", FIR_EINVAL;
@@ -103,11 +120,12 @@ int launch_fir1d_ideal(const uint8_t* x, int64_t rows, int64_t width, const doub
         if (e != hipSuccess) return *err = std::string("ideal launch failed: ") + hipGetErrorString(e), FIR_EHIP;
         return FIR_OK;
     }
-    TapsF64 t;
-    for (int k = 0; k < FIR_MAX_TAPS; ++k) t.h[k] = k < L ? h[k] : 0.0;
+    const double* td = (const double*)device_table(h, sizeof(double) * (size_t)L, err);
+    if (!td) return FIR_ENOMEM;
     const int64_t blocks = (total + kIdealTile - 1) / kIdealTile;
+    if (blocks >= ((int64_t)1 << 31)) return *err = "too many samples for one launch", FIR_EINVAL;
     hipLaunchKernelGGL(fir1d_ideal_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, x, y, total, width,
-                       rows > 1 ? 1 : 0, t, L);
+                       rows > 1 ? 1 : 0, td, L);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return *err = std::string("ideal launch failed: ") + hipGetErrorString(e), FIR_EHIP;
     return FIR_OK;

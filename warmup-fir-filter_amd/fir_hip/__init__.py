@@ -31,7 +31,7 @@ __all__ = [
 IN_U8, IN_I16 = 0, 1
 OUT_U8_SAT, OUT_I32 = 0, 1
 RESTORE_CLIP, RESTORE_NORMALIZE = 0, 1
-MAX_TAPS = 256
+MAX_TAPS = 1 << 24  # FIR_MAX_TAPS: any practical length (the reference has no limit)
 IPC_HANDLE_BYTES = 64
 ABI_VERSION = 2
 GATE_TIMEOUT = 1  # FIR_GATE_TIMEOUT
@@ -244,9 +244,9 @@ def fir1d_fixed_rows_multi(x: np.ndarray, hq2, frac_bits: int = 12, acc_bits: in
     if h2.ndim != 2 or h2.shape[0] < 1:
         raise FirHipError("hq2 must be a non-empty (filters, taps) array")
     nf, L = h2.shape
-    h = _taps_i32(h2.reshape(-1)) if nf * L <= MAX_TAPS else np.ascontiguousarray(h2, dtype=np.int32).reshape(-1)
     if L > MAX_TAPS:
         raise FirHipError(f"{L} taps exceed the library limit of {MAX_TAPS}")
+    h = np.concatenate([_taps_i32(row) for row in h2])
     if x.ndim == 0:
         x = x.reshape(1)
     rowlen = x.shape[-1]
