@@ -92,6 +92,54 @@ def test_pipeline_end_to_end_on_golden_images(tmp_path, image_outputs):
     assert res2["input_manifest"]["skipped_cases"] == 7
 
 
+def test_pipeline_devices_reproduces_all_112_outputs(tmp_path, image_outputs):
+    """``devices`` (pipeline ``--devices``): every image's rows spread over three device slots
+    (repeated ids of the box's one GPU: each slot is its own H2D / kernel / D2H on a row block).
+    All 56 fixed and 56 ideal outputs keep the reference's SHA-256."""
+    res = run_pipeline(tap="all", overwrite_vectors=False, skip_input=False, skip_ideal=False, skip_fixed=False,
+                       skip_report=True, skip_restore=True, restore_kind="all", ideal_policy="clip",
+                       overwrite_images=False, strict_report=False, strict_restore=False, top_k=5,
+                       image_dir=GOLDEN / "images_u8.npz", vector_dir=tmp_path / "vector",
+                       image_out_dir=tmp_path / "img", devices=[0, 0, 0])
+    assert res["ideal_counts"] == {"ideal_3tap": 28, "ideal_5tap": 28}
+    assert res["fixed_counts"] == {"fixed_3tap": 28, "fixed_5tap": 28}
+    out = tmp_path / "vector" / "output"
+    n = 0
+    for o in image_outputs["outputs"]:
+        t, stem, c = o["tap"], o["case_stem"], o["coeff_name"]
+        assert _sha(np.load(out / f"fixed_{t}" / f"{stem}__{c}_fixed_{t}_y_u8.npy")) == o["fixed_u8_sha256"]
+        assert _sha(np.load(out / f"ideal_{t}" / f"{stem}__{c}_ideal_{t}_y_f64.npy")) == o["ideal_f64_sha256"]
+        n += 2
+    assert n == 112
+
+
+def test_stage_clis_devices_flag(tmp_path, images, capsys):
+    """``--devices`` on the pipeline and the fixed / ideal stage CLIs (a count, or a list of ids)."""
+    import pipeline_fir_1d
+    from fir_1d.sim.vector import gen_fixed_output, gen_ideal_output, gen_input_vectors
+
+    small = {k: v for k, v in images.items() if v.size <= 64 * 64}
+    np.savez(tmp_path / "small.npz", **small)
+    inp, out = tmp_path / "in", tmp_path / "out"
+    assert gen_input_vectors.main(["--image-dir", str(tmp_path / "small.npz"), "--output-dir", str(inp)]) == 0
+    assert gen_ideal_output.main(["--input-dir", str(inp), "--output-dir", str(out), "--devices", "0,0"]) == 0
+    assert gen_fixed_output.main(["--input-dir", str(inp), "--output-dir", str(out), "--devices", "1"]) == 0
+    want = np.load(GOLDEN / "small_image_outputs.npz")
+    n = 0
+    for kind, suffix in (("fixed", "_y_u8.npy"), ("ideal", "_y_f64.npy")):
+        for t in ("3tap", "5tap"):
+            for f in (out / f"{kind}_{t}").glob("*.npy"):  # the stage renumbers cases: match past "case_NNN_"
+                (key,) = [k for k in want.files if k.split("_", 2)[2] + suffix == f.name.split("_", 2)[2]]
+                assert np.load(f).tobytes() == want[key].tobytes(), f.name
+                n += 1
+    assert n == 32
+    assert pipeline_fir_1d.main(["--image-dir", str(tmp_path / "small.npz"), "--vector-dir", str(tmp_path / "v2"),
+                                 "--image-out-dir", str(tmp_path / "img2"), "--skip-restore", "--devices",
+                                 "0,0,0"]) == 0
+    lines = [ln for ln in capsys.readouterr().out.splitlines() if ln.startswith(("[OK]", "[FAIL]"))]
+    assert lines and all(ln.startswith("[OK]") for ln in lines), lines
+
+
 def test_pipeline_restore_small_images(tmp_path, images):
     small = {k: v for k, v in images.items() if v.size <= 64 * 64}
     np.savez(tmp_path / "small.npz", **small)

@@ -112,3 +112,27 @@ def test_wrap_round_equals_unbounded_reference_arithmetic():
                     if v & (1 << (a - 1)):
                         v -= 1 << a
                 assert g == (v + (1 << (f - 1))) >> f, (v, f, a)
+
+
+def test_parse_devices():
+    """``--devices``: a count, a comma list (repeats allowed), a sequence; None = device 0."""
+    from fir_hip import parse_devices
+
+    assert parse_devices(None) == [0]
+    assert parse_devices(3) == [0, 1, 2]
+    assert parse_devices("2") == [0, 1]
+    assert parse_devices("0,0,3") == [0, 0, 3]
+    assert parse_devices([1, 1]) == [1, 1]
+    for bad in (0, "0", [], [-1]):
+        with pytest.raises(ValueError):
+            parse_devices(bad)
+
+
+def test_rows_over_devices_blocks_cover_every_row_once():
+    from fir_hip import _over_devices
+
+    for nrows in (0, 1, 5, 37):
+        for devs in ([0], [0, 0, 0], [0, 1], [2, 0, 2, 1]):
+            seen = []
+            _over_devices(nrows, devs, lambda r0, r1, d: seen.extend(range(r0, r1)))
+            assert sorted(seen) == list(range(nrows)), (nrows, devs)

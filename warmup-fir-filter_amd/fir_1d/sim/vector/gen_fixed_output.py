@@ -6,7 +6,9 @@ under ``output_dir/fixed_{3,5}tap``), skip-if-exists / ``overwrite`` behaviour, 
 value (number of files generated) and CLI flags.  The difference is the row driver:
 the reference calls the golden model once per image row (:34-60); here the whole
 image goes to the GPU in one ``fir1d_fixed_rows`` launch (rows are independent and
-zero padding resets at each row edge inside the kernel).
+zero padding resets at each row edge inside the kernel).  ``devices`` / ``--devices N``
+(Config row) spreads an image's rows over several GPUs (rows are independent:
+no exchange).
 """
 from __future__ import annotations
 
@@ -43,14 +45,20 @@ def _case_stem_from_input(path: Path) -> str:
 
 
 def _run_fixed_rowwise(x_u8: np.ndarray, h: list[float], *, frac_bits: int, acc_bits: int,
-                       coeff_bits: int) -> np.ndarray:
-    """Every row of an H x W uint8 image through the fixed model: one GPU launch."""
+                       coeff_bits: int, devices=None) -> np.ndarray:
+    """Every row of an H x W uint8 image through the fixed model: one GPU launch (one per
+    device when ``devices`` lists several)."""
     height, width = x_u8.shape
     if height == 0:
         return np.zeros((0, width), dtype=np.uint8)
     hq = quantize_fixed_taps(h, frac_bits, acc_bits, coeff_bits)
     f, a = device_bits(frac_bits, acc_bits)
-    y = fir_hip.fir1d_fixed_rows(np.ascontiguousarray(x_u8, dtype=np.uint8), hq, f, a, fir_hip.OUT_U8_SAT)
+    xc = np.ascontiguousarray(x_u8, dtype=np.uint8)
+    devs = fir_hip.parse_devices(devices)
+    if len(devs) > 1:
+        y = fir_hip.fir1d_fixed_rows_sharded(xc, hq, f, a, fir_hip.OUT_U8_SAT, devices=devs)
+    else:
+        y = fir_hip.fir1d_fixed_rows(xc, hq, f, a, fir_hip.OUT_U8_SAT, device=devs[0])
     if y.shape != (height, width):
         raise ValueError(f"Output shape mismatch: expected {(height, width)}, got {y.shape}.")
     return y
@@ -58,7 +66,7 @@ def _run_fixed_rowwise(x_u8: np.ndarray, h: list[float], *, frac_bits: int, acc_
 
 def _generate_fixed_outputs_for_tap_map(*, input_dir: Path, out_dir: Path, coeff_map: dict[str, list[float]],
                                         tap_label: str, frac_bits: int, acc_bits: int, coeff_bits: int,
-                                        overwrite: bool = False) -> int:
+                                        overwrite: bool = False, devices=None) -> int:
     inputs = _iter_input_npy_files(input_dir)
     if not inputs:
         raise FileNotFoundError(f"No input .npy files found in {input_dir}")
@@ -72,11 +80,13 @@ def _generate_fixed_outputs_for_tap_map(*, input_dir: Path, out_dir: Path, coeff
             out_path = out_dir / f"{stem}__{coeff_name}_fixed_{tap_label}_y_u8.npy"
             if not out_path.exists() or overwrite:
                 pending.append((out_path, h))
-        generated += _run_bank(x_u8, pending, frac_bits=frac_bits, acc_bits=acc_bits, coeff_bits=coeff_bits)
+        generated += _run_bank(x_u8, pending, frac_bits=frac_bits, acc_bits=acc_bits, coeff_bits=coeff_bits,
+                               devices=devices)
     return generated
 
 
-def _run_bank(x_u8: np.ndarray, pending: list, *, frac_bits: int, acc_bits: int, coeff_bits: int) -> int:
+def _run_bank(x_u8: np.ndarray, pending: list, *, frac_bits: int, acc_bits: int, coeff_bits: int,
+              devices=None) -> int:
     """All pending filters of a bank over one image: one fused launch per group of equal tap
     counts (the image is read once per 4 filters).  Taps are validated in bank order, and if
     one fails the filters before it are still written before the error propagates, as the
@@ -101,8 +111,10 @@ def _run_bank(x_u8: np.ndarray, pending: list, *, frac_bits: int, acc_bits: int,
             ys = np.zeros((len(group), height, width), dtype=np.uint8)
         else:
             f, a = device_bits(frac_bits, acc_bits)
+            devs = fir_hip.parse_devices(devices)
             ys = fir_hip.fir1d_fixed_rows_multi(np.ascontiguousarray(x_u8, dtype=np.uint8),
-                                                np.stack([t for _, t in group]), f, a, fir_hip.OUT_U8_SAT)
+                                                np.stack([t for _, t in group]), f, a, fir_hip.OUT_U8_SAT,
+                                                device=devs[0], devices=devs if len(devs) > 1 else None)
         for (out_path, _), y in zip(group, ys):
             np.save(out_path, y)
             written += 1
@@ -114,20 +126,20 @@ def _run_bank(x_u8: np.ndarray, pending: list, *, frac_bits: int, acc_bits: int,
 
 def generate_fixed_3tap_output_vector(input_dir: Path = DEFAULT_INPUT_DIR, output_dir: Path = DEFAULT_OUTPUT_DIR,
                                       *, frac_bits: int = 12, acc_bits: int = 32, coeff_bits: int = 16,
-                                      overwrite: bool = False) -> int:
+                                      overwrite: bool = False, devices=None) -> int:
     return _generate_fixed_outputs_for_tap_map(
         input_dir=Path(input_dir).resolve(), out_dir=Path(output_dir).resolve() / "fixed_3tap",
         coeff_map=h_coeff_3tap_map, tap_label="3tap", frac_bits=frac_bits, acc_bits=acc_bits,
-        coeff_bits=coeff_bits, overwrite=overwrite)
+        coeff_bits=coeff_bits, overwrite=overwrite, devices=devices)
 
 
 def generate_fixed_5tap_output_vector(input_dir: Path = DEFAULT_INPUT_DIR, output_dir: Path = DEFAULT_OUTPUT_DIR,
                                       *, frac_bits: int = 12, acc_bits: int = 32, coeff_bits: int = 16,
-                                      overwrite: bool = False) -> int:
+                                      overwrite: bool = False, devices=None) -> int:
     return _generate_fixed_outputs_for_tap_map(
         input_dir=Path(input_dir).resolve(), out_dir=Path(output_dir).resolve() / "fixed_5tap",
         coeff_map=h_coeff_5tap_map, tap_label="5tap", frac_bits=frac_bits, acc_bits=acc_bits,
-        coeff_bits=coeff_bits, overwrite=overwrite)
+        coeff_bits=coeff_bits, overwrite=overwrite, devices=devices)
 
 
 def _build_argparser() -> argparse.ArgumentParser:
@@ -139,6 +151,8 @@ def _build_argparser() -> argparse.ArgumentParser:
     ap.add_argument("--acc-bits", type=int, default=32)
     ap.add_argument("--coeff-bits", type=int, default=16)
     ap.add_argument("--overwrite", action="store_true")
+    ap.add_argument("--devices", default=None,
+                    help="GPUs for the rows of each image: N (devices 0..N-1) or a comma list of ids")
     return ap
 
 
@@ -149,7 +163,7 @@ def main(argv=None) -> int:
     counts, expected = {"fixed_3tap": 0, "fixed_5tap": 0}, 0
     try:
         kw = dict(input_dir=in_dir, output_dir=out_dir, frac_bits=args.frac_bits, acc_bits=args.acc_bits,
-                  coeff_bits=args.coeff_bits, overwrite=args.overwrite)
+                  coeff_bits=args.coeff_bits, overwrite=args.overwrite, devices=args.devices)
         if args.tap in ("all", "3"):
             expected += len(_iter_input_npy_files(in_dir)) * len(h_coeff_3tap_map)
             counts["fixed_3tap"] = generate_fixed_3tap_output_vector(**kw)

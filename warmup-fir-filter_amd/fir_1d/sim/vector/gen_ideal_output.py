@@ -3,7 +3,8 @@
 Mirror of the reference stage ``fir_1d/sim/vector/gen_ideal_output.py`` (entry points,
 naming ``{case}__{coeff}_ideal_{3,5}tap_y_f64.npy`` under ``output_dir/ideal_{3,5}tap``,
 skip-if-exists, return count, CLI flags).  The per-row loop of the reference
-(:37-50) becomes one ``fir1d_ideal_rows`` launch per image, bit-exact in float64.
+(:37-50) becomes one ``fir1d_ideal_rows`` launch per image, bit-exact in float64
+(``devices`` / ``--devices N``: the image's rows spread over several GPUs, no exchange).
 """
 from __future__ import annotations
 
@@ -23,18 +24,20 @@ DEFAULT_INPUT_DIR = THIS_FILE.parent / "input"
 DEFAULT_OUTPUT_DIR = THIS_FILE.parent / "output"
 
 
-def _run_ideal_rowwise(x_u8: np.ndarray, h: list[float]) -> np.ndarray:
+def _run_ideal_rowwise(x_u8: np.ndarray, h: list[float], devices=None) -> np.ndarray:
     height, width = x_u8.shape
     if height == 0:
         return np.zeros((0, width), dtype=np.float64)
     _validate_h_coefficients(h)
     if width == 0:
         return np.zeros((height, 0), dtype=np.float64)
-    return fir_hip.fir1d_ideal_rows(np.ascontiguousarray(x_u8, dtype=np.uint8), [float(v) for v in h])
+    devs = fir_hip.parse_devices(devices)
+    return fir_hip.fir1d_ideal_rows(np.ascontiguousarray(x_u8, dtype=np.uint8), [float(v) for v in h],
+                                    device=devs[0], devices=devs if len(devs) > 1 else None)
 
 
 def _generate_ideal_outputs_for_tap_map(*, input_dir: Path, out_dir: Path, coeff_map: dict[str, list[float]],
-                                        tap_label: str, overwrite: bool = False) -> int:
+                                        tap_label: str, overwrite: bool = False, devices=None) -> int:
     inputs = _iter_input_npy_files(input_dir)
     if not inputs:
         raise FileNotFoundError(f"No input .npy files found in {input_dir}")
@@ -47,23 +50,23 @@ def _generate_ideal_outputs_for_tap_map(*, input_dir: Path, out_dir: Path, coeff
             out_path = out_dir / f"{stem}__{coeff_name}_ideal_{tap_label}_y_f64.npy"
             if out_path.exists() and not overwrite:
                 continue
-            np.save(out_path, _run_ideal_rowwise(x_u8, h))
+            np.save(out_path, _run_ideal_rowwise(x_u8, h, devices))
             generated += 1
     return generated
 
 
 def generate_ideal_3tap_output_vector(input_dir: Path = DEFAULT_INPUT_DIR, output_dir: Path = DEFAULT_OUTPUT_DIR,
-                                      *, overwrite: bool = False) -> int:
+                                      *, overwrite: bool = False, devices=None) -> int:
     return _generate_ideal_outputs_for_tap_map(
         input_dir=Path(input_dir).resolve(), out_dir=Path(output_dir).resolve() / "ideal_3tap",
-        coeff_map=h_coeff_3tap_map, tap_label="3tap", overwrite=overwrite)
+        coeff_map=h_coeff_3tap_map, tap_label="3tap", overwrite=overwrite, devices=devices)
 
 
 def generate_ideal_5tap_output_vector(input_dir: Path = DEFAULT_INPUT_DIR, output_dir: Path = DEFAULT_OUTPUT_DIR,
-                                      *, overwrite: bool = False) -> int:
+                                      *, overwrite: bool = False, devices=None) -> int:
     return _generate_ideal_outputs_for_tap_map(
         input_dir=Path(input_dir).resolve(), out_dir=Path(output_dir).resolve() / "ideal_5tap",
-        coeff_map=h_coeff_5tap_map, tap_label="5tap", overwrite=overwrite)
+        coeff_map=h_coeff_5tap_map, tap_label="5tap", overwrite=overwrite, devices=devices)
 
 
 def main(argv=None) -> int:
@@ -72,6 +75,8 @@ def main(argv=None) -> int:
     ap.add_argument("--output-dir", type=Path, default=DEFAULT_OUTPUT_DIR)
     ap.add_argument("--tap", choices=("all", "3", "5"), default="all")
     ap.add_argument("--overwrite", action="store_true")
+    ap.add_argument("--devices", default=None,
+                    help="GPUs for the rows of each image: N (devices 0..N-1) or a comma list of ids")
     args = ap.parse_args(argv)
     t0 = perf_counter()
     in_dir, out_dir = args.input_dir.resolve(), args.output_dir.resolve()
@@ -79,10 +84,12 @@ def main(argv=None) -> int:
     try:
         if args.tap in ("all", "3"):
             expected += len(_iter_input_npy_files(in_dir)) * len(h_coeff_3tap_map)
-            counts["ideal_3tap"] = generate_ideal_3tap_output_vector(in_dir, out_dir, overwrite=args.overwrite)
+            counts["ideal_3tap"] = generate_ideal_3tap_output_vector(in_dir, out_dir, overwrite=args.overwrite,
+                                                                         devices=args.devices)
         if args.tap in ("all", "5"):
             expected += len(_iter_input_npy_files(in_dir)) * len(h_coeff_5tap_map)
-            counts["ideal_5tap"] = generate_ideal_5tap_output_vector(in_dir, out_dir, overwrite=args.overwrite)
+            counts["ideal_5tap"] = generate_ideal_5tap_output_vector(in_dir, out_dir, overwrite=args.overwrite,
+                                                                         devices=args.devices)
     except Exception as exc:
         print(f"[FAIL] gen_ideal_output file=gen_ideal_output.py generated=0 skipped=0 failed=1 "
               f"elapsed={perf_counter() - t0:.2f}s out={out_dir} error=\"{exc}\"")

@@ -25,7 +25,7 @@ __all__ = [
     "fir1d_fixed_rows_sharded", "fir2d_fixed", "fir1d_ideal_rows", "compare_metrics", "restore_u8", "IN_U8", "IN_I16",
     "OUT_U8_SAT", "OUT_I32", "RESTORE_CLIP", "RESTORE_NORMALIZE", "MAX_TAPS", "EXPORTS", "ipc_export", "ipc_import",
     "ipc_close", "peek", "IPC_HANDLE_BYTES", "device_bus_id", "peer_access", "peer_atomics", "halo_mailbox_bytes",
-    "GATE_TIMEOUT", "build_id",
+    "GATE_TIMEOUT", "build_id", "parse_devices",
 ]
 
 IN_U8, IN_I16 = 0, 1
@@ -228,11 +228,75 @@ def fir1d_fixed_rows_sharded(x: np.ndarray, hq, frac_bits: int = 12, acc_bits: i
     return y
 
 
+def parse_devices(spec) -> list[int]:
+    """A ``--devices`` value: N (devices 0..N-1), a comma list of ids (repeats allowed: a
+    device then takes several row blocks in turn), or a sequence of ids; None = [0]."""
+    if spec is None:
+        return [0]
+    if isinstance(spec, str):
+        spec = [int(v) for v in spec.split(",")] if "," in spec else int(spec)
+    if isinstance(spec, (int, np.integer)):
+        if spec < 1:
+            raise ValueError("--devices N needs N >= 1")
+        return list(range(int(spec)))
+    devs = [int(v) for v in spec]
+    if not devs or min(devs) < 0:
+        raise ValueError("devices must be a non-empty list of ids >= 0")
+    return devs
+
+
+def _over_devices(nrows: int, devices, run) -> None:
+    """run(r0, r1, device) over contiguous row blocks, one block per entry of ``devices``; each
+    distinct device on its own host thread (the C ABI is reentrant across devices and serialises
+    calls on one device; ctypes releases the GIL).  Rows are independent: no exchange."""
+    devs = list(devices)
+    by_dev: dict[int, list] = {}
+    for i, d in enumerate(devs):
+        r0, r1 = nrows * i // len(devs), nrows * (i + 1) // len(devs)
+        if r1 > r0:
+            by_dev.setdefault(d, []).append((r0, r1))
+    if len(by_dev) <= 1:
+        for d, blocks in by_dev.items():
+            for r0, r1 in blocks:
+                run(r0, r1, d)
+        return
+    errors = []
+
+    def worker(d, blocks):
+        try:
+            for r0, r1 in blocks:
+                run(r0, r1, d)
+        except BaseException as exc:  # noqa: BLE001 - re-raised in the caller
+            errors.append(exc)
+
+    threads = [threading.Thread(target=worker, args=(d, b)) for d, b in by_dev.items()]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    if errors:
+        raise errors[0]
+
+
 def fir1d_fixed_rows_multi(x: np.ndarray, hq2, frac_bits: int = 12, acc_bits: int = 32,
                            out_stage: int = OUT_U8_SAT, channels: int = 1, device: int = 0,
-                           out: np.ndarray | None = None) -> np.ndarray:
+                           out: np.ndarray | None = None, devices=None) -> np.ndarray:
     """F filters (rows of the F x L array hq2) over the same x in one call; returns an
-    array of shape (F, *x.shape).  u8 input is read once per 4 filters on the GPU."""
+    array of shape (F, *x.shape).  u8 input is read once per 4 filters on the GPU.
+    ``devices`` (a list, see parse_devices) spreads the rows over several devices."""
+    if devices is not None and len(parse_devices(devices)) > 1 and np.ndim(x) >= 2:
+        x = np.ascontiguousarray(x)
+        rowlen = x.shape[-1]
+        x2 = x.reshape(-1, rowlen)
+        nf = np.asarray(hq2).shape[0]
+        y = _out_buf(out, (nf,) + x.shape, np.uint8 if out_stage == OUT_U8_SAT else np.int32, x)
+        y2 = y.reshape(nf, -1, rowlen)
+
+        def run(r0, r1, d):
+            y2[:, r0:r1] = fir1d_fixed_rows_multi(x2[r0:r1], hq2, frac_bits, acc_bits, out_stage, channels, d)
+
+        _over_devices(x2.shape[0], parse_devices(devices), run)
+        return y
     x = np.ascontiguousarray(x)
     if x.dtype == np.uint8:
         in_dtype = IN_U8
@@ -279,8 +343,9 @@ def fir2d_fixed(x: np.ndarray, hq2, frac_bits: int = 12, acc_bits: int = 32, out
     return y
 
 
-def fir1d_ideal_rows(x_u8: np.ndarray, h, device: int = 0) -> np.ndarray:
-    """float64 ideal model over uint8 rows (last axis)."""
+def fir1d_ideal_rows(x_u8: np.ndarray, h, device: int = 0, devices=None) -> np.ndarray:
+    """float64 ideal model over uint8 rows (last axis); ``devices`` spreads the rows over
+    several devices (see parse_devices)."""
     x = np.ascontiguousarray(x_u8, dtype=np.uint8)
     hh = np.ascontiguousarray(np.asarray(h, dtype=np.float64).reshape(-1))
     if hh.size == 0 or hh.size > MAX_TAPS:
@@ -290,8 +355,16 @@ def fir1d_ideal_rows(x_u8: np.ndarray, h, device: int = 0) -> np.ndarray:
     width = x.shape[-1]
     rows = x.size // width if width else 0
     y = np.empty(x.shape, dtype=np.float64)
-    _check(lib().fir1d_ideal_rows(_ptr(x), rows, width, _ptr(hh), hh.size, _ptr(y), int(device)),
-           "fir1d_ideal_rows")
+    x2, y2 = x.reshape(rows, width), y.reshape(rows, width)
+
+    def run(r0, r1, d):
+        _check(lib().fir1d_ideal_rows(_ptr(x2[r0:r1]), r1 - r0, width, _ptr(hh), hh.size, _ptr(y2[r0:r1]), int(d)),
+               "fir1d_ideal_rows")
+
+    if rows == 0:
+        run(0, 0, device)
+    else:
+        _over_devices(rows, [device] if devices is None else parse_devices(devices), run)
     return y
 
 

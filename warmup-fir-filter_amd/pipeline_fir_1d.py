@@ -55,7 +55,8 @@ def _log_stage(message: str) -> None:
 def run_pipeline(*, tap: str, overwrite_vectors: bool, skip_input: bool, skip_ideal: bool, skip_fixed: bool,
                  skip_report: bool, skip_restore: bool, restore_kind: str, ideal_policy: str, overwrite_images: bool,
                  strict_report: bool, strict_restore: bool, top_k: int, image_dir: Path | None = None,
-                 vector_dir: Path = DEFAULT_VECTOR_DIR, image_out_dir: Path = DEFAULT_IMAGE_OUT_DIR) -> dict[str, Any]:
+                 vector_dir: Path = DEFAULT_VECTOR_DIR, image_out_dir: Path = DEFAULT_IMAGE_OUT_DIR,
+                 devices=None) -> dict[str, Any]:
     taps = _selected_taps(tap)
     vector_dir = Path(vector_dir)
     in_dir, out_dir = vector_dir / "input", vector_dir / "output"
@@ -67,11 +68,13 @@ def run_pipeline(*, tap: str, overwrite_vectors: bool, skip_input: bool, skip_id
     if not skip_ideal:
         _log_stage("Generate ideal outputs")
         gen = {"3": generate_ideal_3tap_output_vector, "5": generate_ideal_5tap_output_vector}
-        results["ideal_counts"] = {f"ideal_{t}tap": gen[t](in_dir, out_dir, overwrite=overwrite_vectors) for t in taps}
+        results["ideal_counts"] = {f"ideal_{t}tap": gen[t](in_dir, out_dir, overwrite=overwrite_vectors, devices=devices)
+                                   for t in taps}
     if not skip_fixed:
         _log_stage("Generate fixed outputs")
         gen = {"3": generate_fixed_3tap_output_vector, "5": generate_fixed_5tap_output_vector}
-        results["fixed_counts"] = {f"fixed_{t}tap": gen[t](in_dir, out_dir, overwrite=overwrite_vectors) for t in taps}
+        results["fixed_counts"] = {f"fixed_{t}tap": gen[t](in_dir, out_dir, overwrite=overwrite_vectors, devices=devices)
+                                   for t in taps}
     if not skip_report:
         _log_stage("Generate compare reports")
         gen = {"3": generate_3tap_compare_report, "5": generate_5tap_compare_report}
@@ -100,6 +103,9 @@ def _build_argparser() -> argparse.ArgumentParser:
     ap.add_argument("--image-dir", type=Path, default=None, help="image folder or .npz of decoded uint8 images")
     ap.add_argument("--vector-dir", type=Path, default=DEFAULT_VECTOR_DIR)
     ap.add_argument("--image-out-dir", type=Path, default=DEFAULT_IMAGE_OUT_DIR)
+    ap.add_argument("--devices", default=None,
+                    help="GPUs the ideal / fixed stages spread each image's rows over: N (devices 0..N-1) or a "
+                         "comma list of ids (default: device 0)")
     return ap
 
 
@@ -116,7 +122,7 @@ def main(argv=None) -> int:
                                ideal_policy=args.ideal_policy, overwrite_images=args.overwrite_images,
                                strict_report=args.strict_report, strict_restore=args.strict_restore,
                                top_k=args.top_k, image_dir=args.image_dir, vector_dir=args.vector_dir,
-                               image_out_dir=args.image_out_dir)
+                               image_out_dir=args.image_out_dir, devices=args.devices)
     except Exception as exc:
         print(f"[FAIL] pipeline_fir_1d file=pipeline_fir_1d.py generated=0 skipped={skipped} failed=1 "
               f"elapsed={perf_counter() - t0:.2f}s out={outs} error=\"{exc}\"")
