@@ -48,6 +48,30 @@ constexpr int kMfMaxBlocks = FIR_MFMA_MAXBLOCKS;
 #ifndef FIR_MFMA_MINB                // blocks per CU the register allocation must allow (A/B builds)
 #define FIR_MFMA_MINB 4
 #endif
+#ifndef FIR_MFMA_DEPTH               // windows in flight per wave (1 or 2; A/B builds)
+#define FIR_MFMA_DEPTH 1
+#endif
+#ifndef FIR_MFMA_ACC3                // int16: one middle accumulator for both cross products (A/B)
+#define FIR_MFMA_ACC3 0
+#endif
+#ifndef FIR_MFMA_XCD                 // XCD-major tile order (A/B)
+#define FIR_MFMA_XCD 0
+#endif
+#ifndef FIR_MFMA_LONG_FROM           // filters longer than this take the chunked kernel (A/B: lower)
+#define FIR_MFMA_LONG_FROM 64
+#endif
+#ifndef FIR_MFMA_LONG_BLOCKS         // grid-stride blocks of the chunked kernel
+#define FIR_MFMA_LONG_BLOCKS 2048
+#endif
+#ifndef FIR_MFMA_PIN_A               // keep the tap fragments in registers (A/B)
+#define FIR_MFMA_PIN_A 0
+#endif
+#ifndef FIR_MFMA_EXACT_LOADS         // lanes past a window issue no memory request (A/B)
+#define FIR_MFMA_EXACT_LOADS 0
+#endif
+#ifndef FIR_MFMA_TWIN                // A/B twins: 1 = no MFMAs (memory + staging only), 2 = no window loads
+#define FIR_MFMA_TWIN 0
+#endif
 
 // Tap fragments by diagonal: entry e holds a signed byte of h[d + L/2 + P], d = 31 - e (d = r - k
 // of A[r][k]), 0 outside the filter.  Lane (r, h) of k-step s reads entries
@@ -127,24 +151,45 @@ __global__ __launch_bounds__(kBlock, FIR_MFMA_MINB) void fir1d_mfma_kernel(const
         }
         a_lo[s] = mf_i32x4{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3]};
         a_hi[s] = mf_i32x4{(int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+#if FIR_MFMA_PIN_A
+        // opaque from here on: under register pressure hipcc otherwise re-packs these fragments
+        // from their bytes inside the tile loop (~100 VALU per tile, the int16 kernels' VALU bound)
+        asm volatile("" : "+v"(a_lo[s]), "+v"(a_hi[s]));
+#endif
     }
     // FAST u8 stage: clamp the biased sum, then shift (FAST implies frac <= 22; unused otherwise)
     const int32_t sat_hi = FAST ? (int32_t)((256u << (frac & 31)) - 1u) : 0;
 
-    const uint32_t step = gridDim.x * kMfWaves, nt32 = (uint32_t)ntiles, tpr = (uint32_t)tiles_per_row;
+    uint32_t step = gridDim.x * kMfWaves, nt32 = (uint32_t)ntiles;
+    const uint32_t tpr = (uint32_t)tiles_per_row;
     uint32_t tile = blockIdx.x * kMfWaves + wv;
+#if FIR_MFMA_XCD
+    // XCD-major tiles: blocks b, b + 8, ... share an XCD (round-robin dispatch); give each XCD one
+    // contiguous eighth of the tiles, walked grid-stride by its own waves
+    if (gridDim.x % 8 == 0) {
+        const uint32_t x8 = blockIdx.x % 8, per = (nt32 + 7) / 8, lo = x8 * per;
+        step = gridDim.x / 8 * kMfWaves;
+        tile = lo + (blockIdx.x / 8) * kMfWaves + wv;
+        nt32 = lo + per < nt32 ? lo + per : nt32;
+    }
+#endif
     // the window of a tile: 8-sample vectors v (lanes past the window re-load its last one),
     // through a descriptor over the tile's part of its row; other rows' samples read as zeros
-    uint32_t raw[NIT][4];
-    auto load_window = [&](const MfTile& t) __attribute__((always_inline)) {
+    uint32_t rawA[NIT][4], rawB[NIT][4];  // rawB: the second window in flight (DEPTH 2)
+    auto load_window = [&](const MfTile& t, uint32_t(&raw)[NIT][4]) __attribute__((always_inline)) {
         const int64_t w0 = t.ts - P, base = w0 > t.rs ? w0 : t.rs, end = t.re < w0 + WL ? t.re : w0 + WL;
         const __amdgpu_buffer_rsrc_t rs = mf_rsrc(x + base, (uint32_t)((end - base) * (int64_t)sizeof(InT)));
 #pragma unroll
         for (int it = 0; it < NIT; ++it) {
             const int v = min(it * kWave + lane, NV - 1);
             const int64_t g = w0 + 8 * v;
-            const uint32_t off = g >= base ? (uint32_t)((g - base) * (int64_t)sizeof(InT)) : kMfOff;
-            if constexpr (I16) {
+            uint32_t off = g >= base ? (uint32_t)((g - base) * (int64_t)sizeof(InT)) : kMfOff;
+#if FIR_MFMA_EXACT_LOADS
+            if (NV % kWave != 0 && it * kWave + lane >= NV) off = kMfOff;  // lanes past the window: no request
+#endif
+            if constexpr (FIR_MFMA_TWIN == 2) {  // no window loads: synthetic samples
+                raw[it][0] = off, raw[it][1] = off + 1, raw[it][2] = off + 2, raw[it][3] = off + 3;
+            } else if constexpr (I16) {
                 const mf_i32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
                 raw[it][0] = q.x, raw[it][1] = q.y, raw[it][2] = q.z, raw[it][3] = q.w;
             } else {
@@ -154,7 +199,11 @@ __global__ __launch_bounds__(kBlock, FIR_MFMA_MINB) void fir1d_mfma_kernel(const
             }
         }
     };
-    if (tile < nt32) load_window(mf_tile(tile, rowlen, tpr));  // the first tile's window
+    constexpr int DEPTH = FIR_MFMA_DEPTH;
+    if (tile < nt32) load_window(mf_tile(tile, rowlen, tpr), rawA);  // the first tile's window
+    if constexpr (DEPTH > 1) {  // and the second's (past the end: the first again)
+        if (tile < nt32) load_window(mf_tile(tile + step < nt32 ? tile + step : tile, rowlen, tpr), rawB);
+    }
 
     // A tile's outputs leave LDS into registers at the end of its iteration and are stored one
     // iteration later, right AFTER the next window's conversion: hipcc's wait for a prefetched
@@ -175,7 +224,7 @@ __global__ __launch_bounds__(kBlock, FIR_MFMA_MINB) void fir1d_mfma_kernel(const
 
     // One tile: convert its prefetched window, store the previous tile, prefetch the next window,
     // MFMA, stage the outputs.
-    auto body = [&](uint32_t tile, bool first) __attribute__((always_inline)) {
+    auto body = [&](uint32_t tile, bool first, uint32_t(&raw)[NIT][4]) __attribute__((always_inline)) {
 #if FIR_MFMA_SCHED
         __builtin_amdgcn_sched_barrier(0);  // A/B: keep each tile's instructions in place
 #endif
@@ -203,7 +252,7 @@ __global__ __launch_bounds__(kBlock, FIR_MFMA_MINB) void fir1d_mfma_kernel(const
         // ---- the next tile's window goes out now, its latency hidden behind this tile's math
         // (unconditional: past the last tile it re-loads this one, so every path into the loop
         // header has the same memory operations in flight and the compiler's wait there stays exact)
-        load_window(mf_tile(tile + step < nt32 ? tile + step : tile, rowlen, tpr));
+        load_window(mf_tile(tile + DEPTH * step < nt32 ? tile + DEPTH * step : tile, rowlen, tpr), raw);
         __builtin_amdgcn_wave_barrier();  // one wave's LDS ops complete in order
         asm volatile("" ::: "memory");
 
@@ -216,12 +265,20 @@ __global__ __launch_bounds__(kBlock, FIR_MFMA_MINB) void fir1d_mfma_kernel(const
         for (int s = 0; s < KS; ++s) {
             const int i = mf_pos(32 * r + 32 * s + 16 * hf);
             const mf_i32x4 b_l = *reinterpret_cast<const mf_i32x4*>(&pl[i]);
+#if FIR_MFMA_TWIN == 1
+            acc_ll[s] += b_l.x ^ a_lo[s].y;  // memory-only twin: keep the B reads, drop the MFMAs
+            if constexpr (I16) acc_hh[s] += (*reinterpret_cast<const mf_i32x4*>(&ph[i])).z;
+            continue;
+#endif
             acc_ll = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_lo[s], b_l, acc_ll, 0, 0, 0);
             acc_mid = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_hi[s], b_l, acc_mid, 0, 0, 0);
             if constexpr (I16) {
                 const mf_i32x4 b_h = *reinterpret_cast<const mf_i32x4*>(&ph[i]);
-                acc_m2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_lo[s], b_h, acc_m2, 0, 0, 0);
                 acc_hh = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_hi[s], b_h, acc_hh, 0, 0, 0);
+                if constexpr (FIR_MFMA_ACC3)  // two MFMAs (acc_hh) after the first write of acc_mid
+                    acc_mid = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_lo[s], b_h, acc_mid, 0, 0, 0);
+                else
+                    acc_m2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_lo[s], b_h, acc_m2, 0, 0, 0);
             }
         }
         // u8: acc_mid = sum hh xs, acc_ll = sum hl xs; int16: acc_hh = sum hh xh,
@@ -290,9 +347,20 @@ __global__ __launch_bounds__(kBlock, FIR_MFMA_MINB) void fir1d_mfma_kernel(const
         asm volatile("" ::: "memory");
     };
     if (tile < nt32) {
-        body(tile, true);
+        body(tile, true, rawA);
         tile += step;
-        for (; tile < nt32; tile += step) body(tile, false);
+        if constexpr (DEPTH > 1) {
+            // two windows in flight: tiles alternate between the two register sets
+            while (tile < nt32) {
+                body(tile, false, rawB);
+                tile += step;
+                if (tile >= nt32) break;
+                body(tile, false, rawA);
+                tile += step;
+            }
+        } else {
+            for (; tile < nt32; tile += step) body(tile, false, rawA);
+        }
         flush();  // the last tile's outputs
     }
 }
@@ -471,7 +539,7 @@ static hipError_t launch_mfma_long(const void* x, void* y, int64_t rl, int64_t t
     const mf_i32x4* fr = (const mf_i32x4*)device_table(tab.data(), tab.size(), &err);
     if (!fr) return hipErrorOutOfMemory;
     const int64_t want = (ntiles + kMfWaves - 1) / kMfWaves;
-    const unsigned blocks = (unsigned)(want < kMfMaxBlocks ? want : kMfMaxBlocks);
+    const unsigned blocks = (unsigned)(want < FIR_MFMA_LONG_BLOCKS ? want : FIR_MFMA_LONG_BLOCKS);
     if (fast)
         hipLaunchKernelGGL((fir1d_mfma_long_kernel<InT, STAGE, true, true>), dim3(blocks), dim3(kBlock), 0, s,
                            (const InT*)x, (OutT*)y, rl, tpr, ntiles, fr, KS, P, bias, 0, frac);
@@ -518,7 +586,7 @@ static hipError_t launch_mfma_t(const void* x, void* y, int64_t rows, int64_t ro
     const int64_t rl = rows > 1 ? rowlen : total;
     const int64_t tpr = (rl + kMfTile - 1) / kMfTile;
     const int64_t ntiles = (rows > 1 ? rows : 1) * tpr;
-    if (L > kMfMaxTaps) return launch_mfma_long<InT, STAGE>(x, y, rl, tpr, ntiles, hq, L, P, KS, bias, fast, frac, acc_bits, s);
+    if (L > FIR_MFMA_LONG_FROM) return launch_mfma_long<InT, STAGE>(x, y, rl, tpr, ntiles, hq, L, P, KS, bias, fast, frac, acc_bits, s);
     MfmaTaps t;
     for (int e = 0; e < 128; ++e) {
         const int tap = 31 - e + c + P;
