@@ -185,6 +185,48 @@ def test_fir2d_mfma_frames_and_full_frame(monkeypatch):
     assert np.array_equal(y.cpu().numpy(), co.fir2d(xf, sep))
 
 
+PK16_KERNELS = [  # rank-1 kernels on the separable packed-16 strip kernel (fir2d_pk16.h)
+    np.outer([16, 64, 96, 64, 16], [1, 4, 6, 4, 1]),                 # high-byte output (bench kernel form)
+    np.outer([1, 2, 1], [1, 2, 1]),                                   # unsigned, shift 12, R = 3 (turns of 15)
+    np.outer([-1, 3, -1], [1, -2, 5, -2, 1]),                         # signed sum, 3 x 5
+]
+
+
+@pytest.mark.parametrize("rows", ["", "1", "6", "16", "37"])
+def test_fir2d_pk16_strip_heights_vs_oracle(rows, monkeypatch):
+    """Strips of any height, walking down (even strips) and up (odd strips), over frames whose
+    height is not a whole number of strips (and shorter than one), batched frames included."""
+    if rows:
+        monkeypatch.setenv("FIR2D_PK_ROWS", rows)
+    rng = np.random.default_rng(len(rows) * 31 + 3)
+    co = c_oracle()
+    for k in PK16_KERNELS:
+        for shape in ((1, 64), (2, 48), (5, 4096), (17, 1040), (64, 8192), (101, 256), (3, 41, 512)):
+            x = rng.integers(0, 256, shape, dtype=np.uint8)
+            x[..., 0, :16] = 255
+            got = fir_hip.fir2d_fixed(x, k)
+            xs = x if x.ndim == 3 else x[None]
+            for f in range(xs.shape[0]):
+                want = co.fir2d(xs[f], k, 12, 32, 0)
+                assert np.array_equal(got if x.ndim == 2 else got[f], want), (k.shape, shape, f)
+
+
+def test_fir2d_pk16_frame_past_2p31_pixels():
+    """A 32768 x 65536 frame (2^31 pixels) takes the unrolled 32-row strip kernel; rows at the top,
+    bottom and across strip seams are compared with the oracle run on row bands of the frame."""
+    H, W = 32768, 65536
+    k = PK16_KERNELS[0]
+    xd = torch.randint(0, 256, (H, W), dtype=torch.uint8, device=DEV)
+    yd = torch_ops.fir2d_fixed_dev(xd, k)
+    torch.cuda.synchronize()
+    co = c_oracle()
+    for a, b in ((0, 40), (16000, 16070), (H - 40, H)):
+        lo, hi = max(a - 2, 0), min(b + 2, H)
+        band = xd[lo:hi].cpu().numpy()
+        want = co.fir2d(band, k, 12, 32, 0)[a - lo:a - lo + (b - a)]
+        assert np.array_equal(yd[a:b].cpu().numpy(), want), (a, b)
+
+
 def test_fir2d_frame_batches_device_and_host():
     """(frames, H, W) batches: one launch, every frame = its own single-frame result, on the
     register (8192-wide, separable packed-16 and general) and generic (odd width) paths."""

@@ -33,7 +33,6 @@
 namespace fir {
 
 constexpr int kMfTile = 1024;        // outputs per wave tile (32 B columns x 32 A rows)
-constexpr int kMfMaxTaps = 64;
 constexpr int kMfWaves = kBlock / kWave;
 // grid-stride blocks: 2048 (two resident rounds at 4 blocks per CU) rather than one round, 1-5 %
 // faster for u8 input (u8 -> u8 at 31 taps 95.7 -> 91.5 us, u8 -> int32 196.5 -> 193.3 us;

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <string>
 
+#include "fir2d_pk16.h"
 #include "fir2d_reg.h"
 #include "fir_common.h"
 #include "fir_launch.h"
@@ -38,7 +39,43 @@ constexpr int kPdGen = 2;
 #define FIR2D_PK_STRIP 32
 #endif
 constexpr int kStrip2dPk = FIR2D_PK_STRIP;
-constexpr int kPdPk = 4;
+#ifndef FIR2D_PK_PD  // A/B builds
+#define FIR2D_PK_PD 4
+#endif
+constexpr int kPdPk = FIR2D_PK_PD;
+#ifndef FIR2D_PK_MINW  // A/B builds: waves per SIMD the register allocation must allow
+#define FIR2D_PK_MINW 1
+#endif
+constexpr int kMinwPk = FIR2D_PK_MINW;
+#ifndef FIR2D_PK_ROLLED  // A/B builds: 0 = the fully unrolled 32-row strip kernel
+#define FIR2D_PK_ROLLED 1  // 0: the unrolled 32-row fir2d_reg_kernel strip
+#endif
+
+// The separable packed-16 form on fir2d_pk16_strip_kernel: strips of about kPkRows rows (whole
+// turns of U input rows), FIR2D_PK_ROWS=n forces n (A/B).  Short strips keep the two neighbours
+// that share R - 1 rows in step with each other (see the kernel's walk directions): 16-26 rows
+// measured 79.7-81.3 us per 4 frames, 6 rows 97, 36 rows 86, one resident round (56 rows) 85.5
+// (profiles/r03/ab2d_pk16_rows.txt).
+constexpr int kPkRows = 16;
+template <int R, int C, int MODE>
+static hipError_t launch_pk16_rolled(const uint8_t* x, uint8_t* y, int64_t frames, int64_t H, int64_t W,
+                                     const Taps2<R, C>& t, hipStream_t s) {
+    constexpr int PD = kPdPk, U = p16_lcm(R, PD + 1);
+    auto kern = fir2d_pk16_strip_kernel<R, C, PD, MODE, kMinwPk>;
+    const int64_t gx = (W / 16 + kBlock - 1) / kBlock;
+    const char* env = getenv("FIR2D_PK_ROWS");
+    int64_t rows = env && atoi(env) > 0 ? atoi(env) : kPkRows;
+    // whole turns of U input rows per strip (S + R - 1 a multiple of U), and at most 65535 strips
+    rows = std::max<int64_t>(rows, (H + 65534) / 65535);
+    const int64_t lo = rows;
+    rows = std::max<int64_t>((rows + R - 1 + U / 2) / U, 1) * U - (R - 1);  // nearest whole turns (U >= R)
+    if ((H + rows - 1) / rows > 65535) rows = ((lo + R - 1 + U - 1) / U) * U - (R - 1);
+    if (rows > H) rows = H;  // one strip: the kernel stops at its last row (t < T), not at a turn
+    const int64_t nstrips = (H + rows - 1) / rows;
+    hipLaunchKernelGGL(kern, dim3((unsigned)gx, (unsigned)nstrips, (unsigned)frames), dim3(kBlock), 0, s, x, y, H, W,
+                       t, (int)rows);
+    return hipGetLastError();
+}
 // general packed-16 form: 16-row strips (a 32-row strip's R*C MACs per row exceed the forced
 // unroll budget: the loop stays rolled and its ring spills to scratch)
 #ifndef FIR2D_PKG_VEC  // overridable for the A/B builds (tools/lib_ab2d.py)
@@ -161,19 +198,26 @@ static hipError_t launch2d_reg(const uint8_t* x, void* y, int64_t frames, int64_
         // packed 16-bit pixel pairs when the whole sum provably fits 16 bits (u8 stage only)
         if constexpr (STAGE == FIR_OUT_U8_SAT) {
             const int pk = nowrap ? plan_pk16(t, t.col, rowt, frac) : 0;
+            if (FIR2D_PK_ROLLED && H * W < ((int64_t)1 << 31)) {
+                if (pk == (kMode2dPk16 | kMode2dPkHi8))
+                    return launch_pk16_rolled<R, C, kMode2dPk16 | kMode2dPkHi8>(x, (uint8_t*)y, frames, H, W, t, s);
+                if (pk == kMode2dPk16) return launch_pk16_rolled<R, C, kMode2dPk16>(x, (uint8_t*)y, frames, H, W, t, s);
+                if (pk == (kMode2dPk16 | kMode2dPkSigned))
+                    return launch_pk16_rolled<R, C, kMode2dPk16 | kMode2dPkSigned>(x, (uint8_t*)y, frames, H, W, t, s);
+            }
             const dim3 gpk = fir2d_reg_grid<kVec2d, kStrip2dPk>(H, W, frames);
             if (pk == (kMode2dPk16 | kMode2dPkHi8)) {
-                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dPk, SNW | kMode2dPk16 | kMode2dPkHi8, 1, kPdPk, false, true, true>),
+                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dPk, SNW | kMode2dPk16 | kMode2dPkHi8, kMinwPk, kPdPk, false, true, true>),
                                    gpk, dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
                 return hipGetLastError();
             }
             if (pk == kMode2dPk16) {
-                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dPk, SNW | kMode2dPk16, 1, kPdPk, false, true, true>), gpk,
+                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dPk, SNW | kMode2dPk16, kMinwPk, kPdPk, false, true, true>), gpk,
                                    dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
                 return hipGetLastError();
             }
             if (pk == (kMode2dPk16 | kMode2dPkSigned)) {
-                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dPk, SNW | kMode2dPk16 | kMode2dPkSigned, 1, kPdPk, false, true, true>),
+                hipLaunchKernelGGL((fir2d_reg_kernel<R, C, STAGE, kVec2d, kStrip2dPk, SNW | kMode2dPk16 | kMode2dPkSigned, kMinwPk, kPdPk, false, true, true>),
                                    gpk, dim3(kBlock), 0, s, x, (OutT*)y, H, W, t, 32 - acc_bits, frac);
                 return hipGetLastError();
             }
