@@ -221,6 +221,45 @@ def test_xgmi_peer_halos_across_processes(world, taps, ch):
     assert kind == "xgmi" and ok
 
 
+def _gate_buffers(hl_bytes, hr_bytes):
+    mb = torch.empty(fir_hip.halo_mailbox_bytes(hl_bytes, hr_bytes), dtype=torch.uint8, device=DEV)
+    return torch_ops.halo_mailbox_init_dev(mb)
+
+
+def test_halo_gate_two_streams_and_timeout():
+    """The gate kernel itself (csrc/halo_gate.hip) in one process: two 'ranks' whose gates run
+    concurrently on two streams hand their edges over for several epochs (changing segments);
+    a gate whose neighbour never publishes reports FIR_GATE_TIMEOUT and leaves zero halos."""
+    hl, hr = 2, 2  # int16 samples of a 5-tap filter
+    hlb, hrb = 2 * hl, 2 * hr
+    mb_a, mb_b = _gate_buffers(hlb, hrb), _gate_buffers(hlb, hrb)
+    a = torch.arange(1000, dtype=torch.int16, device=DEV)
+    b = torch.arange(5000, 6000, dtype=torch.int16, device=DEV)
+    la = torch.empty(hl, dtype=torch.int16, device=DEV)  # a's left halo = b's tail (b sits left of a)
+    rb = torch.empty(hr, dtype=torch.int16, device=DEV)  # b's right halo = a's head
+    st_a = torch.full((1,), -1, dtype=torch.int32, device=DEV)
+    st_b = torch.full((1,), -1, dtype=torch.int32, device=DEV)
+    s1, s2 = torch.cuda.Stream(device=DEV), torch.cuda.Stream(device=DEV)
+    torch.cuda.synchronize()
+    for step in range(5):
+        a.add_(step + 1)
+        b.sub_(step + 3)
+        torch.cuda.synchronize()
+        torch_ops.halo_gate_dev(a, hlb, hrb, mb_a, mb_b.data_ptr(), None, la, None, st_a, 5.0, stream=s1)
+        torch_ops.halo_gate_dev(b, hlb, hrb, mb_b, None, mb_a.data_ptr(), None, rb, st_b, 5.0, stream=s2)
+        torch.cuda.synchronize()
+        assert st_a.item() == 0 and st_b.item() == 0, step
+        assert torch.equal(la, b[-hl:]) and torch.equal(rb, a[:hr]), step
+    # a neighbour that never publishes: bounded wait, reported, zero halos
+    lone = _gate_buffers(hlb, hrb)
+    never = _gate_buffers(hlb, hrb)
+    la.fill_(7)
+    torch_ops.halo_gate_dev(a, hlb, hrb, lone, never.data_ptr(), None, la, None, st_a, 0.05)
+    torch.cuda.synchronize()
+    assert st_a.item() == fir_hip.GATE_TIMEOUT
+    assert int(la.abs().sum()) == 0
+
+
 def test_peer_access_check():
     """The guard XgmiHalo runs before any kernel reads a neighbour: this GPU can read itself,
     and a bus id no visible GPU has is refused (that rank then takes the RCCL path)."""

@@ -44,6 +44,9 @@ constexpr int kM2MaxC = 5;      // horizontal halo <= 2 pixels per side
 #ifndef FIR2D_MFMA_COLFAST       // wave order: column tiles fastest (1) or strips fastest (0)
 #define FIR2D_MFMA_COLFAST 1
 #endif
+#ifndef FIR2D_MFMA_ALT           // odd strips walk up (0: every strip walks down; A/B builds)
+#define FIR2D_MFMA_ALT 1
+#endif
 #ifndef FIR2D_MFMA_MINW
 #define FIR2D_MFMA_MINW 3
 #endif
@@ -122,8 +125,19 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
     const int64_t j0 = (int64_t)col * kM2Tile;
     const int64_t i0 = (int64_t)strip * kM2Strip;
     const uint32_t wb = (uint32_t)W;  // W < 2^31 (host-checked)
+    // Walk direction: odd strips walk UP, so two vertically adjacent strips read the R - 1 rows
+    // they share at the same moment (both at their start or both at their end) and the second
+    // read hits L2 (fir2d_pk16.h measured it on the separable kernel).  Walk step q handles output
+    // row orow0 + dir q; walk row s of the ring is input row wrow0 + dir s; the window position mm
+    // (oldest first) multiplies tap row tap_row(mm).
+    const bool up = FIR2D_MFMA_ALT && (strip & 1);
+    const int64_t dir = up ? -1 : 1;
+    const int64_t orow0 = up ? i0 + kM2Strip - 1 : i0;
+    const int64_t wrow0 = up ? i0 + kM2Strip - 1 + D : i0 - U;
+    auto tap_row = [&](int mm) __attribute__((always_inline)) { return up ? mm : R - 1 - mm; };
 
-    // ---- tap fragments: A_m[r = n][k = 16 hf + j] (main) and A_tail[r][32 + 16 hf + j]
+    // ---- tap fragments by window position (am[p][mm] = tap row tap_row(mm)): A_m[r = n][k = 16 hf + j]
+    // (main) and A_tail[r][32 + 16 hf + j]
     m2_i32x4 am[NP][R], at[NP];
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
@@ -131,16 +145,15 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
         for (int m = 0; m < R; ++m) {
             uint32_t v[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-            for (int j = 0; j < 16; ++j) v[j / 4] |= (uint32_t)(uint8_t)taps.tm[p][m][33 - (n - 16 * hf - j)] << (8 * (j % 4));
+            for (int j = 0; j < 16; ++j) v[j / 4] |= (uint32_t)(uint8_t)taps.tm[p][tap_row(m)][33 - (n - 16 * hf - j)] << (8 * (j % 4));
             am[p][m] = m2_i32x4{(int)v[0], (int)v[1], (int)v[2], (int)v[3]};
         }
         uint32_t v[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-            const int mm = 4 * hf + j / 4, t = j % 4;  // tail row slot m'' (input row i - U + m''), pixel
+            const int mm = 4 * hf + j / 4, t = j % 4;  // tail window position m'', pixel
             const int kc = t == 0 ? -2 : (t == 1 ? -1 : 30 + t);
-            const int m = R - 1 - mm;
-            const uint32_t tb = m >= 0 ? (uint32_t)(uint8_t)taps.tm[p][m < 0 ? 0 : m][33 - (n - kc)] : 0u;
+            const uint32_t tb = mm < R ? (uint32_t)(uint8_t)taps.tm[p][tap_row(mm < R ? mm : 0)][33 - (n - kc)] : 0u;
             v[j / 4] |= tb << (8 * (j % 4));
         }
         at[p] = m2_i32x4{(int)v[0], (int)v[1], (int)v[2], (int)v[3]};
@@ -180,9 +193,9 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
         tl[slot] = __builtin_amdgcn_perm(r, l, 0x05040302u);  // l.b2, l.b3, r.b0, r.b1
     };
 
-    // rows i0 - U .. i0 + D + PD - 1 into slots 0 .. RING - 2; slot(rho) = (rho - i0 + U) % RING
+    // walk rows 0 .. RING - 2 into slots 0 .. RING - 2; slot(walk row s) = s % RING
 #pragma unroll
-    for (int s = 0; s < kM2Ring - 1; ++s) load_row(i0 - U + s, s);
+    for (int s = 0; s < kM2Ring - 1; ++s) load_row(wrow0 + dir * s, s);
 #pragma unroll
     for (int s = 0; s < R - 1; ++s) prep_row(s);
 
@@ -257,22 +270,22 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
     // ring slot and the accumulator parity of every row are compile-time
     constexpr int UN = (kM2Ring & 1) ? 2 * kM2Ring : kM2Ring;
     static_assert(UN % 2 == 0, "rows per unrolled turn must be even (accumulator parity)");
-    for (int64_t iq = i0; iq < i0 + kM2Strip; iq += UN) {
+    for (int64_t iq = 0; iq < kM2Strip; iq += UN) {
 #pragma unroll
         for (int kk = 0; kk < UN; ++kk) {
             const int k = kk % kM2Ring;  // ring position
-            const int64_t i = iq + kk;
+            const int64_t q = iq + kk;   // walk step: output row orow0 + dir q
             // keep each iteration's instructions in place: hipcc otherwise hoists a row's signed-
             // byte XOR up to its load, several iterations early, and waits for that load there
             __builtin_amdgcn_sched_barrier(0);
-            prep_row((k + U + D) % kM2Ring);                   // row i + D has arrived
-            load_row(i + D + PD, (k + U + D + PD) % kM2Ring);  // slot of row i - U - 1
+            prep_row((k + R - 1) % kM2Ring);                              // walk row q + R - 1 has arrived
+            load_row(wrow0 + dir * (q + R - 1 + PD), (k + R - 1 + PD) % kM2Ring);  // slot of walk row q - 1
 
 #if FIR2D_MFMA_COPYONLY  // memory-only twin (A/B builds): the same loads and stores, no arithmetic
             {
                 const m2_u4 rv = ring[(k + U) % kM2Ring];
                 const uint32_t g[4] = {rv.x, rv.y, rv.z, rv.w};
-                store_row(g, i - 1, kk > 0 || iq > i0);
+                store_row(g, orow0 + dir * (q - 1), q > 0);
                 continue;
             }
 #endif
@@ -284,17 +297,17 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
 #pragma unroll
             for (int mm = 0; mm < R + 1; ++mm) {
                 m2_i32x4 bv, av0, av1;
-                if (mm < R) {  // input row i - U + mm, tap row R - 1 - mm
+                if (mm < R) {  // walk row q + mm, tap row tap_row(mm)
                     bv = __builtin_bit_cast(m2_i32x4, ring[(k + mm) % kM2Ring]);
-                    av0 = am[0][mm < R ? R - 1 - mm : 0];
-                    if constexpr (NP == 2) av1 = am[1][mm < R ? R - 1 - mm : 0];
-                } else {  // the tail: halo dwords of rows i - U + q (lanes h = 0), i - U + 4 + q (h = 1)
+                    av0 = am[0][mm < R ? mm : 0];
+                    if constexpr (NP == 2) av1 = am[1][mm < R ? mm : 0];
+                } else {  // the tail: halo dwords of walk rows q + e (lanes h = 0), q + 4 + e (h = 1)
                     uint32_t tv[4];
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {  // a bit-select, not a select of array elements
+                    for (int e = 0; e < 4; ++e) {  // a bit-select, not a select of array elements
                         // (hipcc turns that into a dynamically indexed array in LDS)
-                        const uint32_t lo = tl[(k + q) % kM2Ring], hi = tl[(k + 4 + q) % kM2Ring];
-                        tv[q] = (hi & hmask) | (lo & ~hmask);
+                        const uint32_t lo = tl[(k + e) % kM2Ring], hi = tl[(k + 4 + e) % kM2Ring];
+                        tv[e] = (hi & hmask) | (lo & ~hmask);
                     }
                     bv = m2_i32x4{(int)tv[0], (int)tv[1], (int)tv[2], (int)tv[3]};
                     av0 = at[0];
@@ -304,7 +317,7 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
                 if constexpr (NP == 2) ah = __builtin_amdgcn_mfma_i32_32x32x32_i8(av1, bv, mm ? ah : m2_i32x16{}, 0, 0, 0);
                 if (mm < 4) g[mm] = stage4(pa, pah, mm);  // row i - 1, between the MFMAs
             }
-            store_row(g, i - 1, kk > 0 || iq > i0);
+            store_row(g, orow0 + dir * (q - 1), q > 0);
         }
     }
     {  // the strip's last row
@@ -312,7 +325,7 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
         uint32_t g[4];
 #pragma unroll
         for (int gi = 0; gi < 4; ++gi) g[gi] = stage4(acc[kl & 1], acch[kl & 1], gi);
-        store_row(g, i0 + kM2Strip - 1, true);
+        store_row(g, orow0 + dir * (kM2Strip - 1), true);
     }
 }
 
