@@ -70,7 +70,7 @@ SELF_HALO = os.environ.get("FIR_SELF_HALO") == "1"
 # N > 1 halo source: "xgmi" (default: neighbours' HBM mapped once, read by the edge kernel) or
 # "rccl" (send/recv every step); xgmi falls back to rccl on every rank if any rank cannot map.
 HALO_PREF = os.environ.get("FIR_HALO", "xgmi")
-KERNELS = {"fir1d_i16": "fir1d_reg_kernel", "cplx_i16": "fir1d_reg_kernel", "fir2d_u8": "fir2d_reg_kernel",
+KERNELS = {"fir1d_i16": "fir1d_reg_kernel", "cplx_i16": "fir1d_reg_kernel", "fir2d_u8": "fir2d_pk16_strip_kernel",
            "fir1d_u8": "fir1d_reg_kernel", "ideal_u8": "fir1d_ideal_kernel", "bank_u8": "fir1d_reg_kernel",
            "restore_u8": "restore_map_kernel", "metrics_u8": "metrics_pass1+2"}
 NUMPY_ONLY = ("restore_u8", "metrics_u8")  # no C oracle leg: the NumPy restatement is the CPU baseline
@@ -547,7 +547,8 @@ def main() -> int:
                      "kernel": "fir2d_mfma_kernel" if wl.gen2d else KERNELS[args.workload],
                      "limiter": ("HBM (int8 MFMA Toeplitz rows; the memory-only twin of its loads and stores "
                                  "takes 82.5 us per 4 frames, DESIGN.md §5)" if wl.gen2d else
-                                 "VALU (~8.8 VALU instructions/pixel on packed 16-bit pixel pairs, DESIGN.md §5)")
+                                 "HBM (separable packed-16 strips; alternate strips walk up so the rows two "
+                                 "strips share are read once, PMC 1.001x; DESIGN.md §5)")
                      if args.workload == "fir2d_u8" else "HBM",
                      "kernel_avg_us": round(kern_avg_s * 1e6, 2), "algorithmic_bytes_per_launch": alg_bytes,
                      "timing": f"HIP events around {args.steps} back-to-back launches of the kernel"},

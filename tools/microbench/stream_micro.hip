@@ -349,6 +349,161 @@ void l_copy(const Bufs& b, hipStream_t s) {
                        reinterpret_cast<u32x4*>(b.y));
 }
 
+// int16 -> u8 narrowing copies (the i16 -> u8 FIR's bytes: 2 B in, 1 B out per sample): a wave
+// reads K KiB (K 16-byte loads per lane, each a contiguous 1 KiB) and writes K/2 KiB (the high
+// bytes), as 8-byte (K = 1) or 16-byte stores per lane; POL as st16 (0 plain, 1 nt).
+template <int K, int POL>
+__global__ __launch_bounds__(256) void narrow_copy(const u32x4* __restrict__ x, uint8_t* __restrict__ y) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const u32x4* src = x + wave * (64 * K);
+    u32x4 d[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) d[k] = __builtin_nontemporal_load(src + k * 64 + lane);
+    uint32_t h[2 * K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        h[2 * k] = __builtin_amdgcn_perm(d[k].y, d[k].x, 0x07050301u);
+        h[2 * k + 1] = __builtin_amdgcn_perm(d[k].w, d[k].z, 0x07050301u);
+    }
+    if constexpr (K == 1) {
+        u32x2* dst = reinterpret_cast<u32x2*>(y) + wave * 64 + lane;
+        if constexpr (POL == 1) __builtin_nontemporal_store(u32x2{h[0], h[1]}, dst);
+        else *dst = u32x2{h[0], h[1]};
+    } else {
+        // two input rows' high bytes per 1 KiB of output, as two 512-byte row stores (a traffic
+        // ceiling: the byte order differs from the input's and is not checked)
+#pragma unroll
+        for (int j = 0; j < K / 2; ++j) {
+            u32x2* dst = reinterpret_cast<u32x2*>(y) + wave * (64 * K) + 128 * j;
+            if constexpr (POL == 1) {
+                __builtin_nontemporal_store(u32x2{h[4 * j], h[4 * j + 1]}, dst + lane);
+                __builtin_nontemporal_store(u32x2{h[4 * j + 2], h[4 * j + 3]}, dst + 64 + lane);
+            } else {
+                dst[lane] = u32x2{h[4 * j], h[4 * j + 1]};
+                dst[64 + lane] = u32x2{h[4 * j + 2], h[4 * j + 3]};
+            }
+        }
+    }
+}
+template <int K, int POL>
+void l_narrow(const Bufs& b, hipStream_t s) {
+    hipLaunchKernelGGL((narrow_copy<K, POL>), dim3((unsigned)(b.n / (512 * K) / 4)), dim3(256), 0, s,
+                       reinterpret_cast<const u32x4*>(b.x), reinterpret_cast<uint8_t*>(b.y));
+}
+
+// The long-filter MFMA kernel's memory pattern, rebuilt step by step from narrow_copy (dev
+// ladder): persistent waves walk 1024-sample tiles grid-stride (2048 blocks of 4 waves), read a
+// tile's window and write its 1 KiB of u8.  W: 0 = the tile's 2 KiB, 1 = the MFMA kernel's
+// window (1088 samples from 16 before the tile, 3 loads per lane, lanes past it re-load its last
+// vector).  PF: window of the next tile loaded before this tile's store (1 in flight).  LDS:
+// the window goes through wave-private LDS as two byte planes, read back as 16-byte fragments.
+template <int W, bool PF, bool LDS>
+__global__ __launch_bounds__(256, 4) void mfpat(const int16_t* __restrict__ x, uint8_t* __restrict__ y, uint32_t ntiles) {
+    constexpr int NIT = W ? 3 : 2;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[4][2 * 1632];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t step = gridDim.x * 4;
+    uint32_t tile = blockIdx.x * 4 + wv;
+    u32x4 raw[NIT];
+    auto load = [&](uint32_t t) {
+        const int64_t w0 = (int64_t)t * 1024 - (W ? 16 : 0);
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            int v = it * 64 + lane;
+            if (W) v = v < 136 ? v : 135;
+            int64_t g = w0 + 8 * v;
+            g = g < 0 ? 0 : (g > (int64_t)ntiles * 1024 - 8 ? (int64_t)ntiles * 1024 - 8 : g);  // stay inside x
+            raw[it] = *reinterpret_cast<const u32x4*>(x + g);
+        }
+    };
+    if (tile < ntiles) load(tile);
+    for (; tile < ntiles; tile += step) {
+        uint32_t hv[4];
+        if constexpr (LDS) {
+            uint8_t* ph = lds[wv];
+            uint8_t* pl = lds[wv] + 1632;
+#pragma unroll
+            for (int it = 0; it < NIT; ++it) {
+                const int v = it * 64 + lane;
+                if (v < 136) {
+                    const int pos = 8 * v + ((8 * v) >> 5) * 16;
+                    *reinterpret_cast<u32x2*>(&ph[pos]) = u32x2{__builtin_amdgcn_perm(raw[it].y, raw[it].x, 0x07050301u),
+                                                                __builtin_amdgcn_perm(raw[it].w, raw[it].z, 0x07050301u)};
+                    *reinterpret_cast<u32x2*>(&pl[pos]) = u32x2{__builtin_amdgcn_perm(raw[it].y, raw[it].x, 0x06040200u),
+                                                                __builtin_amdgcn_perm(raw[it].w, raw[it].z, 0x06040200u)};
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            const int r = lane & 31, hf = lane >> 5;
+            u32x4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int i = 32 * r + 32 * s + 16 * hf, pos = i + (i >> 5) * 16;
+                acc ^= *reinterpret_cast<const u32x4*>(&ph[pos]);
+                acc ^= *reinterpret_cast<const u32x4*>(&pl[pos]);
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            hv[0] = acc.x, hv[1] = acc.y, hv[2] = acc.z, hv[3] = acc.w;
+        } else {
+            hv[0] = __builtin_amdgcn_perm(raw[0].y, raw[0].x, 0x07050301u);
+            hv[1] = __builtin_amdgcn_perm(raw[0].w, raw[0].z, 0x07050301u);
+            hv[2] = __builtin_amdgcn_perm(raw[1].y, raw[1].x, 0x07050301u);
+            hv[3] = __builtin_amdgcn_perm(raw[1].w, raw[1].z, 0x07050301u);
+        }
+        const uint32_t nxt = tile + step < ntiles ? tile + step : tile;
+        if constexpr (PF) load(nxt);
+        __builtin_nontemporal_store(u32x4{hv[0], hv[1], hv[2], hv[3]}, reinterpret_cast<u32x4*>(y + (int64_t)tile * 1024) + lane);
+        if constexpr (!PF) load(nxt);
+    }
+}
+template <int W, bool PF, bool LDS>
+void l_mfpat(const Bufs& b, hipStream_t s) {
+    hipLaunchKernelGGL((mfpat<W, PF, LDS>), dim3(2048), dim3(256), 0, s, b.x, reinterpret_cast<uint8_t*>(b.y),
+                       (uint32_t)(b.n / 1024));
+}
+// The same tile loop (2 KiB aligned read, 1 KiB store, next tile prefetched) with the work split
+// varied: BLOCKS grid-stride blocks (0 = one tile per wave), ORDER 0 = tile += all waves, 1 = each
+// wave a contiguous run of tiles, 2 = each XCD (blocks b % 8) a contiguous eighth, walked
+// grid-stride by its own waves; MINB = blocks per CU the registers must allow.
+template <int ORDER, int MINB>
+__global__ __launch_bounds__(256, MINB) void mfsplit(const int16_t* __restrict__ x, uint8_t* __restrict__ y,
+                                                     uint32_t ntiles) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t nw = gridDim.x * 4, w = blockIdx.x * 4 + wv;
+    uint32_t t0, t1, step;
+    if constexpr (ORDER == 0) {
+        t0 = w, t1 = ntiles, step = nw;
+    } else if constexpr (ORDER == 1) {
+        const uint32_t per = (ntiles + nw - 1) / nw;
+        t0 = w * per, t1 = min(t0 + per, ntiles), step = 1;
+    } else {
+        const uint32_t x8 = blockIdx.x % 8, per = (ntiles + 7) / 8, lo = x8 * per;
+        t0 = lo + (blockIdx.x / 8) * 4 + wv, t1 = min(lo + per, ntiles), step = nw / 8;
+    }
+    u32x4 raw[2];
+    auto load = [&](uint32_t t) {
+        const u32x4* src = reinterpret_cast<const u32x4*>(x + (int64_t)t * 1024);
+        raw[0] = src[lane];
+        raw[1] = src[64 + lane];
+    };
+    if (t0 < t1) load(t0);
+    for (uint32_t t = t0; t < t1; t += step) {
+        const u32x4 h = {__builtin_amdgcn_perm(raw[0].y, raw[0].x, 0x07050301u), __builtin_amdgcn_perm(raw[0].w, raw[0].z, 0x07050301u),
+                         __builtin_amdgcn_perm(raw[1].y, raw[1].x, 0x07050301u), __builtin_amdgcn_perm(raw[1].w, raw[1].z, 0x07050301u)};
+        load(t + step < t1 ? t + step : t);
+        __builtin_nontemporal_store(h, reinterpret_cast<u32x4*>(y + (int64_t)t * 1024) + lane);
+    }
+}
+template <int BLOCKS, int ORDER, int MINB>
+void l_mfsplit(const Bufs& b, hipStream_t s) {
+    const uint32_t nt = (uint32_t)(b.n / 1024);
+    hipLaunchKernelGGL((mfsplit<ORDER, MINB>), dim3(BLOCKS ? BLOCKS : nt / 4), dim3(256), 0, s, b.x,
+                       reinterpret_cast<uint8_t*>(b.y), nt);
+}
+
 template <int E>
 void l_whe(const Bufs& b, hipStream_t s) {
     hipLaunchKernelGGL((widen_half_edge<E>), dim3((unsigned)(b.n / 4 / 256)), dim3(256), 0, s, b.x, b.y, b.n / 4);
@@ -378,14 +533,21 @@ int main(int argc, char** argv) {
     const double rw = b.n * 6.0, rd = b.n * 2.0, wr = b.n * 4.0;
     std::vector<V> vs = {
         {"widen half row nt", l_wdpat<1, 0, 1, 256>, rw, true, {}},
-        {"widen half row nt +4K", l_wdpat_off<4096>, rw, false, {}},
-        {"widen half row nt +64K", l_wdpat_off<65536>, rw, false, {}},
-        {"widen half row nt +1M4K", l_wdpat_off<(1 << 20) + 4096>, rw, false, {}},
-        {"widen half row nt +2M", l_wdpat_off<(2 << 20)>, rw, false, {}},
-        {"widen half row nt +3M", l_wdpat_off<(3 << 20)>, rw, false, {}},
-        {"widen half row nt +256", l_wdpat_off<256>, rw, false, {}},
-        {"widen half row nt b", l_wdpat<1, 0, 1, 256>, rw, true, {}},
         {"copy 1:1 int16 nt", l_copy, b.n * 4.0, false, {}},
+        {"narrow i16->u8 K2 nt", l_narrow<2, 1>, b.n * 3.0, false, {}},
+        {"narrow i16->u8 K4 nt", l_narrow<4, 1>, b.n * 3.0, false, {}},
+        {"mfpat tile2K pf", l_mfpat<0, true, false>, b.n * 3.0, false, {}},
+        {"mfpat win pf lds", l_mfpat<1, true, true>, b.n * 3.0, false, {}},
+        {"split one-shot", l_mfsplit<0, 0, 4>, b.n * 3.0, false, {}},
+        {"split 1024 stride", l_mfsplit<1024, 0, 4>, b.n * 3.0, false, {}},
+        {"split 2048 stride", l_mfsplit<2048, 0, 4>, b.n * 3.0, false, {}},
+        {"split 4096 stride", l_mfsplit<4096, 0, 4>, b.n * 3.0, false, {}},
+        {"split 8192 stride", l_mfsplit<8192, 0, 4>, b.n * 3.0, false, {}},
+        {"split 2048 stride mb8", l_mfsplit<2048, 0, 8>, b.n * 3.0, false, {}},
+        {"split 2048 contig", l_mfsplit<2048, 1, 4>, b.n * 3.0, false, {}},
+        {"split 1024 contig", l_mfsplit<1024, 1, 4>, b.n * 3.0, false, {}},
+        {"split 2048 xcd", l_mfsplit<2048, 2, 4>, b.n * 3.0, false, {}},
+        {"split 1024 xcd", l_mfsplit<1024, 2, 4>, b.n * 3.0, false, {}},
         {"read reg K1 b256", l_read_reg<1, 256>, rd, false, {}},
         {"write nt rows R1", l_wpat<0, 1, 1, 256>, wr, false, {}},
     };
