@@ -468,7 +468,7 @@ void l_mfpat(const Bufs& b, hipStream_t s) {
 // varied: BLOCKS grid-stride blocks (0 = one tile per wave), ORDER 0 = tile += all waves, 1 = each
 // wave a contiguous run of tiles, 2 = each XCD (blocks b % 8) a contiguous eighth, walked
 // grid-stride by its own waves; MINB = blocks per CU the registers must allow.
-template <int ORDER, int MINB>
+template <int ORDER, int MINB, bool NTL = false>
 __global__ __launch_bounds__(256, MINB) void mfsplit(const int16_t* __restrict__ x, uint8_t* __restrict__ y,
                                                      uint32_t ntiles) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -486,8 +486,13 @@ __global__ __launch_bounds__(256, MINB) void mfsplit(const int16_t* __restrict__
     u32x4 raw[2];
     auto load = [&](uint32_t t) {
         const u32x4* src = reinterpret_cast<const u32x4*>(x + (int64_t)t * 1024);
-        raw[0] = src[lane];
-        raw[1] = src[64 + lane];
+        if constexpr (NTL) {
+            raw[0] = __builtin_nontemporal_load(src + lane);
+            raw[1] = __builtin_nontemporal_load(src + 64 + lane);
+        } else {
+            raw[0] = src[lane];
+            raw[1] = src[64 + lane];
+        }
     };
     if (t0 < t1) load(t0);
     for (uint32_t t = t0; t < t1; t += step) {
@@ -497,10 +502,18 @@ __global__ __launch_bounds__(256, MINB) void mfsplit(const int16_t* __restrict__
         __builtin_nontemporal_store(h, reinterpret_cast<u32x4*>(y + (int64_t)t * 1024) + lane);
     }
 }
-template <int BLOCKS, int ORDER, int MINB>
+// contiguous runs of RUN tiles per wave over a grid sized to cover them once (dispatch order keeps
+// the active region compact)
+template <int RUN, int MINB>
+void l_mfrun(const Bufs& b, hipStream_t s) {
+    const uint32_t nt = (uint32_t)(b.n / 1024);
+    hipLaunchKernelGGL((mfsplit<1, MINB, false>), dim3(nt / (4 * RUN)), dim3(256), 0, s, b.x,
+                       reinterpret_cast<uint8_t*>(b.y), nt);
+}
+template <int BLOCKS, int ORDER, int MINB, bool NTL = false>
 void l_mfsplit(const Bufs& b, hipStream_t s) {
     const uint32_t nt = (uint32_t)(b.n / 1024);
-    hipLaunchKernelGGL((mfsplit<ORDER, MINB>), dim3(BLOCKS ? BLOCKS : nt / 4), dim3(256), 0, s, b.x,
+    hipLaunchKernelGGL((mfsplit<ORDER, MINB, NTL>), dim3(BLOCKS ? BLOCKS : nt / 4), dim3(256), 0, s, b.x,
                        reinterpret_cast<uint8_t*>(b.y), nt);
 }
 
@@ -536,18 +549,14 @@ int main(int argc, char** argv) {
         {"copy 1:1 int16 nt", l_copy, b.n * 4.0, false, {}},
         {"narrow i16->u8 K2 nt", l_narrow<2, 1>, b.n * 3.0, false, {}},
         {"narrow i16->u8 K4 nt", l_narrow<4, 1>, b.n * 3.0, false, {}},
-        {"mfpat tile2K pf", l_mfpat<0, true, false>, b.n * 3.0, false, {}},
-        {"mfpat win pf lds", l_mfpat<1, true, true>, b.n * 3.0, false, {}},
         {"split one-shot", l_mfsplit<0, 0, 4>, b.n * 3.0, false, {}},
-        {"split 1024 stride", l_mfsplit<1024, 0, 4>, b.n * 3.0, false, {}},
-        {"split 2048 stride", l_mfsplit<2048, 0, 4>, b.n * 3.0, false, {}},
-        {"split 4096 stride", l_mfsplit<4096, 0, 4>, b.n * 3.0, false, {}},
-        {"split 8192 stride", l_mfsplit<8192, 0, 4>, b.n * 3.0, false, {}},
-        {"split 2048 stride mb8", l_mfsplit<2048, 0, 8>, b.n * 3.0, false, {}},
-        {"split 2048 contig", l_mfsplit<2048, 1, 4>, b.n * 3.0, false, {}},
-        {"split 1024 contig", l_mfsplit<1024, 1, 4>, b.n * 3.0, false, {}},
-        {"split 2048 xcd", l_mfsplit<2048, 2, 4>, b.n * 3.0, false, {}},
-        {"split 1024 xcd", l_mfsplit<1024, 2, 4>, b.n * 3.0, false, {}},
+        {"split 1024 stride ntl", l_mfsplit<1024, 0, 4, true>, b.n * 3.0, false, {}},
+        {"run 2", l_mfrun<2, 4>, b.n * 3.0, false, {}},
+        {"run 4", l_mfrun<4, 4>, b.n * 3.0, false, {}},
+        {"run 8", l_mfrun<8, 4>, b.n * 3.0, false, {}},
+        {"run 16", l_mfrun<16, 4>, b.n * 3.0, false, {}},
+        {"run 4 mb2", l_mfrun<4, 2>, b.n * 3.0, false, {}},
+        {"run 8 mb2", l_mfrun<8, 2>, b.n * 3.0, false, {}},
         {"read reg K1 b256", l_read_reg<1, 256>, rd, false, {}},
         {"write nt rows R1", l_wpat<0, 1, 1, 256>, wr, false, {}},
     };

@@ -68,6 +68,12 @@ constexpr int kMfMaxBlocks = FIR_MFMA_MAXBLOCKS;
 #ifndef FIR_MFMA_EXACT_LOADS         // lanes past a window issue no memory request (A/B)
 #define FIR_MFMA_EXACT_LOADS 0
 #endif
+#ifndef FIR_MFMA_LDAUX               // cache policy of the window loads (2 = non-temporal; A/B)
+#define FIR_MFMA_LDAUX 0
+#endif
+#ifndef FIR_MFMA_TPW                 // > 0: one-shot grid, each wave a run of TPW consecutive tiles with
+#define FIR_MFMA_TPW 0               // its tap fragments loaded from a device table (A/B)
+#endif
 #ifndef FIR_MFMA_TWIN                // A/B twins: 1 = no MFMAs (memory + staging only), 2 = no window loads
 #define FIR_MFMA_TWIN 0
 #endif
@@ -119,7 +125,8 @@ template <typename InT, int STAGE, int KS, bool ACC32, bool FAST>
 __global__ __launch_bounds__(kBlock, FIR_MFMA_MINB) void fir1d_mfma_kernel(const InT* __restrict__ x,
                                                             typename OutTraits<STAGE>::T* __restrict__ y,
                                                             int64_t rowlen, int64_t tiles_per_row, int64_t ntiles,
-                                                            MfmaTaps taps, int P, uint32_t bias, int shl, int frac) {
+                                                            MfmaTaps taps, const mf_i32x4* __restrict__ frag,
+                                                            int P, uint32_t bias, int shl, int frac) {
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     typedef uint32_t u2 __attribute__((ext_vector_type(2)));
     constexpr bool I16 = sizeof(InT) == 2;
@@ -141,6 +148,11 @@ __global__ __launch_bounds__(kBlock, FIR_MFMA_MINB) void fir1d_mfma_kernel(const
     mf_i32x4 a_lo[KS], a_hi[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
+        if constexpr (FIR_MFMA_TPW > 0) {  // from the device table: one coalesced 1 KiB load each
+            a_lo[s] = frag[(2 * s) * kWave + lane];
+            a_hi[s] = frag[(2 * s + 1) * kWave + lane];
+            continue;
+        }
         uint32_t lo[4] = {0u, 0u, 0u, 0u}, hi[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
@@ -162,6 +174,11 @@ __global__ __launch_bounds__(kBlock, FIR_MFMA_MINB) void fir1d_mfma_kernel(const
     uint32_t step = gridDim.x * kMfWaves, nt32 = (uint32_t)ntiles;
     const uint32_t tpr = (uint32_t)tiles_per_row;
     uint32_t tile = blockIdx.x * kMfWaves + wv;
+    if constexpr (FIR_MFMA_TPW > 0) {  // a run of consecutive tiles per wave, grid covering them once
+        tile = (blockIdx.x * kMfWaves + wv) * FIR_MFMA_TPW;
+        step = 1;
+        nt32 = tile + FIR_MFMA_TPW < nt32 ? tile + FIR_MFMA_TPW : nt32;
+    }
 #if FIR_MFMA_XCD
     // XCD-major tiles: blocks b, b + 8, ... share an XCD (round-robin dispatch); give each XCD one
     // contiguous eighth of the tiles, walked grid-stride by its own waves
@@ -189,11 +206,11 @@ __global__ __launch_bounds__(kBlock, FIR_MFMA_MINB) void fir1d_mfma_kernel(const
             if constexpr (FIR_MFMA_TWIN == 2) {  // no window loads: synthetic samples
                 raw[it][0] = off, raw[it][1] = off + 1, raw[it][2] = off + 2, raw[it][3] = off + 3;
             } else if constexpr (I16) {
-                const mf_i32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+                const mf_i32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, FIR_MFMA_LDAUX);
                 raw[it][0] = q.x, raw[it][1] = q.y, raw[it][2] = q.z, raw[it][3] = q.w;
             } else {
                 typedef int i32x2 __attribute__((ext_vector_type(2)));
-                const i32x2 q = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+                const i32x2 q = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, FIR_MFMA_LDAUX);
                 raw[it][0] = q.x, raw[it][1] = q.y, raw[it][2] = 0u, raw[it][3] = 0u;
             }
         }
@@ -517,11 +534,9 @@ __global__ __launch_bounds__(kBlock) void fir1d_mfma_long_kernel(const InT* __re
     }
 }
 
-template <typename InT, int STAGE>
-static hipError_t launch_mfma_long(const void* x, void* y, int64_t rl, int64_t tpr, int64_t ntiles, const int32_t* hq,
-                                   int L, int P, int KS, uint32_t bias, bool fast, int frac, int acc_bits, hipStream_t s) {
-    using OutT = typename OutTraits<STAGE>::T;
-    // frag[s][p][lane] = bytes j = 0..15 of plane p's diagonal entries e = 31 - r + 32 s + 16 hf + j
+// frag[s][p][lane] = bytes j = 0..15 of plane p (0: hl, 1: hh) of the diagonal entries
+// e = 31 - r + 32 s + 16 hf + j (lane = r + 32 hf), as MfmaTaps lays them out
+static const mf_i32x4* mfma_frag_table(const int32_t* hq, int L, int P, int KS, std::string* err) {
     const int c = L / 2;
     std::vector<int8_t> tab((size_t)KS * 2 * kWave * 16);
     for (int st = 0; st < KS; ++st)
@@ -534,8 +549,15 @@ static hipError_t launch_mfma_long(const void* x, void* y, int64_t rl, int64_t t
                 tab[(((size_t)st * 2 + 0) * kWave + lane) * 16 + j] = (int8_t)lo;
                 tab[(((size_t)st * 2 + 1) * kWave + lane) * 16 + j] = (int8_t)((v - lo) / 256);
             }
+    return (const mf_i32x4*)device_table(tab.data(), tab.size(), err);
+}
+
+template <typename InT, int STAGE>
+static hipError_t launch_mfma_long(const void* x, void* y, int64_t rl, int64_t tpr, int64_t ntiles, const int32_t* hq,
+                                   int L, int P, int KS, uint32_t bias, bool fast, int frac, int acc_bits, hipStream_t s) {
+    using OutT = typename OutTraits<STAGE>::T;
     std::string err;
-    const mf_i32x4* fr = (const mf_i32x4*)device_table(tab.data(), tab.size(), &err);
+    const mf_i32x4* fr = mfma_frag_table(hq, L, P, KS, &err);
     if (!fr) return hipErrorOutOfMemory;
     const int64_t want = (ntiles + kMfWaves - 1) / kMfWaves;
     const unsigned blocks = (unsigned)(want < FIR_MFMA_LONG_BLOCKS ? want : FIR_MFMA_LONG_BLOCKS);
@@ -553,19 +575,28 @@ static hipError_t launch_mfma_long(const void* x, void* y, int64_t rl, int64_t t
 
 template <typename InT, int STAGE, int KS>
 static hipError_t launch_mfma_ks(const void* x, void* y, int64_t rowlen, int64_t tpr, int64_t ntiles, const MfmaTaps& t,
-                                 int P, uint32_t bias, bool fast, int frac, int acc_bits, hipStream_t s) {
+                                 const int32_t* hq, int L, int P, uint32_t bias, bool fast, int frac, int acc_bits,
+                                 hipStream_t s) {
     using OutT = typename OutTraits<STAGE>::T;
     const int64_t want = (ntiles + kMfWaves - 1) / kMfWaves;
-    const unsigned blocks = (unsigned)(want < kMfMaxBlocks ? want : kMfMaxBlocks);
+    unsigned blocks = (unsigned)(want < kMfMaxBlocks ? want : kMfMaxBlocks);
+    const mf_i32x4* fr = nullptr;
+    if constexpr (FIR_MFMA_TPW > 0) {
+        std::string err;
+        fr = mfma_frag_table(hq, L, P, KS, &err);
+        if (!fr) return hipErrorOutOfMemory;
+        const int64_t per_block = (int64_t)kMfWaves * FIR_MFMA_TPW;
+        blocks = (unsigned)((ntiles + per_block - 1) / per_block);
+    }
     if (fast)
         hipLaunchKernelGGL((fir1d_mfma_kernel<InT, STAGE, KS, true, true>), dim3(blocks), dim3(kBlock), 0, s, (const InT*)x,
-                           (OutT*)y, rowlen, tpr, ntiles, t, P, bias, 0, frac);
+                           (OutT*)y, rowlen, tpr, ntiles, t, fr, P, bias, 0, frac);
     else if (acc_bits == 32)
         hipLaunchKernelGGL((fir1d_mfma_kernel<InT, STAGE, KS, true, false>), dim3(blocks), dim3(kBlock), 0, s, (const InT*)x,
-                           (OutT*)y, rowlen, tpr, ntiles, t, P, bias, 0, frac);
+                           (OutT*)y, rowlen, tpr, ntiles, t, fr, P, bias, 0, frac);
     else
         hipLaunchKernelGGL((fir1d_mfma_kernel<InT, STAGE, KS, false, false>), dim3(blocks), dim3(kBlock), 0, s,
-                           (const InT*)x, (OutT*)y, rowlen, tpr, ntiles, t, P, bias, 32 - acc_bits, frac);
+                           (const InT*)x, (OutT*)y, rowlen, tpr, ntiles, t, fr, P, bias, 32 - acc_bits, frac);
     return hipGetLastError();
 }
 
@@ -594,8 +625,8 @@ static hipError_t launch_mfma_t(const void* x, void* y, int64_t rows, int64_t ro
         t.lo[e] = (int8_t)lo;
         t.hi[e] = (int8_t)((v - lo) / 256);
     }
-    if (KS == 2) return launch_mfma_ks<InT, STAGE, 2>(x, y, rl, tpr, ntiles, t, P, bias, fast, frac, acc_bits, s);
-    return launch_mfma_ks<InT, STAGE, 3>(x, y, rl, tpr, ntiles, t, P, bias, fast, frac, acc_bits, s);
+    if (KS == 2) return launch_mfma_ks<InT, STAGE, 2>(x, y, rl, tpr, ntiles, t, hq, L, P, bias, fast, frac, acc_bits, s);
+    return launch_mfma_ks<InT, STAGE, 3>(x, y, rl, tpr, ntiles, t, hq, L, P, bias, fast, frac, acc_bits, s);
 }
 
 bool mfma_path_ok(const void* x, const void* y, int in_dtype, int64_t rows, int64_t rowlen, int64_t total, int ch,
