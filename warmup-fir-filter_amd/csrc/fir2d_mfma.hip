@@ -329,9 +329,10 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
     }
 }
 
-// Output rows per wave: by default the strips are sized so that the launch is ONE round of
-// resident waves (occupancy x CUs x 4), which removes the partial last round of fixed strips;
-// FIR2D_MFMA_ROWS=n forces n (rounded up to the unrolled turn; A/B).
+// Output rows per wave: 32 for one tap plane (alternating walks, below); otherwise the strips are
+// sized so that the launch is ONE round of resident waves (occupancy x CUs x 4), which removes the
+// partial last round of fixed strips; FIR2D_MFMA_ROWS=n forces n (rounded up to the unrolled
+// turn; A/B).
 template <int R, int NP, bool FAST, bool ACC32>
 static int m2_rows_per_strip(int64_t frames, int64_t ncol, int64_t H, hipStream_t s) {
     constexpr int UN = (M2Geom<R>::RING & 1) ? 2 * M2Geom<R>::RING : M2Geom<R>::RING;
@@ -339,6 +340,12 @@ static int m2_rows_per_strip(int64_t frames, int64_t ncol, int64_t H, hipStream_
     const char* env = getenv("FIR2D_MFMA_ROWS");
     if (env && atoi(env) > 0) {
         rows = atoi(env);
+    } else if (NP == 1 && FIR2D_MFMA_ALT) {
+        // one tap plane with alternating walks: short strips keep neighbours in step (their
+        // shared rows then come from L2); 32 rows: the general 5x5 85.4 -> 81.2 us per 4
+        // frames, while two planes stay faster with one round (108 vs 119;
+        // profiles/r03/ab2d_mfma_alt_rows.txt)
+        rows = 32;
     } else {
         // waves of this instantiation resident at once on the stream's device, cached per device
         // (a benign race: concurrent first calls compute the same value)
