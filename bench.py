@@ -545,8 +545,8 @@ def main() -> int:
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "fir2d_mfma_kernel" if wl.gen2d else KERNELS[args.workload],
-                     "limiter": ("HBM (int8 MFMA Toeplitz rows; the memory-only twin of its loads and stores "
-                                 "takes 82.5 us per 4 frames, DESIGN.md §5)" if wl.gen2d else
+                     "limiter": ("HBM (int8 MFMA Toeplitz rows, 32-row strips walking alternately down and up; "
+                                 "PMC 1.008x, DESIGN.md §5)" if wl.gen2d else
                                  "HBM (separable packed-16 strips; alternate strips walk up so the rows two "
                                  "strips share are read once, PMC 1.001x; DESIGN.md §5)")
                      if args.workload == "fir2d_u8" else "HBM",
