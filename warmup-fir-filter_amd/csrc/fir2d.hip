@@ -288,23 +288,6 @@ static bool sep2d_register_form(const int32_t* hq, int R, int C) {
     return R > 1 && C > 1 && rank1_factor(hq, R, C, col, row);
 }
 
-// kernels of at most 3x3 taps whose general packed-16 register form applies (2 pixels per
-// v_pk_mad_u16, <= 4.5 per pixel): the register kernel beats the MFMA path there
-static bool small_pk16_form(const int32_t* hq, int R, int C, int frac, int acc_bits) {
-    if (R * C > 9 || frac > 22 || acc_bits > 32) return false;
-    int64_t habs = 0;
-    for (int k = 0; k < R * C; ++k) habs += hq[k] < 0 ? -(int64_t)hq[k] : hq[k];
-    if (255 * habs + ((int64_t)1 << (frac - 1)) >= ((int64_t)1 << (acc_bits - 1))) return false;  // nowrap
-#define FIR2D_PKC(r, c)                            \
-    if (R == r && C == c) {                        \
-        Taps2<r, c> t = {};                        \
-        return plan_pk16_gen(t, hq, frac) != 0;    \
-    }
-    FIR2D_PKC(1, 3) FIR2D_PKC(3, 1) FIR2D_PKC(3, 3)
-#undef FIR2D_PKC
-    return false;
-}
-
 int launch_fir2d(const uint8_t* x, int64_t frames, int64_t H, int64_t W, const int32_t* hq, int R, int C, int frac,
                  int acc_bits, int stage, void* y, hipStream_t stream, std::string* err) {
     if (stage != FIR_OUT_U8_SAT && stage != FIR_OUT_I32) return *err = "out_stage must be FIR_OUT_U8_SAT or FIR_OUT_I32", FIR_EINVAL;
@@ -329,13 +312,14 @@ int launch_fir2d(const uint8_t* x, int64_t frames, int64_t H, int64_t W, const i
     const bool fast = reg2d_shape(R, C) && W % kVec2d == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)y % 16 == 0 &&
                       acc_bits <= 32 && frac <= 31 && taps16 && W >= kVec2d && H <= 65535 * (int64_t)kStrip2dSep;
     hipError_t e = hipErrorNotSupported;
-    // matrix-core path (fir2d_mfma.hip) unless FIR2D_PATH=reg; rank-1 kernels and <= 3x3 kernels
-    // with a packed-16 register form keep the register kernels by default (faster there:
-    // 85.8 vs 88.4 us for the bench's separable 5x5, 82.7 vs 86.9 us for a 3x3 sharpen per
-    // 4-frame launch; profiles/r02/ab2d_mfma_*.txt).  FIR2D_PATH=mfma takes the MFMA path for them.
+    // matrix-core path (fir2d_mfma.hip) unless FIR2D_PATH=reg; rank-1 kernels keep the separable
+    // register kernels by default (faster there: 79.3 vs 83.7 us for the bench's separable 5x5 per
+    // 4-frame launch).  Since the MFMA kernel's strips walk both ways it also beats the general
+    // packed-16 register form of a 3x3 sharpen (82.6 vs 83.8 us; round 2 had 86.9 vs 82.7;
+    // profiles/r03/ab2d_paths.txt).  FIR2D_PATH=mfma takes the MFMA path for rank-1 kernels too.
     const char* path = getenv("FIR2D_PATH");
     const bool force = path && !strcmp(path, "mfma"), off = path && !strcmp(path, "reg");
-    if (!off && (force || (!sep2d_register_form(hq, R, C) && !small_pk16_form(hq, R, C, frac, acc_bits))))
+    if (!off && (force || !sep2d_register_form(hq, R, C)))
         e = launch_fir2d_mfma(x, frames, H, W, hq, R, C, frac, acc_bits, stage, y, stream);
     if (e != hipErrorNotSupported) {
         // launched (or failed to launch) on the matrix cores
