@@ -468,13 +468,13 @@ void l_mfpat(const Bufs& b, hipStream_t s) {
 // varied: BLOCKS grid-stride blocks (0 = one tile per wave), ORDER 0 = tile += all waves, 1 = each
 // wave a contiguous run of tiles, 2 = each XCD (blocks b % 8) a contiguous eighth, walked
 // grid-stride by its own waves; MINB = blocks per CU the registers must allow.
-template <int ORDER, int MINB, bool NTL = false>
+template <int ORDER, int MINB, bool NTL = false, bool ST2 = false>
 __global__ __launch_bounds__(256, MINB) void mfsplit(const int16_t* __restrict__ x, uint8_t* __restrict__ y,
                                                      uint32_t ntiles) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t nw = gridDim.x * 4, w = blockIdx.x * 4 + wv;
     uint32_t t0, t1, step;
-    if constexpr (ORDER == 0) {
+    if constexpr (ORDER == 0 || ORDER == 3) {
         t0 = w, t1 = ntiles, step = nw;
     } else if constexpr (ORDER == 1) {
         const uint32_t per = (ntiles + nw - 1) / nw;
@@ -498,8 +498,14 @@ __global__ __launch_bounds__(256, MINB) void mfsplit(const int16_t* __restrict__
     for (uint32_t t = t0; t < t1; t += step) {
         const u32x4 h = {__builtin_amdgcn_perm(raw[0].y, raw[0].x, 0x07050301u), __builtin_amdgcn_perm(raw[0].w, raw[0].z, 0x07050301u),
                          __builtin_amdgcn_perm(raw[1].y, raw[1].x, 0x07050301u), __builtin_amdgcn_perm(raw[1].w, raw[1].z, 0x07050301u)};
-        load(t + step < t1 ? t + step : t);
-        __builtin_nontemporal_store(h, reinterpret_cast<u32x4*>(y + (int64_t)t * 1024) + lane);
+        if (ORDER != 3 || t + step < t1) load(t + step < t1 ? t + step : t);  // ORDER 3: no reload past the end
+        if constexpr (ST2) {  // two 512-byte row stores (8 bytes per lane each)
+            u32x2* d2 = reinterpret_cast<u32x2*>(y + (int64_t)t * 1024);
+            __builtin_nontemporal_store(u32x2{h.x, h.y}, d2 + lane);
+            __builtin_nontemporal_store(u32x2{h.z, h.w}, d2 + 64 + lane);
+        } else {
+            __builtin_nontemporal_store(h, reinterpret_cast<u32x4*>(y + (int64_t)t * 1024) + lane);
+        }
     }
 }
 // contiguous runs of RUN tiles per wave over a grid sized to cover them once (dispatch order keeps
@@ -510,10 +516,10 @@ void l_mfrun(const Bufs& b, hipStream_t s) {
     hipLaunchKernelGGL((mfsplit<1, MINB, false>), dim3(nt / (4 * RUN)), dim3(256), 0, s, b.x,
                        reinterpret_cast<uint8_t*>(b.y), nt);
 }
-template <int BLOCKS, int ORDER, int MINB, bool NTL = false>
+template <int BLOCKS, int ORDER, int MINB, bool NTL = false, bool ST2 = false>
 void l_mfsplit(const Bufs& b, hipStream_t s) {
     const uint32_t nt = (uint32_t)(b.n / 1024);
-    hipLaunchKernelGGL((mfsplit<ORDER, MINB, NTL>), dim3(BLOCKS ? BLOCKS : nt / 4), dim3(256), 0, s, b.x,
+    hipLaunchKernelGGL((mfsplit<ORDER, MINB, NTL, ST2>), dim3(BLOCKS ? BLOCKS : nt / 4), dim3(256), 0, s, b.x,
                        reinterpret_cast<uint8_t*>(b.y), nt);
 }
 
@@ -550,13 +556,12 @@ int main(int argc, char** argv) {
         {"narrow i16->u8 K2 nt", l_narrow<2, 1>, b.n * 3.0, false, {}},
         {"narrow i16->u8 K4 nt", l_narrow<4, 1>, b.n * 3.0, false, {}},
         {"split one-shot", l_mfsplit<0, 0, 4>, b.n * 3.0, false, {}},
-        {"split 1024 stride ntl", l_mfsplit<1024, 0, 4, true>, b.n * 3.0, false, {}},
-        {"run 2", l_mfrun<2, 4>, b.n * 3.0, false, {}},
-        {"run 4", l_mfrun<4, 4>, b.n * 3.0, false, {}},
-        {"run 8", l_mfrun<8, 4>, b.n * 3.0, false, {}},
-        {"run 16", l_mfrun<16, 4>, b.n * 3.0, false, {}},
-        {"run 4 mb2", l_mfrun<4, 2>, b.n * 3.0, false, {}},
-        {"run 8 mb2", l_mfrun<8, 2>, b.n * 3.0, false, {}},
+        {"oneshot", l_mfsplit<0, 3, 4>, b.n * 3.0, false, {}},
+        {"oneshot ntl", l_mfsplit<0, 3, 4, true>, b.n * 3.0, false, {}},
+        {"oneshot st2", l_mfsplit<0, 3, 4, false, true>, b.n * 3.0, false, {}},
+        {"oneshot ntl st2", l_mfsplit<0, 3, 4, true, true>, b.n * 3.0, false, {}},
+        {"stride1024 ntl st2", l_mfsplit<1024, 3, 4, true, true>, b.n * 3.0, false, {}},
+        {"stride2048 ntl st2", l_mfsplit<2048, 3, 4, true, true>, b.n * 3.0, false, {}},
         {"read reg K1 b256", l_read_reg<1, 256>, rd, false, {}},
         {"write nt rows R1", l_wpat<0, 1, 1, 256>, wr, false, {}},
     };

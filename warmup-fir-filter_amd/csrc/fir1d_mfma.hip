@@ -268,7 +268,8 @@ __global__ __launch_bounds__(kBlock, FIR_MFMA_MINB) void fir1d_mfma_kernel(const
         // ---- the next tile's window goes out now, its latency hidden behind this tile's math
         // (unconditional: past the last tile it re-loads this one, so every path into the loop
         // header has the same memory operations in flight and the compiler's wait there stays exact)
-        load_window(mf_tile(tile + DEPTH * step < nt32 ? tile + DEPTH * step : tile, rowlen, tpr), raw);
+        if constexpr (FIR_MFMA_TPW != 1)  // one tile per wave: nothing to prefetch
+            load_window(mf_tile(tile + DEPTH * step < nt32 ? tile + DEPTH * step : tile, rowlen, tpr), raw);
         __builtin_amdgcn_wave_barrier();  // one wave's LDS ops complete in order
         asm volatile("" ::: "memory");
 
