@@ -523,6 +523,64 @@ void l_mfsplit(const Bufs& b, hipStream_t s) {
                        reinterpret_cast<uint8_t*>(b.y), nt);
 }
 
+// Round 3b: persistent grid-stride with BIG steps: a wave reads TPS consecutive 1024-sample int16
+// tiles (2 TPS loads of 16 B per lane, all issued together) plus one 16-byte halo vector per lane
+// (the next step's first 1 KiB, as a long filter's window needs), converts, and writes TPS KiB of
+// u8; the next step's loads are issued right after the conversion (one step in flight while the
+// stores go).  LDS: the high bytes pass through wave-private LDS (write + read back) as the MFMA
+// kernel's byte planes do.  WALK > 0: each wave instead walks a contiguous run of WALK steps.
+template <int TPS, bool LDS, int WALK>
+__global__ __launch_bounds__(256, 4) void mfbig(const int16_t* __restrict__ x, uint8_t* __restrict__ y, uint32_t nsteps) {
+    constexpr int NL = 2 * TPS;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[4][LDS ? 1024 * TPS + 64 : 16];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t step = gridDim.x * 4, s0 = blockIdx.x * 4 + wv, s1 = nsteps;
+    if constexpr (WALK > 0) {
+        s0 = (blockIdx.x * 4 + wv) * WALK, s1 = min(s0 + WALK, nsteps), step = 1;
+    }
+    u32x4 raw[NL], halo;
+    auto load = [&](uint32_t t) {
+        const u32x4* src = reinterpret_cast<const u32x4*>(x + (int64_t)t * 1024 * TPS);
+#pragma unroll
+        for (int k = 0; k < NL; ++k) raw[k] = src[64 * k + lane];
+        halo = t + 1 < nsteps ? src[64 * NL + (lane & 7)] : u32x4{0u, 0u, 0u, 0u};
+    };
+    if (s0 < s1) load(s0);
+    for (uint32_t t = s0; t < s1; t += step) {
+        uint32_t h[2 * NL];
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+            h[2 * k] = __builtin_amdgcn_perm(raw[k].y, raw[k].x, 0x07050301u);
+            h[2 * k + 1] = __builtin_amdgcn_perm(raw[k].w, raw[k].z, 0x07050301u) ^ halo.x;
+        }
+        if constexpr (LDS) {
+            uint8_t* p = lds[wv];
+#pragma unroll
+            for (int k = 0; k < NL; ++k) *reinterpret_cast<u32x2*>(&p[512 * k + 8 * lane]) = u32x2{h[2 * k], h[2 * k + 1]};
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int k = 0; k < TPS; ++k) {
+                const u32x4 q = *reinterpret_cast<const u32x4*>(&p[1024 * k + 16 * lane]);
+                h[4 * k] = q.x, h[4 * k + 1] = q.y, h[4 * k + 2] = q.z, h[4 * k + 3] = q.w;
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+        }
+        load(t + step < s1 ? t + step : t);
+#pragma unroll
+        for (int k = 0; k < TPS; ++k)
+            __builtin_nontemporal_store(u32x4{h[4 * k], h[4 * k + 1], h[4 * k + 2], h[4 * k + 3]},
+                                        reinterpret_cast<u32x4*>(y + ((int64_t)t * TPS + k) * 1024) + lane);
+    }
+}
+template <int TPS, bool LDS, int BLOCKS, int WALK = 0>
+void l_mfbig(const Bufs& b, hipStream_t s) {
+    const uint32_t ns = (uint32_t)(b.n / 1024 / TPS);
+    const unsigned blocks = WALK ? (ns / WALK + 3) / 4 : BLOCKS;
+    hipLaunchKernelGGL((mfbig<TPS, LDS, WALK>), dim3(blocks), dim3(256), 0, s, b.x, reinterpret_cast<uint8_t*>(b.y), ns);
+}
+
 template <int E>
 void l_whe(const Bufs& b, hipStream_t s) {
     hipLaunchKernelGGL((widen_half_edge<E>), dim3((unsigned)(b.n / 4 / 256)), dim3(256), 0, s, b.x, b.y, b.n / 4);
@@ -556,12 +614,18 @@ int main(int argc, char** argv) {
         {"narrow i16->u8 K2 nt", l_narrow<2, 1>, b.n * 3.0, false, {}},
         {"narrow i16->u8 K4 nt", l_narrow<4, 1>, b.n * 3.0, false, {}},
         {"split one-shot", l_mfsplit<0, 0, 4>, b.n * 3.0, false, {}},
-        {"oneshot", l_mfsplit<0, 3, 4>, b.n * 3.0, false, {}},
         {"oneshot ntl", l_mfsplit<0, 3, 4, true>, b.n * 3.0, false, {}},
-        {"oneshot st2", l_mfsplit<0, 3, 4, false, true>, b.n * 3.0, false, {}},
-        {"oneshot ntl st2", l_mfsplit<0, 3, 4, true, true>, b.n * 3.0, false, {}},
-        {"stride1024 ntl st2", l_mfsplit<1024, 3, 4, true, true>, b.n * 3.0, false, {}},
-        {"stride2048 ntl st2", l_mfsplit<2048, 3, 4, true, true>, b.n * 3.0, false, {}},
+        {"mfpat win pf lds", l_mfpat<1, true, true>, b.n * 3.0, false, {}},
+        {"big1 b1k", l_mfbig<1, false, 1024>, b.n * 3.0, false, {}},
+        {"big2 b1k", l_mfbig<2, false, 1024>, b.n * 3.0, false, {}},
+        {"big4 b1k", l_mfbig<4, false, 1024>, b.n * 3.0, false, {}},
+        {"big2 b2k", l_mfbig<2, false, 2048>, b.n * 3.0, false, {}},
+        {"big4 b2k", l_mfbig<4, false, 2048>, b.n * 3.0, false, {}},
+        {"big2 lds b1k", l_mfbig<2, true, 1024>, b.n * 3.0, false, {}},
+        {"big4 lds b1k", l_mfbig<4, true, 1024>, b.n * 3.0, false, {}},
+        {"big4 lds b2k", l_mfbig<4, true, 2048>, b.n * 3.0, false, {}},
+        {"big4 lds oneshot", l_mfbig<4, true, 0, 1>, b.n * 3.0, false, {}},
+        {"big2 lds walk4", l_mfbig<2, true, 0, 4>, b.n * 3.0, false, {}},
         {"read reg K1 b256", l_read_reg<1, 256>, rd, false, {}},
         {"write nt rows R1", l_wpat<0, 1, 1, 256>, wr, false, {}},
     };

@@ -383,6 +383,265 @@ __global__ __launch_bounds__(kBlock, FIR_MFMA_MINB) void fir1d_mfma_kernel(const
 }
 
 // ---------------------------------------------------------------------------------------
+// Step form (round 3b; the default up to FIR_MFMA_LONG_FROM taps): the same Toeplitz product,
+// but a wave's grid-stride unit is a STEP of TPS consecutive tiles of one row, whose window
+// (TPS * 1024 + 32 KS - 32 samples) is loaded at once and staged as byte planes in the wave's
+// LDS, the tiles' MFMAs reading it at offsets 1024 q.  Why: the tile kernel above keeps about
+// 2.2 KiB of useful loads in flight per wave (one window) and its loop header drains the
+// second window when two are prefetched (hipcc's wait merges the loop's entry edge, where no
+// stores follow the loads, with the back edge: measured DEPTH 2 = no gain), so its int16 forms
+// sat at the 147 us the same loop reaches as a pure copy (profiles/r03/long_taps_mfma_structure
+// .txt).  Here each wave keeps TPS * 2 KiB (int16) in flight during the whole step's math, the
+// window's halo is re-read once per step instead of once per tile, and the loop is shaped so
+// the compiler's waits are exact: every path into the loop header has the same memory operations
+// in flight (the entry edge issues the step's store count as dropped stores, descriptor size 0),
+// every load and store is unconditional (ranges clipped by the descriptors), and the wait at the
+// top of a step is vmcnt(stores of the previous step).
+#ifndef FIR_MF2                      // 0: the tile kernel for every short filter (A/B)
+#define FIR_MF2 1
+#endif
+#ifndef FIR_MF2_TPS                  // tiles per step
+#define FIR_MF2_TPS 2
+#endif
+#ifndef FIR_MF2_MINB                 // waves per SIMD the register allocation must allow
+#define FIR_MF2_MINB 4
+#endif
+#ifndef FIR_MF2_BLOCKS               // grid-stride blocks (4 waves each)
+#define FIR_MF2_BLOCKS 1024
+#endif
+#ifndef FIR_MF2_OLDS                 // int32 outputs through LDS as 1 KiB rows (0: permlane32 pairs)
+#define FIR_MF2_OLDS 1
+#endif
+#ifndef FIR_MF2_ACC3                 // int16: one accumulator for both cross products
+#define FIR_MF2_ACC3 1
+#endif
+#ifndef FIR_MF2_LDAUX                // cache policy of the body loads (2 = non-temporal; A/B)
+#define FIR_MF2_LDAUX 0
+#endif
+#ifndef FIR_MF2_TWIN                 // A/B twins: 1 = no MFMAs, 2 = no window loads, 3 = no stores
+#define FIR_MF2_TWIN 0
+#endif
+constexpr int kMf2Tps = FIR_MF2_TPS;
+
+template <typename InT, int STAGE, int KS, bool ACC32, bool FAST>
+__global__ __launch_bounds__(kBlock, FIR_MF2_MINB) void fir1d_mfma_step_kernel(const InT* __restrict__ x,
+                                                                typename OutTraits<STAGE>::T* __restrict__ y,
+                                                                int64_t rowlen, uint32_t steps_per_row, uint32_t nsteps,
+                                                                MfmaTaps taps, int P, uint32_t bias, int shl, int frac) {
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+    typedef int i32x2 __attribute__((ext_vector_type(2)));
+    constexpr bool I16 = sizeof(InT) == 2;
+    constexpr int TPS = kMf2Tps;
+    constexpr int HX = 32 * KS - 32;           // window samples past the step's TPS * 1024
+    constexpr int NB = 2 * TPS;                // body loads per lane: 8 samples each, 512 per load
+    constexpr int NL = NB + 1;                 // + one halo load (lanes 0 .. HX/8 - 1 distinct)
+    constexpr int PL = TPS * kMfTile + HX;     // bytes per byte plane
+    constexpr bool OLDS = STAGE == FIR_OUT_I32 && FIR_MF2_OLDS;
+    constexpr int OB = OLDS ? 4608 : 0;        // int32 output image (36-dword rows)
+    constexpr int WB = (I16 ? 2 * PL : PL) + OB;
+    constexpr int NST = STAGE == FIR_OUT_I32 ? 4 * TPS : TPS;  // 16-byte stores per lane and step
+    static_assert(HX / 8 >= 1 && HX / 8 <= kWave, "halo vectors");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kMfWaves][WB];
+
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & 31, hf = lane >> 5;
+    uint8_t* pl = lds[wv];             // xs (u8) or xls (int16) plane
+    uint8_t* ph = lds[wv] + PL;        // xh plane (int16)
+    uint32_t* ob = reinterpret_cast<uint32_t*>(lds[wv] + (I16 ? 2 * PL : PL));
+
+    // tap fragments A[r][32 s + 16 hf + j], j = 0..15 (as fir1d_mfma_kernel)
+    mf_i32x4 a_lo[KS], a_hi[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+        uint32_t lo[4] = {0u, 0u, 0u, 0u}, hi[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int e = 31 - r + 32 * s + 16 * hf + j;
+            lo[j / 4] |= (uint32_t)(uint8_t)taps.lo[e] << (8 * (j % 4));
+            hi[j / 4] |= (uint32_t)(uint8_t)taps.hi[e] << (8 * (j % 4));
+        }
+        a_lo[s] = mf_i32x4{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3]};
+        a_hi[s] = mf_i32x4{(int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+    const int32_t sat_hi = FAST ? (int32_t)((256u << (frac & 31)) - 1u) : 0;
+
+    const uint32_t stride = gridDim.x * kMfWaves;
+    uint32_t st = blockIdx.x * kMfWaves + wv;
+    if (st >= nsteps) return;  // wave-uniform: nothing issued yet
+
+    // ---- a step's window: NB body vectors per lane + one halo vector, from a descriptor over
+    // the row's part of [w0, w0 + PL); samples outside the row read as zeros
+    uint32_t raw[NL][4];
+    auto step_start = [&](uint32_t s, int64_t& rs, int64_t& re) __attribute__((always_inline)) -> int64_t {
+        const uint32_t row = __builtin_amdgcn_readfirstlane(s / steps_per_row);
+        const uint32_t k = __builtin_amdgcn_readfirstlane(s - row * steps_per_row);
+        rs = (int64_t)row * rowlen;
+        re = rs + rowlen;
+        return rs + (int64_t)k * (TPS * kMfTile);
+    };
+    auto load_step = [&](uint32_t s) __attribute__((always_inline)) {
+        int64_t rs, re;
+        const int64_t w0 = step_start(s, rs, re) - P;
+        const int64_t base = w0 > rs ? w0 : rs, end = re < w0 + PL ? re : w0 + PL;
+        const __amdgpu_buffer_rsrc_t rd = mf_rsrc(x + base, (uint32_t)(end > base ? (end - base) * (int64_t)sizeof(InT) : 0));
+#pragma unroll
+        for (int it = 0; it < NL; ++it) {
+            const int v = it < NB ? it * kWave + lane : NB * kWave + (lane & (HX / 8 - 1));
+            const int64_t g = w0 + 8 * v;
+            const uint32_t off = g >= base ? (uint32_t)((g - base) * (int64_t)sizeof(InT)) : kMfOff;
+            constexpr int aux = FIR_MF2_LDAUX;
+            if constexpr (FIR_MF2_TWIN == 2) {
+                raw[it][0] = off, raw[it][1] = off + 1, raw[it][2] = off + 2, raw[it][3] = off + 3;
+            } else if constexpr (I16) {
+                const mf_i32x4 q = it < NB ? __builtin_amdgcn_raw_buffer_load_b128(rd, off, 0, aux)
+                                           : __builtin_amdgcn_raw_buffer_load_b128(rd, off, 0, 0);
+                raw[it][0] = q.x, raw[it][1] = q.y, raw[it][2] = q.z, raw[it][3] = q.w;
+            } else {
+                const i32x2 q = it < NB ? __builtin_amdgcn_raw_buffer_load_b64(rd, off, 0, aux)
+                                        : __builtin_amdgcn_raw_buffer_load_b64(rd, off, 0, 0);
+                raw[it][0] = q.x, raw[it][1] = q.y, raw[it][2] = 0u, raw[it][3] = 0u;
+            }
+        }
+    };
+    load_step(st);
+    {
+        // the entry edge issues the step's store count as dropped stores (descriptor size 0), so
+        // both edges into the loop header have the same operations in flight and hipcc's wait
+        // for the window there is exact (vmcnt(NST)) instead of a drain
+        const __amdgpu_buffer_rsrc_t none = mf_rsrc(y, 0u);
+#pragma unroll
+        for (int k = 0; k < NST; ++k)
+            __builtin_amdgcn_raw_buffer_store_b128(mf_i32x4{0, 0, 0, 0}, none, (uint32_t)(1024 * k + 16 * lane), 0,
+                                                   kMfAuxNt);  // distinct offsets: not merged as redundant
+    }
+
+    for (;;) {
+        int64_t rs, re;
+        const int64_t ss = step_start(st, rs, re);
+        // ---- the window as signed-byte planes: vector v at plane bytes [8 v, 8 v + 8)
+#pragma unroll
+        for (int it = 0; it < NL; ++it) {
+            const int v = it < NB ? it * kWave + lane : NB * kWave + (lane & (HX / 8 - 1));
+            const uint32_t* d = raw[it];
+            if constexpr (I16) {
+                *reinterpret_cast<u2*>(&ph[8 * v]) =
+                    u2{__builtin_amdgcn_perm(d[1], d[0], 0x07050301u), __builtin_amdgcn_perm(d[3], d[2], 0x07050301u)};
+                *reinterpret_cast<u2*>(&pl[8 * v]) = u2{__builtin_amdgcn_perm(d[1], d[0], 0x06040200u) ^ 0x80808080u,
+                                                        __builtin_amdgcn_perm(d[3], d[2], 0x06040200u) ^ 0x80808080u};
+            } else {
+                *reinterpret_cast<u2*>(&pl[8 * v]) = u2{d[0] ^ 0x80808080u, d[1] ^ 0x80808080u};
+            }
+        }
+        // ---- the next step's window goes out now, in flight during this step's math (past the
+        // last step: this one again, so every path into the header has the same loads in flight)
+        const uint32_t nx = st + stride;
+        load_step(nx < nsteps ? nx : st);
+        __builtin_amdgcn_wave_barrier();  // one wave's LDS ops complete in order
+        asm volatile("" ::: "memory");
+
+#pragma unroll
+        for (int q = 0; q < TPS; ++q) {
+            const int64_t ts = ss + (int64_t)q * kMfTile;
+            // outputs of this tile (0: past the row; the twin 3 drops every store)
+            const int m = FIR_MF2_TWIN == 3 ? 0 : (int)max((int64_t)0, min((int64_t)kMfTile, re - ts));
+            mf_i32x16 acc_ll = {}, acc_mid = {}, acc_m2 = {}, acc_hh = {};
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const int i = q * kMfTile + 32 * r + 32 * s + 16 * hf;
+                const mf_i32x4 b_l = *reinterpret_cast<const mf_i32x4*>(&pl[i]);
+                if constexpr (FIR_MF2_TWIN == 1) {  // memory-only twin: keep the B reads, drop the MFMAs
+                    acc_ll[s] += b_l.x ^ a_lo[s].y;
+                    if constexpr (I16) acc_hh[s] += (*reinterpret_cast<const mf_i32x4*>(&ph[i])).z;
+                    continue;
+                }
+                acc_ll = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_lo[s], b_l, acc_ll, 0, 0, 0);
+                acc_mid = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_hi[s], b_l, acc_mid, 0, 0, 0);
+                if constexpr (I16) {
+                    const mf_i32x4 b_h = *reinterpret_cast<const mf_i32x4*>(&ph[i]);
+                    acc_hh = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_hi[s], b_h, acc_hh, 0, 0, 0);
+                    if constexpr (FIR_MF2_ACC3)
+                        acc_mid = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_lo[s], b_h, acc_mid, 0, 0, 0);
+                    else
+                        acc_m2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_lo[s], b_h, acc_m2, 0, 0, 0);
+                }
+            }
+            // combine (mod 2^32), wrap, round; register i is tile output 32 r + (i & 3) + 8 (i >> 2) + 4 hf
+            int32_t o[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                uint32_t a;
+                if constexpr (I16)
+                    a = ((uint32_t)(acc_mid[i] + (FIR_MF2_ACC3 ? 0 : acc_m2[i])) << 8) + (uint32_t)acc_ll[i] +
+                        ((uint32_t)acc_hh[i] << 16) + bias;
+                else
+                    a = ((uint32_t)acc_mid[i] << 8) + (uint32_t)acc_ll[i] + bias;
+                if constexpr (FAST)
+                    o[i] = STAGE == FIR_OUT_U8_SAT ? min(max((int32_t)a, 0), sat_hi) : (int32_t)a >> frac;
+                else
+                    o[i] = round_acc<ACC32>(a, shl, frac);
+            }
+            if constexpr (STAGE == FIR_OUT_U8_SAT) {
+                // 4 outputs per dword g (bytes 32 r + 8 g + 4 hf ..); one permlane32 swap per pair of
+                // dwords gives each lane 16 contiguous bytes: lanes 0-31 at 32 r, 32-63 at 32 r + 16
+                uint32_t w[4];
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4) {
+                    if constexpr (FAST)
+                        w[g4] = ((uint32_t)o[4 * g4] >> frac) | (((uint32_t)o[4 * g4 + 1] >> frac) << 8) |
+                                (((uint32_t)o[4 * g4 + 2] >> frac) << 16) | (((uint32_t)o[4 * g4 + 3] >> frac) << 24);
+                    else
+                        w[g4] = (uint32_t)stage_out32<STAGE>(o[4 * g4]) | ((uint32_t)stage_out32<STAGE>(o[4 * g4 + 1]) << 8) |
+                                ((uint32_t)stage_out32<STAGE>(o[4 * g4 + 2]) << 16) |
+                                ((uint32_t)stage_out32<STAGE>(o[4 * g4 + 3]) << 24);
+                }
+                const auto s02 = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
+                const auto s13 = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
+                __builtin_amdgcn_raw_buffer_store_b128(mf_i32x4{(int)s02[0], (int)s02[1], (int)s13[0], (int)s13[1]},
+                                                       mf_rsrc(y + ts, (uint32_t)m), (uint32_t)(32 * r + 16 * hf), 0, kMfAuxNt);
+            } else if constexpr (OLDS) {
+                // LDS image: block n at dwords [36 n, 36 n + 32), read back as 1 KiB rows
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4)
+                    *reinterpret_cast<u4*>(&ob[36 * r + 8 * g4 + 4 * hf]) =
+                        u4{(uint32_t)o[4 * g4], (uint32_t)o[4 * g4 + 1], (uint32_t)o[4 * g4 + 2], (uint32_t)o[4 * g4 + 3]};
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");
+                const __amdgpu_buffer_rsrc_t rd = mf_rsrc(y + ts, (uint32_t)m * 4u);
+#pragma unroll
+                for (int rho = 0; rho < 4; ++rho) {
+                    const int oo = 256 * rho + 4 * lane;
+                    __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const mf_i32x4*>(&ob[36 * (oo >> 5) + (oo & 31)]), rd,
+                                                           (uint32_t)oo * 4u, 0, kMfAuxNt);
+                }
+            } else {
+                // permlane32 pairs: lanes 0-31 hold outputs 32 r + 0..15, lanes 32-63 32 r + 16..31
+                uint32_t g[4][4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const auto s02 = __builtin_amdgcn_permlane32_swap((uint32_t)o[k], (uint32_t)o[8 + k], false, false);
+                    const auto s13 = __builtin_amdgcn_permlane32_swap((uint32_t)o[4 + k], (uint32_t)o[12 + k], false, false);
+                    g[0][k] = s02[0], g[1][k] = s02[1], g[2][k] = s13[0], g[3][k] = s13[1];
+                }
+                const __amdgpu_buffer_rsrc_t rd = mf_rsrc(y + ts, (uint32_t)m * 4u);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    __builtin_amdgcn_raw_buffer_store_b128(mf_i32x4{(int)g[j][0], (int)g[j][1], (int)g[j][2], (int)g[j][3]}, rd,
+                                                           (uint32_t)(128 * r + 64 * hf + 16 * j), 0, kMfAuxNt);
+            }
+        }
+        st = nx;
+        if (st >= nsteps) break;
+        __builtin_amdgcn_wave_barrier();  // the B reads of this step are done before the next staging
+        asm volatile("" ::: "memory");
+    }
+    (void)ob;
+}
+
+// ---------------------------------------------------------------------------------------
 // Filters longer than kMfMaxTaps (any length): the same Toeplitz product with K = 32 + L/2 + P
 // split into chunks of kMlChunk k-steps.  Per tile and chunk the wave stages the chunk's window
 // (992 + 32 * steps samples) as byte planes in its LDS, then runs the chunk's k-steps with the
@@ -579,6 +838,22 @@ static hipError_t launch_mfma_ks(const void* x, void* y, int64_t rowlen, int64_t
                                  const int32_t* hq, int L, int P, uint32_t bias, bool fast, int frac, int acc_bits,
                                  hipStream_t s) {
     using OutT = typename OutTraits<STAGE>::T;
+    if constexpr (FIR_MF2) {
+        const int64_t spr = (tpr + kMf2Tps - 1) / kMf2Tps, nsteps = ntiles / tpr * spr;
+        const int64_t want2 = (nsteps + kMfWaves - 1) / kMfWaves;
+        const unsigned b2 = (unsigned)(want2 < FIR_MF2_BLOCKS ? want2 : FIR_MF2_BLOCKS);
+        const uint32_t sp = (uint32_t)spr, ns = (uint32_t)nsteps;
+        if (fast)
+            hipLaunchKernelGGL((fir1d_mfma_step_kernel<InT, STAGE, KS, true, true>), dim3(b2), dim3(kBlock), 0, s,
+                               (const InT*)x, (OutT*)y, rowlen, sp, ns, t, P, bias, 0, frac);
+        else if (acc_bits == 32)
+            hipLaunchKernelGGL((fir1d_mfma_step_kernel<InT, STAGE, KS, true, false>), dim3(b2), dim3(kBlock), 0, s,
+                               (const InT*)x, (OutT*)y, rowlen, sp, ns, t, P, bias, 0, frac);
+        else
+            hipLaunchKernelGGL((fir1d_mfma_step_kernel<InT, STAGE, KS, false, false>), dim3(b2), dim3(kBlock), 0, s,
+                               (const InT*)x, (OutT*)y, rowlen, sp, ns, t, P, bias, 32 - acc_bits, frac);
+        return hipGetLastError();
+    }
     const int64_t want = (ntiles + kMfWaves - 1) / kMfWaves;
     unsigned blocks = (unsigned)(want < kMfMaxBlocks ? want : kMfMaxBlocks);
     const mf_i32x4* fr = nullptr;
