@@ -1,5 +1,5 @@
 """Dev driver for profiling one long-filter configuration: 2^28 samples, `reps` back-to-back
-device launches.  Usage: python tools/long_taps_one.py <taps> <i16|u8> [reps]"""
+device launches.  Usage: python tools/long_taps_one.py <taps> <i16|i16u8|u8> [reps]"""
 import sys
 from pathlib import Path
 
@@ -22,6 +22,10 @@ def main():
         x = torch.from_numpy(rng.integers(-32768, 32768, n, dtype=np.int16)).to(dev)
         y = torch.empty(n, dtype=torch.int32, device=dev)
         st = fir_hip.OUT_I32
+    elif kind == "i16u8":
+        x = torch.from_numpy(rng.integers(-32768, 32768, (n // 4096, 4096), dtype=np.int16)).to(dev)
+        y = torch.empty(x.shape, dtype=torch.uint8, device=dev)
+        st = fir_hip.OUT_U8_SAT
     else:
         x = torch.from_numpy(rng.integers(0, 256, (n // 4096, 4096), dtype=np.uint8)).to(dev)
         y = torch.empty(x.shape, dtype=torch.uint8, device=dev)

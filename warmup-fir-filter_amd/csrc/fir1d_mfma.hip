@@ -406,8 +406,8 @@ __global__ __launch_bounds__(kBlock, FIR_MFMA_MINB) void fir1d_mfma_kernel(const
 #ifndef FIR_MF2_MINB                 // waves per SIMD the register allocation must allow
 #define FIR_MF2_MINB 4
 #endif
-#ifndef FIR_MF2_BLOCKS               // grid-stride blocks (4 waves each)
-#define FIR_MF2_BLOCKS 1024
+#ifndef FIR_MF2_BLOCKS               // grid-stride blocks (4 waves each; 2048 = two resident rounds)
+#define FIR_MF2_BLOCKS 2048
 #endif
 #ifndef FIR_MF2_OLDS                 // int32 outputs through LDS as 1 KiB rows (0: permlane32 pairs)
 #define FIR_MF2_OLDS 1
@@ -415,13 +415,42 @@ __global__ __launch_bounds__(kBlock, FIR_MFMA_MINB) void fir1d_mfma_kernel(const
 #ifndef FIR_MF2_ACC3                 // int16: one accumulator for both cross products
 #define FIR_MF2_ACC3 1
 #endif
-#ifndef FIR_MF2_LDAUX                // cache policy of the body loads (2 = non-temporal; A/B)
-#define FIR_MF2_LDAUX 0
-#endif
+#ifndef FIR_MF2_LDAUX                // cache policy of the body loads: -1 = non-temporal for int16 input
+#define FIR_MF2_LDAUX -1             // (i16 -> u8 150-155 -> 141-146 us), default for u8 input (whose
+#endif                               // 256 MiB planes partly stay in the Infinity Cache between calls)
 #ifndef FIR_MF2_TWIN                 // A/B twins: 1 = no MFMAs, 2 = no window loads, 3 = no stores
 #define FIR_MF2_TWIN 0
 #endif
 constexpr int kMf2Tps = FIR_MF2_TPS;
+
+// (a << S) + b (v_lshl_add_u32; pure VALU, no hazards)
+template <int S>
+__device__ __forceinline__ uint32_t mf_lshl_add(uint32_t a, uint32_t b) {
+    uint32_t d;
+    asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "n"(S), "v"(b));
+    return d;
+}
+// clamp(a, 0, hi) for hi > 0 (v_med3_i32)
+__device__ __forceinline__ uint32_t mf_med3_0(uint32_t a, int32_t hi) {
+    uint32_t d;
+    asm("v_med3_i32 %0, %1, 0, %2" : "=v"(d) : "v"(a), "s"(hi));
+    return d;
+}
+// byte B of w replaced by (c >> f) (< 256), the other bytes kept: one SDWA shift
+template <int B>
+__device__ __forceinline__ uint32_t mf_shr_byte(uint32_t w, uint32_t c, int f) {
+    static_assert(B >= 1 && B <= 3, "byte");
+    if constexpr (B == 1)
+        asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+            : "+v"(w) : "s"(f), "v"(c));
+    else if constexpr (B == 2)
+        asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+            : "+v"(w) : "s"(f), "v"(c));
+    else
+        asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+            : "+v"(w) : "s"(f), "v"(c));
+    return w;
+}
 
 template <typename InT, int STAGE, int KS, bool ACC32, bool FAST>
 __global__ __launch_bounds__(kBlock, FIR_MF2_MINB) void fir1d_mfma_step_kernel(const InT* __restrict__ x,
@@ -491,7 +520,7 @@ __global__ __launch_bounds__(kBlock, FIR_MF2_MINB) void fir1d_mfma_step_kernel(c
             const int v = it < NB ? it * kWave + lane : NB * kWave + (lane & (HX / 8 - 1));
             const int64_t g = w0 + 8 * v;
             const uint32_t off = g >= base ? (uint32_t)((g - base) * (int64_t)sizeof(InT)) : kMfOff;
-            constexpr int aux = FIR_MF2_LDAUX;
+            constexpr int aux = FIR_MF2_LDAUX >= 0 ? FIR_MF2_LDAUX : (I16 ? kMfAuxNt : 0);
             if constexpr (FIR_MF2_TWIN == 2) {
                 raw[it][0] = off, raw[it][1] = off + 1, raw[it][2] = off + 2, raw[it][3] = off + 3;
             } else if constexpr (I16) {
@@ -568,17 +597,22 @@ __global__ __launch_bounds__(kBlock, FIR_MF2_MINB) void fir1d_mfma_step_kernel(c
                 }
             }
             // combine (mod 2^32), wrap, round; register i is tile output 32 r + (i & 3) + 8 (i >> 2) + 4 hf
+            // (the accumulators are read by compiler-visible code only: hipcc's hazard recognizer
+            // does not pad an inline-asm read of an MFMA result, which then reads stale values)
             int32_t o[16];
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 uint32_t a;
-                if constexpr (I16)
-                    a = ((uint32_t)(acc_mid[i] + (FIR_MF2_ACC3 ? 0 : acc_m2[i])) << 8) + (uint32_t)acc_ll[i] +
-                        ((uint32_t)acc_hh[i] << 16) + bias;
-                else
-                    a = ((uint32_t)acc_mid[i] << 8) + (uint32_t)acc_ll[i] + bias;
+                if constexpr (I16) {
+                    const uint32_t mid = FIR_MF2_ACC3 ? (uint32_t)acc_mid[i] : (uint32_t)(acc_mid[i] + acc_m2[i]);
+                    // 3 VALU: (hh << 8) + mid and ll + bias by hipcc (which pads the MFMA reads), the
+                    // outer (t << 8) + u as asm (hipcc would re-associate it into 2 shifts + add3)
+                    a = mf_lshl_add<8>(((uint32_t)acc_hh[i] << 8) + mid, (uint32_t)acc_ll[i] + bias);
+                } else {
+                    a = (((uint32_t)acc_mid[i] << 8) + (uint32_t)acc_ll[i]) + bias;
+                }
                 if constexpr (FAST)
-                    o[i] = STAGE == FIR_OUT_U8_SAT ? min(max((int32_t)a, 0), sat_hi) : (int32_t)a >> frac;
+                    o[i] = STAGE == FIR_OUT_U8_SAT ? (int32_t)mf_med3_0(a, sat_hi) : (int32_t)a >> frac;
                 else
                     o[i] = round_acc<ACC32>(a, shl, frac);
             }
@@ -588,9 +622,10 @@ __global__ __launch_bounds__(kBlock, FIR_MF2_MINB) void fir1d_mfma_step_kernel(c
                 uint32_t w[4];
 #pragma unroll
                 for (int g4 = 0; g4 < 4; ++g4) {
-                    if constexpr (FAST)
-                        w[g4] = ((uint32_t)o[4 * g4] >> frac) | (((uint32_t)o[4 * g4 + 1] >> frac) << 8) |
-                                (((uint32_t)o[4 * g4 + 2] >> frac) << 16) | (((uint32_t)o[4 * g4 + 3] >> frac) << 24);
+                    if constexpr (FAST)  // clamped sums c in [0, 2^(frac+8)): the byte is c >> frac
+                        w[g4] = mf_shr_byte<3>(mf_shr_byte<2>(mf_shr_byte<1>((uint32_t)o[4 * g4] >> frac, (uint32_t)o[4 * g4 + 1], frac),
+                                                              (uint32_t)o[4 * g4 + 2], frac),
+                                               (uint32_t)o[4 * g4 + 3], frac);
                     else
                         w[g4] = (uint32_t)stage_out32<STAGE>(o[4 * g4]) | ((uint32_t)stage_out32<STAGE>(o[4 * g4 + 1]) << 8) |
                                 ((uint32_t)stage_out32<STAGE>(o[4 * g4 + 2]) << 16) |
