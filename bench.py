@@ -72,7 +72,7 @@ SELF_HALO = os.environ.get("FIR_SELF_HALO") == "1"
 HALO_PREF = os.environ.get("FIR_HALO", "xgmi")
 KERNELS = {"fir1d_i16": "fir1d_reg_kernel", "cplx_i16": "fir1d_reg_kernel", "fir2d_u8": "fir2d_pk16_strip_kernel",
            "fir1d_u8": "fir1d_reg_kernel", "ideal_u8": "fir1d_ideal_kernel", "bank_u8": "fir1d_reg_kernel",
-           "restore_u8": "restore_map_kernel", "metrics_u8": "metrics_pass1+2"}
+           "restore_u8": "restore_map_kernel", "metrics_u8": "metrics_blocks+chain"}
 NUMPY_ONLY = ("restore_u8", "metrics_u8")  # no C oracle leg: the NumPy restatement is the CPU baseline
 
 
@@ -176,11 +176,11 @@ class Workload:
             self.x_host = rng.uniform(-64.0, 320.0, self.n)  # ideal-output-like f64
             self.fixed_host = np.clip(np.rint(self.x_host) + rng.integers(-3, 4, self.n), 0, 255).astype(np.uint8)
             self.fixed = torch.from_numpy(self.fixed_host).to(dev)
-            self.work = torch.empty(int(fir_hip.lib().fir_metrics_work_bytes()), dtype=torch.uint8, device=dev)
+            self.work = torch.empty(int(fir_hip.lib().fir_metrics_work_bytes(self.n)), dtype=torch.uint8, device=dev)
             self.units = self.n
             self.unit = "Gsamples/s"
             self.bytes_per_unit = 8 + 1
-            self.dtype = "f64 (Neumaier-compensated sums; counts and max exact)"
+            self.dtype = "f64 (sums in NumPy's order, bit-exact; counts and max exact)"
             self.config = {"workload": "compare_metrics_f64_u8", "samples_per_gpu": self.n,
                            "parallelism": "single GPU (replicas when N > 1)"}
         else:
@@ -368,14 +368,11 @@ class Workload:
         return n
 
     def matches(self, ref) -> bool:
-        """Full-output parity; the metrics' float sums to 1e-12 relative (counts, max exact)."""
+        """Full-output parity: every output, and every report metric, bit for bit."""
         got = self.y.cpu().numpy()
         if self.name != "metrics_u8":
             return bool(np.array_equal(got, ref))
-        m = fir_hip.metrics_from_sums(got, self.n)
-        exact = ("num_samples", "max_abs_err", "sat_low_ratio", "sat_high_ratio", "sat_ratio", "clip_needed_ratio")
-        return all(m[k] == ref[k] for k in exact) and all(
-            abs(m[k] - ref[k]) <= 1e-12 * abs(ref[k]) + 1e-15 for k in ("mae", "rmse", "mean_err"))
+        return fir_hip.metrics_from_sums(got, self.n) == ref
 
 
 def main() -> int:

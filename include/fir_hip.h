@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define FIR_HIP_ABI_VERSION 2
+#define FIR_HIP_ABI_VERSION 3
 /* Tap counts: any length up to FIR_MAX_TAPS (1-D taps; 2-D tap_rows * tap_cols), like the
  * reference's Python loop (fir_1d_fixed_ref.py:83-107, fir_1d_ref.py:49-63).  Sums are exact in
  * 64 bits: mod 2^64 for acc_bits < 64; with acc_bits >= 64 (no wrap) sum|hq| * max|x| must stay
@@ -162,9 +162,11 @@ int fir1d_ideal_rows_dev(const uint8_t* x_dev, int64_t rows, int64_t width, cons
 /* ---- fixed-vs-ideal comparison metrics -----------------------------
  * One pass over `n` samples of ideal (float64) and fixed (uint8) outputs.  out[9] =
  * {max|d|, sum|d|, sum d^2, sum d, #(fixed==0), #(fixed==255), #(ideal<0 or >255), n, 0}
- * with d = fixed - ideal; the report ratios are these over n.  Float64 sums are
- * compensated and reduced in a fixed order (deterministic); counts and max are exact. */
-int64_t fir_metrics_work_bytes(void);
+ * with d = fixed - ideal; the report ratios are these over n.  The float64 sums are added in
+ * NumPy's order (8192-sample blocks summed pairwise, block sums in order), so they equal the
+ * reference's np.mean values bit for bit; counts and max are exact.  `work_dev` of the _dev
+ * form holds at least fir_metrics_work_bytes(n) bytes (ABI 3: the size depends on n). */
+int64_t fir_metrics_work_bytes(int64_t n);
 int fir_compare_metrics(const double* ideal, const uint8_t* fixed, int64_t n, double* out, int device);
 int fir_compare_metrics_dev(const double* ideal_dev, const uint8_t* fixed_dev, int64_t n, double* out_dev,
                             void* work_dev, void* stream);

@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.fir_abi_version() == fir_hip.ABI_VERSION == 2
+    assert lib.fir_abi_version() == fir_hip.ABI_VERSION == 3
 
 
 def test_invalid_arguments_are_rejected_without_device(lib):
@@ -78,6 +78,10 @@ def test_sharded_and_restore_argument_checks_without_device(lib):
     assert lib.fir_restore_u8_dev(None, 0, 1, None, None, None) == 0
     assert lib.fir_restore_u8_dev(None, 8, 1, None, None, None) == 1
     assert lib.fir_restore_work_bytes() >= 256
+    # the metrics work buffer: fixed part + 3 float64 sums per 8192-sample block (NumPy's order)
+    w0 = lib.fir_metrics_work_bytes(0)
+    assert w0 > 0 and lib.fir_metrics_work_bytes(1) == w0 + 24 == lib.fir_metrics_work_bytes(8192)
+    assert lib.fir_metrics_work_bytes(1 << 28) == w0 + 24 * (1 << 15)
 
 
 def test_ipc_argument_checks_without_device(lib):

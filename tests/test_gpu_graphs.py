@@ -31,7 +31,7 @@ def test_captured_pipeline_replays_bit_exact():
     rest = torch.empty((H, W), dtype=torch.uint8, device=DEV)
     y16 = torch.empty(N16, dtype=torch.int32, device=DEV)
     y2d = torch.empty((H, W), dtype=torch.uint8, device=DEV)
-    mwork = torch.empty(int(fir_hip.lib().fir_metrics_work_bytes()), dtype=torch.uint8, device=DEV)
+    mwork = torch.empty(int(fir_hip.lib().fir_metrics_work_bytes(H * W)), dtype=torch.uint8, device=DEV)
     rwork = torch.empty(int(fir_hip.lib().fir_restore_work_bytes()), dtype=torch.uint8, device=DEV)
     taps16 = torch_ops.Taps(SHARPEN5)
 
@@ -67,10 +67,7 @@ def test_captured_pipeline_replays_bit_exact():
         assert np.array_equal(ideal.cpu().numpy().view(np.uint64), ideal_ref.view(np.uint64))
         m = fir_hip.metrics_from_sums(sums.cpu().numpy(), H * W)
         ref = fo.compute_metrics(ideal_ref, co.fir1d_rows(xh, BANK3[3], 12, 32, 0))
-        for k in ("max_abs_err", "sat_low_ratio", "sat_high_ratio", "clip_needed_ratio"):
-            assert m[k] == ref[k], (seed, k)
-        for k in ("mae", "rmse", "mean_err"):
-            assert abs(m[k] - ref[k]) <= 1e-12 * abs(ref[k]) + 1e-15, (seed, k)
+        assert m == ref, seed  # every report metric bit for bit (NumPy's summation order)
         assert np.array_equal(rest.cpu().numpy(), fo.to_u8_normalized(ideal_ref))
         assert np.array_equal(y16.cpu().numpy(), fo.fir1d_i16_i32(x16h, SHARPEN5))
         assert np.array_equal(y2d.cpu().numpy(), co.fir2d(xh, np.asarray(K2D), 12, 32, 0))

@@ -645,7 +645,7 @@ int fir1d_ideal_rows_dev(const uint8_t* x_dev, int64_t rows, int64_t width, cons
     }
 }
 
-int64_t fir_metrics_work_bytes(void) { return (int64_t)fir::metrics_work_bytes(); }
+int64_t fir_metrics_work_bytes(int64_t n) { return (int64_t)fir::metrics_work_bytes(n); }
 
 int fir_compare_metrics(const double* ideal, const uint8_t* fixed, int64_t n, double* out, int device) {
     try {
@@ -658,7 +658,7 @@ int fir_compare_metrics(const double* ideal, const uint8_t* fixed, int64_t n, do
         if ((rc = init_locked(st, device))) return rc;
         const size_t ib = (size_t)n * 8, fb = (size_t)n;
         const size_t fo = (ib + 255) / 256 * 256;
-        if ((rc = ensure(st->in, fo + fb + 1)) || (rc = ensure(st->out, fir::metrics_work_bytes() + 256))) return rc;
+        if ((rc = ensure(st->in, fo + fb + 1)) || (rc = ensure(st->out, fir::metrics_work_bytes(n) + 256))) return rc;
         char* din = (char*)st->in.ptr;
         if (n > 0) {
             HIP_TRY(hipMemcpyAsync(din, ideal, ib, hipMemcpyHostToDevice, st->stream));

@@ -67,8 +67,8 @@ int launch_fir2d(const uint8_t* x, int64_t frames, int64_t height, int64_t width
 int launch_fir1d_ideal(const uint8_t* x, int64_t rows, int64_t width, const double* h, int L, double* y,
                        hipStream_t stream, std::string* err);
 
-// Fixed-vs-ideal comparison metrics (one pass); `work` >= metrics_work_bytes().
-size_t metrics_work_bytes();
+// Fixed-vs-ideal comparison metrics (one pass); `work` >= metrics_work_bytes(n).
+size_t metrics_work_bytes(int64_t n);
 int launch_metrics(const double* ideal, const uint8_t* fixed, int64_t n, double* out, void* work,
                    hipStream_t stream, std::string* err);
 

@@ -1,14 +1,31 @@
-// metrics.hip — fixed-vs-ideal comparison metrics in one pass over HBM.
+// metrics.hip — fixed-vs-ideal comparison metrics in one pass over HBM,
+// bit for bit the reference's NumPy values.
 //
 // Restates fir_1d/sim/vector/gen_3tap_compare_report.py:67-112 (_compute_metrics): with
 // d = fixed - ideal (float64), it needs max|d|, sum|d|, sum d^2, sum d, #(fixed == 0),
-// #(fixed == 255) and #(ideal < 0 or ideal > 255).  The reference takes each from a
-// separate NumPy reduction (seven passes over 9 bytes/sample); here one kernel reads
-// each sample once.  Sums are float64: plain per 8-sample tile, Neumaier-compensated across
-// tiles per thread, then a fixed reduction order (per-block tree, then one block over the
-// partials), so results are deterministic run to run; they differ from NumPy's pairwise
-// summation only in the last bits (tests use a 1e-12 relative tolerance).  Counts and
-// max|d| are exact.
+// #(fixed == 255) and #(ideal < 0 or ideal > 255).  The reference takes each from a separate
+// NumPy reduction (seven passes over 9 bytes/sample); here one kernel reads each sample once.
+// Counts and max|d| do not depend on the order of the reduction.  The three float64 sums do,
+// and they follow NumPy's own order exactly (pinned against np.sum / np.mean of NumPy 2.2 on
+// random arrays and image shapes: tests/test_metrics_order.py): a contiguous float64 array is
+// summed in blocks of 8192 elements (the ufunc buffer), the block sums added in order to 0.0,
+// each block by pairwise_sum: n < 8 a plain loop from 0.0; n <= 128 eight strided accumulators
+// r[j] (element j, then += j + 8, j + 16, ...) combined as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7))
+// with the elements past the last multiple of 8 added in order; larger n split at
+// n2 = floor(n/2) rounded down to a multiple of 8, sum = pw(left) + pw(right).
+//
+//   pass 1 (metrics_blocks): one wave per full 8192-sample block, grid-stride; a full block is
+//     a balanced tree of 64 leaves of 128: 4 rounds of 16 leaves, 4 lanes a leaf (2 accumulators
+//     each, 16 steps of 16-byte loads), the leaf and round trees by lane shuffles (IEEE addition
+//     is commutative, so a lane adding its partner's value to its own matches either order);
+//     counts and max per workgroup; metrics_ragged: the ragged last block by the general
+//     recursion (leaves enumerated, summed one per thread, recombined in post-order).
+//   the chain: waves 0-2 of one workgroup add the block sums of |d|, d^2 and d in order (a
+//     dependent float64 chain).  The full blocks are split
+//     into parts of one launch each, shrinking toward the end (last 512 blocks), and the chain
+//     over part k-1 runs as an extra workgroup of the launch that streams part k (2^28 samples:
+//     the chain's 168 us are hidden but for the last part's); metrics_final adds the last part
+//     (and the ragged block) and reduces the counts and max.
 #include <string>
 
 #include "fir_common.h"
@@ -16,178 +33,396 @@
 
 namespace fir {
 
-// 2048 blocks (8192 waves, 32 per CU) over 4096: 359 -> 356 / 369 -> 362 us in two same-process
-// A/Bs; 1024 blocks, 8 or 4 loads per tile, the next tile's loads issued before the arithmetic
-// (+3-5 %), and the fixed bytes as whole rows through LDS gained nothing
-// (profiles/r02/ab_restore_metrics.txt).  FIR_METRIC_*: A/B builds only.
 #ifndef FIR_METRIC_BLOCKS
 #define FIR_METRIC_BLOCKS 2048
 #endif
-#ifndef FIR_METRIC_LOADS
-#define FIR_METRIC_LOADS 16
-#endif
-
 constexpr int kMetricBlocks = FIR_METRIC_BLOCKS;
+#ifndef FIR_METRIC_MINB  // waves per SIMD the block kernel's registers must allow
+#define FIR_METRIC_MINB 4
+#endif
+constexpr int kPwBlock = 8192;   // NumPy's ufunc buffer (NPY_BUFSIZE elements)
+constexpr int kPwLeaf = 128;     // pairwise_sum's PW_BLOCKSIZE
+constexpr int kPwMaxLeaves = 128;  // leaves of a block shorter than 8192 (each >= 64 samples)
 
-struct Part {
-    double sabs, cabs, ssq, csq, sd, cd, mx;
+struct Cnt {
+    double mx;
     unsigned long long lo, hi, clip;
 };
 
-__device__ __forceinline__ void neu_add(double& s, double& c, double v) {
-    const double t = __dadd_rn(s, v);
-    c = __dadd_rn(c, fabs(s) >= fabs(v) ? __dadd_rn(__dsub_rn(s, t), v) : __dadd_rn(__dsub_rn(v, t), s));
-    s = t;
-}
-
-__device__ void reduce_block(Part& p) {
-    __shared__ Part sh[kBlock];
-    sh[threadIdx.x] = p;
-    __syncthreads();
-    for (int w = kBlock / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w) {
-            Part& a = sh[threadIdx.x];
-            const Part& b = sh[threadIdx.x + w];
-            neu_add(a.sabs, a.cabs, b.sabs);
-            a.cabs = __dadd_rn(a.cabs, b.cabs);
-            neu_add(a.ssq, a.csq, b.ssq);
-            a.csq = __dadd_rn(a.csq, b.csq);
-            neu_add(a.sd, a.cd, b.sd);
-            a.cd = __dadd_rn(a.cd, b.cd);
-            a.mx = fmax(a.mx, b.mx);
-            a.lo += b.lo;
-            a.hi += b.hi;
-            a.clip += b.clip;
-        }
-        __syncthreads();
-    }
-    p = sh[0];
-}
-
-// One sample's terms: |d| and d^2 and d into the tile partials, max and the three counts.
-__device__ __forceinline__ void metrics_term(double id, uint32_t fx, double& sabs, double& ssq, double& sd,
-                                             double& mx, uint32_t& lo, uint32_t& hi, uint32_t& clip) {
+// One sample: d = fixed - ideal, its |d|, d^2, d, and the max / counts.
+struct Term {
+    double a, q, d;
+};
+__device__ __forceinline__ Term metrics_term(double id, uint32_t fx, double& mx, uint32_t& lo, uint32_t& hi,
+                                             uint32_t& clip) {
     const double d = __dsub_rn((double)fx, id);
     const double ad = fabs(d);
-    sabs = __dadd_rn(sabs, ad);
-    ssq = __dadd_rn(ssq, __dmul_rn(d, d));
-    sd = __dadd_rn(sd, d);
     mx = fmax(mx, ad);
     lo += fx == 0;
     hi += fx == 255;
     clip += (id < 0.0) | (id > 255.0);
+    return Term{ad, __dmul_rn(d, d), d};
+}
+__device__ __forceinline__ void tadd(Term& s, const Term& t) {
+    s.a = __dadd_rn(s.a, t.a);
+    s.q = __dadd_rn(s.q, t.q);
+    s.d = __dadd_rn(s.d, t.d);
+}
+__device__ __forceinline__ Term tadd2(const Term& s, const Term& t) {
+    return Term{__dadd_rn(s.a, t.a), __dadd_rn(s.q, t.q), __dadd_rn(s.d, t.d)};
+}
+__device__ __forceinline__ Term tshfl_xor(const Term& s, int m) {
+    return Term{__shfl_xor(s.a, m), __shfl_xor(s.q, m), __shfl_xor(s.d, m)};
 }
 
-// VEC (ideal 16-byte and fixed 2-byte aligned): a wave reads tiles of kMetricTile samples as
-// whole 1 KiB f64 rows plus 128 B u8 rows, 16 non-temporal f64 loads in flight per lane
-// (the read-stream A/B, tools/microbench/read_micro.hip); each lane sums its 32 samples of
-// a tile plainly and adds the tile partials into its Neumaier-compensated accumulators
-// (a compensated add per sample made the kernel latency-bound).  The ragged tail and
-// unaligned inputs take the per-sample grid-stride loop.
-constexpr int kMetricLoads = FIR_METRIC_LOADS;
-constexpr int kMetricTile = kMetricLoads * kWave * 2;
+// pairwise_sum of one leaf (n <= 128) of samples [o, o + n), as NumPy's loop does it
+__device__ Term pw_leaf(const double* ideal, const uint8_t* fixed, int64_t o, int n, double& mx, uint32_t& lo,
+                        uint32_t& hi, uint32_t& clip) {
+    if (n < 8) {
+        Term res{0.0, 0.0, 0.0};
+        for (int i = 0; i < n; ++i) tadd(res, metrics_term(ideal[o + i], fixed[o + i], mx, lo, hi, clip));
+        return res;
+    }
+    Term r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = metrics_term(ideal[o + j], fixed[o + j], mx, lo, hi, clip);
+    int i = 8;
+    for (; i < n - (n % 8); i += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) tadd(r[j], metrics_term(ideal[o + i + j], fixed[o + i + j], mx, lo, hi, clip));
+    }
+    Term res = tadd2(tadd2(tadd2(r[0], r[1]), tadd2(r[2], r[3])), tadd2(tadd2(r[4], r[5]), tadd2(r[6], r[7])));
+    for (; i < n; ++i) tadd(res, metrics_term(ideal[o + i], fixed[o + i], mx, lo, hi, clip));
+    return res;
+}
 
+// counts and max of a workgroup into *dst (wave shuffles, then the 4 wave results)
+__device__ void block_counts(Cnt c, Cnt* dst) {
+    __shared__ Cnt red[kBlock / kWave];
+#pragma unroll
+    for (int m = 1; m < kWave; m <<= 1) {
+        c.mx = fmax(c.mx, __shfl_xor(c.mx, m));
+        c.lo += __shfl_xor(c.lo, m);
+        c.hi += __shfl_xor(c.hi, m);
+        c.clip += __shfl_xor(c.clip, m);
+    }
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        Cnt a = red[0];
+        for (int w = 1; w < kBlock / kWave; ++w)
+            a.mx = fmax(a.mx, red[w].mx), a.lo += red[w].lo, a.hi += red[w].hi, a.clip += red[w].clip;
+        *dst = a;
+    }
+}
+
+// The running sums state[0..2] += block sums [lo, hi) of |d|, d^2, d, in order (from 0.0 when
+// lo == 0).  Waves 0-2 take one array each: 64 block sums per coalesced load (8 such loads in
+// flight), moved to the running sum one by one with v_readlane (SGPR operands, independent of
+// the sum), so the dependent chain is one float64 add per 8192 samples.  No barrier inside.
+constexpr int kChainDepth = 8;
+__device__ double pw_lane(double v, int j) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, j);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), j);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ void chain_range(const double* __restrict__ bsum, int64_t nb, int64_t lo, int64_t hi, double* state,
+                            double* out = nullptr) {
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
+    if (wv >= 3) return;
+    const double* src = bsum + (int64_t)wv * nb;
+    double s = lo == 0 ? 0.0 : state[wv];
+    // groups of kChainDepth batches of 64: the next group's loads go out before this group's adds
+    // (one batch in flight took ~1.5 us of load latency per 64 adds)
+    constexpr int D = kChainDepth;
+    auto fetch = [&](int64_t c0, double (&q)[D]) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) q[d] = c0 + d * kWave + lane < hi ? src[c0 + d * kWave + lane] : 0.0;
+    };
+    double q[D], r[D];
+    fetch(lo, q);
+    for (int64_t g0 = lo; g0 < hi; g0 += D * kWave) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) r[d] = q[d];
+        fetch(g0 + D * kWave, q);
+        if (hi - g0 >= D * kWave) {
+#pragma unroll
+            for (int d = 0; d < D; ++d)
+#pragma unroll
+                for (int j = 0; j < kWave; ++j) s = __dadd_rn(s, pw_lane(r[d], j));
+        } else {
+            const int len = (int)(hi - g0);
+            for (int e = 0; e < len; ++e) {
+                double v = r[0];
+#pragma unroll
+                for (int d = 1; d < D; ++d) v = e / kWave == d ? r[d] : v;
+                s = __dadd_rn(s, pw_lane(v, e % kWave));
+            }
+        }
+    }
+    if (lane == 0) state[wv] = s;
+    if (out && lane == 0) out[1 + wv] = s;
+}
+
+// One WAVE per full block (no workgroup barrier: waves stream independently), grid-stride over
+// the blocks; a block = 8 rounds of 8 leaves (1024 samples, one balanced subtree each).  A round
+// is loaded as contiguous 1 KiB rows (leaf i by load i: 16 bytes per lane) plus one 16-byte load
+// of its fixed bytes, staged in the wave's LDS and read back transposed: lane (leaf k, j) takes
+// the 16 terms of accumulator r[j] (samples 8 s + j) in order.  (Reading those stride-8 samples
+// straight from HBM touches 16 half lines per load and ran at 3.3 TB/s.)
+constexpr int kMetRow = 1024 + 64;                      // LDS bytes per leaf row (+64: conflict-free reads)
+constexpr int kMetWaveLds = 8 * kMetRow + 1024;         // + the round's 1 KiB of fixed bytes
 template <bool VEC>
-__global__ __launch_bounds__(kBlock) void metrics_pass1(const double* __restrict__ ideal,
-                                                        const uint8_t* __restrict__ fixed, int64_t n,
-                                                        Part* __restrict__ parts) {
+__global__ __launch_bounds__(kBlock, FIR_METRIC_MINB) void metrics_blocks(const double* __restrict__ ideal,
+                                                                         const uint8_t* __restrict__ fixed,
+                                                                         double* __restrict__ bsum, int64_t nb,
+                                                                         int64_t b_lo, int64_t b_hi, int64_t c_lo,
+                                                                         int64_t c_hi, double* __restrict__ state,
+                                                                         Cnt* __restrict__ parts) {
     typedef double d2 __attribute__((ext_vector_type(2)));
-    Part p{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock / kWave * kMetWaveLds];
+    const bool chain = c_hi > c_lo;
+    if (chain && blockIdx.x == 0) {  // dispatched first: the chain starts with the part
+        chain_range(bsum, nb, c_lo, c_hi, state);
+        return;
+    }
+    const int wg = blockIdx.x - (chain ? 1 : 0);
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x >> 6;
+    const int k = lane >> 3, j = lane & 7;  // leaf of the round, accumulator
+    uint8_t* wl = smem + wv * kMetWaveLds;
+    const int64_t nwaves = (int64_t)(gridDim.x - (chain ? 1 : 0)) * (kBlock / kWave);
     double mx = 0.0;
     uint32_t lo = 0, hi = 0, clip = 0;
-    int64_t start = 0;
-    if constexpr (VEC) {
-        const int lane = threadIdx.x & (kWave - 1);
-        const int64_t ntile = n / kMetricTile;
-        const int64_t nwaves = (int64_t)gridDim.x * (kBlock / kWave);
-        auto load_tile = [&](int64_t t, d2 (&a)[kMetricLoads], uint32_t (&f)[kMetricLoads]) {
-            const d2* pi = reinterpret_cast<const d2*>(ideal + t * kMetricTile);
-            const uint16_t* pf = reinterpret_cast<const uint16_t*>(fixed + t * kMetricTile);
+
+    for (int64_t b = b_lo + (int64_t)wg * (kBlock / kWave) + wv; b < b_hi; b += nwaves) {
+        Term st[4];  // pairwise stack of round sums: ((R0+R1)+(R2+R3))+((R4+R5)+(R6+R7))
+#pragma unroll 1
+        for (int rd = 0; rd < 8; ++rd) {
+            const int64_t base = b * kPwBlock + rd * 1024;
+            d2 v[8];
+            u4 fx;
+            if constexpr (VEC) {
 #pragma unroll
-            for (int i = 0; i < kMetricLoads; ++i) {
-                a[i] = __builtin_nontemporal_load(pi + i * kWave + lane);
-                f[i] = __builtin_nontemporal_load(pf + i * kWave + lane);
-            }
-        };
-        auto tile_sums = [&](const d2 (&a)[kMetricLoads], const uint32_t (&f)[kMetricLoads]) {
-            double sabs = 0.0, ssq = 0.0, sd = 0.0;
+                for (int i = 0; i < 8; ++i)
+                    v[i] = __builtin_nontemporal_load(reinterpret_cast<const d2*>(ideal + base + 128 * i) + lane);
+                fx = *reinterpret_cast<const u4*>(fixed + base + 16 * lane);
+            } else {
 #pragma unroll
-            for (int i = 0; i < kMetricLoads; ++i) {
-                metrics_term(a[i].x, f[i] & 0xFFu, sabs, ssq, sd, mx, lo, hi, clip);
-                metrics_term(a[i].y, f[i] >> 8, sabs, ssq, sd, mx, lo, hi, clip);
+                for (int i = 0; i < 8; ++i) v[i] = d2{ideal[base + 128 * i + 2 * lane], ideal[base + 128 * i + 2 * lane + 1]};
+                uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int e = 0; e < 16; ++e) w[e / 4] |= (uint32_t)fixed[base + 16 * lane + e] << (8 * (e % 4));
+                fx = u4{w[0], w[1], w[2], w[3]};
             }
-            neu_add(p.sabs, p.cabs, sabs);
-            neu_add(p.ssq, p.csq, ssq);
-            neu_add(p.sd, p.cd, sd);
-        };
-        for (int64_t t = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6); t < ntile; t += nwaves) {
-            d2 a[kMetricLoads];
-            uint32_t f[kMetricLoads];
-            load_tile(t, a, f);
-            tile_sums(a, f);
+            __builtin_amdgcn_wave_barrier();  // the previous round's reads are done (one wave: in order)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) *reinterpret_cast<d2*>(wl + i * kMetRow + 16 * lane) = v[i];
+            *reinterpret_cast<u4*>(wl + 8 * kMetRow + 16 * lane) = fx;
+            __builtin_amdgcn_wave_barrier();
+            const uint8_t* row = wl + k * kMetRow + 8 * j;
+            const uint8_t* frow = wl + 8 * kMetRow + 128 * k + j;
+            Term r{0.0, 0.0, 0.0};
+#pragma unroll
+            for (int s = 0; s < 16; ++s) {
+                double id = *reinterpret_cast<const double*>(row + 64 * s);
+                uint32_t f = frow[8 * s];
+                asm volatile("" : "+v"(id), "+v"(f), "+v"(mx), "+v"(lo), "+v"(hi), "+v"(clip));
+                const Term t = metrics_term(id, f, mx, lo, hi, clip);
+                if (s == 0) r = t;
+                else tadd(r, t);
+            }
+            // leaf: ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the round's 8 leaves pairwise
+            Term t = r;
+#pragma unroll
+            for (int m = 1; m < kWave; m <<= 1) t = tadd2(t, tshfl_xor(t, m));
+            // fold into the block's tree: st[0] R_even, st[1] pairs, st[2] quads
+            if ((rd & 1) == 0) {
+                st[0] = t;
+            } else {
+                const Term pr = tadd2(st[0], t);
+                if ((rd & 2) == 0) {
+                    st[1] = pr;
+                } else {
+                    const Term q = tadd2(st[1], pr);
+                    if ((rd & 4) == 0) st[2] = q;
+                    else st[3] = tadd2(st[2], q);
+                }
+            }
         }
-        start = ntile * kMetricTile;
+        const Term s = st[3];
+        if (lane == 0) bsum[b] = s.a, bsum[nb + b] = s.q, bsum[2 * nb + b] = s.d;
     }
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t i = start + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-        double sabs = 0.0, ssq = 0.0, sd = 0.0;
-        metrics_term(ideal[i], fixed[i], sabs, ssq, sd, mx, lo, hi, clip);
-        neu_add(p.sabs, p.cabs, sabs);
-        neu_add(p.ssq, p.csq, ssq);
-        neu_add(p.sd, p.cd, sd);
-    }
-    p.mx = mx;
-    p.lo = lo;
-    p.hi = hi;
-    p.clip = clip;
-    reduce_block(p);
-    if (threadIdx.x == 0) parts[blockIdx.x] = p;
+    block_counts(Cnt{mx, lo, hi, clip}, parts + wg);
 }
 
-// out: [max_abs, sum_abs, sum_sq, sum_d, n_low, n_high, n_clip, n, 0]
-__global__ __launch_bounds__(kBlock) void metrics_pass2(const Part* __restrict__ parts, int nparts, int64_t n,
-                                                        double* __restrict__ out) {
-    Part p{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int i = threadIdx.x; i < nparts; i += kBlock) {  // fixed order per thread
-        const Part& b = parts[i];
-        neu_add(p.sabs, p.cabs, b.sabs);
-        p.cabs = __dadd_rn(p.cabs, b.cabs);
-        neu_add(p.ssq, p.csq, b.ssq);
-        p.csq = __dadd_rn(p.csq, b.csq);
-        neu_add(p.sd, p.cd, b.sd);
-        p.cd = __dadd_rn(p.cd, b.cd);
-        p.mx = fmax(p.mx, b.mx);
-        p.lo += b.lo;
-        p.hi += b.hi;
-        p.clip += b.clip;
+// The ragged last block [nbf * 8192, n) (0 < m < 8192 samples): NumPy's recursion over it, one
+// workgroup (leaves enumerated, summed one per thread, recombined in post-order).
+__global__ __launch_bounds__(kBlock) void metrics_ragged(const double* __restrict__ ideal, const uint8_t* __restrict__ fixed,
+                                                         int64_t n, double* __restrict__ bsum, int64_t nb,
+                                                         Cnt* __restrict__ part) {
+    __shared__ int leaf_off[kPwMaxLeaves], leaf_len[kPwMaxLeaves];
+    __shared__ Term lsum[kPwMaxLeaves];
+    __shared__ int nleaves;
+    const int64_t nbf = n / kPwBlock;
+    const int m = (int)(n - nbf * kPwBlock);
+    double mx = 0.0;
+    uint32_t lo = 0, hi = 0, clip = 0;
+    {
+        const int64_t o0 = nbf * kPwBlock;
+        if (threadIdx.x == 0) {  // leaves in left-to-right order (a right part pushed before its left)
+            int so[16], sl[16], sp = 1, cnt = 0;
+            so[0] = 0, sl[0] = m;
+            while (sp) {
+                --sp;
+                const int o = so[sp], len = sl[sp];
+                if (len <= kPwLeaf) {
+                    leaf_off[cnt] = o, leaf_len[cnt] = len, ++cnt;
+                } else {
+                    const int n2 = len / 2 - (len / 2) % 8;
+                    so[sp] = o + n2, sl[sp] = len - n2, ++sp;
+                    so[sp] = o, sl[sp] = n2, ++sp;
+                }
+            }
+            nleaves = cnt;
+        }
+        __syncthreads();
+        for (int l = threadIdx.x; l < nleaves; l += kBlock)
+            lsum[l] = pw_leaf(ideal, fixed, o0 + leaf_off[l], leaf_len[l], mx, lo, hi, clip);
+        __syncthreads();
+        if (threadIdx.x == 0) {  // post-order: sum = pw(left) + pw(right)
+            int fl[16], fst[16], fp = 1, vp = 0, li = 0;
+            Term vs[16];
+            fl[0] = m, fst[0] = 0;
+            while (fp) {
+                const int len = fl[fp - 1];
+                if (len <= kPwLeaf) {
+                    vs[vp++] = lsum[li++];
+                    --fp;
+                    continue;
+                }
+                const int n2 = len / 2 - (len / 2) % 8;
+                if (fst[fp - 1] == 0) {
+                    fst[fp - 1] = 1, fl[fp] = n2, fst[fp] = 0, ++fp;
+                } else if (fst[fp - 1] == 1) {
+                    fst[fp - 1] = 2, fl[fp] = len - n2, fst[fp] = 0, ++fp;
+                } else {
+                    const Term rr = vs[--vp], ll = vs[--vp];
+                    vs[vp++] = tadd2(ll, rr);
+                    --fp;
+                }
+            }
+            bsum[nbf] = vs[0].a, bsum[nb + nbf] = vs[0].q, bsum[2 * nb + nbf] = vs[0].d;
+        }
     }
-    reduce_block(p);
-    if (threadIdx.x == 0) {
-        out[0] = p.mx;
-        out[1] = __dadd_rn(p.sabs, p.cabs);
-        out[2] = __dadd_rn(p.ssq, p.csq);
-        out[3] = __dadd_rn(p.sd, p.cd);
-        out[4] = (double)p.lo;
-        out[5] = (double)p.hi;
-        out[6] = (double)p.clip;
+
+    block_counts(Cnt{mx, lo, hi, clip}, part);
+}
+
+// out: [max_abs, sum_abs, sum_sq, sum_d, n_low, n_high, n_clip, n, 0]: the last part's chain
+// (and the ragged block's sum, the last in order), the counts and max of every workgroup.
+__global__ __launch_bounds__(kBlock) void metrics_final(const double* __restrict__ bsum, int64_t nb, int64_t c_lo,
+                                                        double* __restrict__ state, const Cnt* __restrict__ parts,
+                                                        int nparts, int64_t n, double* __restrict__ out) {
+    __shared__ Cnt red[kBlock];
+    const int t = threadIdx.x;
+    Cnt c{0.0, 0, 0, 0};
+    for (int i = t; i < nparts; i += kBlock) {
+        const Cnt& q = parts[i];
+        c.mx = fmax(c.mx, q.mx), c.lo += q.lo, c.hi += q.hi, c.clip += q.clip;
+    }
+    red[t] = c;
+    if (c_lo < nb) chain_range(bsum, nb, c_lo, nb, state, out);  // out[1..3]
+    if (c_lo >= nb && t < 3) out[1 + t] = nb > 0 ? state[t] : 0.0;  // (no last part: n == 0)
+    __syncthreads();
+    for (int w = kBlock / 2; w > 0; w >>= 1) {
+        if (t < w) {
+            Cnt& a = red[t];
+            const Cnt& q = red[t + w];
+            a.mx = fmax(a.mx, q.mx), a.lo += q.lo, a.hi += q.hi, a.clip += q.clip;
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        out[0] = red[0].mx;
+        out[4] = (double)red[0].lo;
+        out[5] = (double)red[0].hi;
+        out[6] = (double)red[0].clip;
         out[7] = (double)n;
         out[8] = 0.0;
     }
 }
 
-size_t metrics_work_bytes() { return sizeof(Part) * kMetricBlocks; }
+static int64_t metrics_nblocks(int64_t n) { return (n + kPwBlock - 1) / kPwBlock; }
+
+// Work buffer: Cnt per workgroup of every launch (+ the ragged block's), the 3 running sums, then
+// the block sums [3][nb].
+constexpr int64_t kLastPart = 512;  // blocks
+#ifndef FIR_METRIC_GROWTH
+#define FIR_METRIC_GROWTH 3
+#endif
+constexpr int64_t kPartGrowth = FIR_METRIC_GROWTH;  // / 2
+constexpr int kMaxParts = 16;
+#ifndef FIR_METRIC_EQUAL
+#define FIR_METRIC_EQUAL 0
+#endif
+constexpr int64_t kEqualPart = FIR_METRIC_EQUAL > 0 ? FIR_METRIC_EQUAL : 4096;
+constexpr int64_t kCntSlots = (int64_t)kMaxParts * kMetricBlocks + 1;
+
+size_t metrics_work_bytes(int64_t n) {
+    return sizeof(Cnt) * kCntSlots + 64 + 3 * sizeof(double) * (size_t)metrics_nblocks(n < 0 ? 0 : n);
+}
 
 int launch_metrics(const double* ideal, const uint8_t* fixed, int64_t n, double* out, void* work,
                    hipStream_t stream, std::string* err) {
     if (n < 0) return *err = "n must be >= 0", FIR_EINVAL;
     if (!out || !work || (n > 0 && (!ideal || !fixed))) return *err = "null pointer argument", FIR_EINVAL;
-    int64_t want = (n + kBlock - 1) / kBlock;
-    const int blocks = (int)(want < 1 ? 1 : (want > kMetricBlocks ? kMetricBlocks : want));
-    if ((uintptr_t)ideal % 16 == 0 && (uintptr_t)fixed % 2 == 0)
-        hipLaunchKernelGGL(metrics_pass1<true>, dim3(blocks), dim3(kBlock), 0, stream, ideal, fixed, n, (Part*)work);
-    else
-        hipLaunchKernelGGL(metrics_pass1<false>, dim3(blocks), dim3(kBlock), 0, stream, ideal, fixed, n, (Part*)work);
-    hipLaunchKernelGGL(metrics_pass2, dim3(1), dim3(kBlock), 0, stream, (const Part*)work, blocks, n, out);
+    const int64_t nb = metrics_nblocks(n), nbf = n / kPwBlock;
+    Cnt* parts = (Cnt*)work;
+    double* state = (double*)((char*)work + sizeof(Cnt) * kCntSlots);
+    double* bsum = state + 8;
+    const bool vec = (uintptr_t)ideal % 16 == 0 && (uintptr_t)fixed % 16 == 0;
+    // part sizes from the end: kLastPart blocks, each earlier part at most kPartGrowth / 2 x the
+    // next (a part's chain, ~9 ns per block, then hides under the next part's streaming, ~14 ns
+    // per block), the first part taking the rest: only the last part's chain is exposed
+    int64_t bounds[kMaxParts + 1];
+    int nparts = 0;
+    {
+        int64_t sizes[kMaxParts], left = nbf, sz = kLastPart;
+        while (left > 0) {
+            int64_t take = nparts == kMaxParts - 1 || sz >= left ? left : sz;
+            if (FIR_METRIC_EQUAL)  // A/B: equal parts of kEqualPart blocks
+                take = nparts == kMaxParts - 1 || left <= kEqualPart ? left : (left % kEqualPart ? left % kEqualPart : kEqualPart);
+            sizes[nparts++] = take;
+            left -= take;
+            sz = sz * kPartGrowth / 2;
+        }
+        bounds[0] = 0;
+        for (int q = 0; q < nparts; ++q) bounds[q + 1] = bounds[q] + sizes[nparts - 1 - q];
+    }
+    int slot = 0;
+    int64_t prev_lo = 0, prev_hi = 0;  // the part whose chain runs in the next launch
+    for (int k = 0; k < nparts; ++k) {
+        const int64_t lo = bounds[k], hi = bounds[k + 1];
+        const int64_t want = (hi - lo + kBlock / kWave - 1) / (kBlock / kWave);
+        const int g = (int)(want > kMetricBlocks ? kMetricBlocks : want);
+        const unsigned grid = (unsigned)g + (prev_hi > prev_lo ? 1u : 0u);
+        if (vec)
+            hipLaunchKernelGGL(metrics_blocks<true>, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, lo, hi,
+                               prev_lo, prev_hi, state, parts + slot);
+        else
+            hipLaunchKernelGGL(metrics_blocks<false>, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, lo, hi,
+                               prev_lo, prev_hi, state, parts + slot);
+        slot += g;
+        prev_lo = lo, prev_hi = hi;
+    }
+    if (nb > nbf) {  // the ragged last block (its sum is the last in order)
+        hipLaunchKernelGGL(metrics_ragged, dim3(1), dim3(kBlock), 0, stream, ideal, fixed, n, bsum, nb, parts + slot);
+        ++slot;
+    }
+    hipLaunchKernelGGL(metrics_final, dim3(1), dim3(kBlock), 0, stream, (const double*)bsum, nb, prev_lo, state,
+                       (const Cnt*)parts, slot, n, out);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return *err = std::string("metrics launch failed: ") + hipGetErrorString(e), FIR_EHIP;
     return FIR_OK;

@@ -33,7 +33,7 @@ OUT_U8_SAT, OUT_I32 = 0, 1
 RESTORE_CLIP, RESTORE_NORMALIZE = 0, 1
 MAX_TAPS = 1 << 24  # FIR_MAX_TAPS: any practical length (the reference has no limit)
 IPC_HANDLE_BYTES = 64
-ABI_VERSION = 2
+ABI_VERSION = 3
 GATE_TIMEOUT = 1  # FIR_GATE_TIMEOUT
 
 _HERE = Path(__file__).resolve().parent
@@ -67,7 +67,7 @@ EXPORTS = {
     "fir2d_fixed_frames_dev": (_i32, [_vp, _i64, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
     "fir1d_ideal_rows": (_i32, [_vp, _i64, _i64, _vp, _i32, _vp, _i32]),
     "fir1d_ideal_rows_dev": (_i32, [_vp, _i64, _i64, _vp, _i32, _vp, _vp]),
-    "fir_metrics_work_bytes": (_i64, []),
+    "fir_metrics_work_bytes": (_i64, [_i64]),
     "fir_compare_metrics": (_i32, [_vp, _vp, _i64, _vp, _i32]),
     "fir_compare_metrics_dev": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp]),
     "fir1d_fixed_rows_sharded": (_i32, [_vp, _i32, _i64, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _i32]),

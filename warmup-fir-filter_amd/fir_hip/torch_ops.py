@@ -244,8 +244,11 @@ def compare_metrics_dev(ideal: torch.Tensor, fixed: torch.Tensor, out: torch.Ten
         raise FirHipError("ideal must be float64 and fixed uint8 of the same shape")
     if out is None:
         out = torch.empty(9, dtype=torch.float64, device=ideal.device)
+    need = int(lib().fir_metrics_work_bytes(ideal.numel()))
     if work is None:
-        work = torch.empty(int(lib().fir_metrics_work_bytes()), dtype=torch.uint8, device=ideal.device)
+        work = torch.empty(need, dtype=torch.uint8, device=ideal.device)
+    elif work.numel() * work.element_size() < need or not work.is_contiguous():
+        raise FirHipError(f"work must be a contiguous device buffer of >= {need} bytes for {ideal.numel()} samples")
     _check(lib().fir_compare_metrics_dev(ctypes.c_void_p(ideal.data_ptr()), ctypes.c_void_p(fixed.data_ptr()),
                                          ideal.numel(), ctypes.c_void_p(out.data_ptr()),
                                          ctypes.c_void_p(work.data_ptr()), _stream_ptr(ideal, stream)),
