@@ -364,9 +364,9 @@ constexpr int64_t kLastPart = 512;  // blocks
 #endif
 constexpr int64_t kPartGrowth = FIR_METRIC_GROWTH;  // / 2
 constexpr int kMaxParts = 16;
-#ifndef FIR_METRIC_EQUAL
-#define FIR_METRIC_EQUAL 0
-#endif
+#ifndef FIR_METRIC_EQUAL  // > 0: equal parts of that many blocks (default); 0: the geometric
+#define FIR_METRIC_EQUAL 4096  // schedule below (A/B, 2^28: 500 vs 631 us, 2^24: 50 vs 97 us;
+#endif                     // profiles/r03/metrics_exact_ab.txt)
 constexpr int64_t kEqualPart = FIR_METRIC_EQUAL > 0 ? FIR_METRIC_EQUAL : 4096;
 constexpr int64_t kCntSlots = (int64_t)kMaxParts * kMetricBlocks + 1;
 
@@ -383,9 +383,10 @@ int launch_metrics(const double* ideal, const uint8_t* fixed, int64_t n, double*
     double* state = (double*)((char*)work + sizeof(Cnt) * kCntSlots);
     double* bsum = state + 8;
     const bool vec = (uintptr_t)ideal % 16 == 0 && (uintptr_t)fixed % 16 == 0;
-    // part sizes from the end: kLastPart blocks, each earlier part at most kPartGrowth / 2 x the
-    // next (a part's chain, ~9 ns per block, then hides under the next part's streaming, ~14 ns
-    // per block), the first part taking the rest: only the last part's chain is exposed
+    // parts of kEqualPart blocks (2^25 samples), the remainder first: the chain of a part (~9 ns
+    // per block) hides under the next part's streaming (~14 ns per block), only the last part's
+    // chain is exposed.  (A/B: sizes shrinking geometrically toward the end, kLastPart blocks
+    // last, each earlier part kPartGrowth / 2 x the next, lost to the extra launches.)
     int64_t bounds[kMaxParts + 1];
     int nparts = 0;
     {
