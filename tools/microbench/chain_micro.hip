@@ -25,9 +25,12 @@ __device__ double lane_d(double v, int j) {
 
 template <int MODE>
 __global__ void chain(const double* x, double* out) {
+    __shared__ double sh[64];
     const int lane = threadIdx.x;
     double s = 0.0, s2 = 0.0, s3 = 0.0;
     const double v = x[lane];
+    sh[lane] = v;
+    __syncthreads();
     for (int it = 0; it < kN / 64; ++it) {
 #pragma unroll
         for (int j = 0; j < 64; ++j) {
@@ -38,6 +41,7 @@ __global__ void chain(const double* x, double* out) {
                 s = __dadd_rn(s, w), s2 = __dadd_rn(s2, w * 2.0), s3 = __dadd_rn(s3, w * 3.0);
             }
             if constexpr (MODE == 3) s = (double)((float)s + (float)v);  // f32 reference
+            if constexpr (MODE == 4) s = __dadd_rn(s, sh[j]);           // LDS broadcast-fed
         }
     }
     out[lane] = s + s2 + s3;
@@ -63,7 +67,7 @@ int main() {
     CK(hipMalloc(&x, 64 * sizeof(double)));
     CK(hipMalloc(&o, 64 * sizeof(double)));
     CK(hipMemset(x, 0, 64 * sizeof(double)));
-    printf("ns per dependent step: f64 VGPR %.2f, f64 readlane-fed %.2f, 3 chains readlane-fed %.2f, f32-ish %.2f\n",
-           run<0>(x, o), run<1>(x, o), run<2>(x, o), run<3>(x, o));
+    printf("ns per dependent step: f64 VGPR %.2f, f64 readlane-fed %.2f, 3 chains readlane-fed %.2f, f32-ish %.2f, "
+           "f64 LDS-broadcast-fed %.2f\n", run<0>(x, o), run<1>(x, o), run<2>(x, o), run<3>(x, o), run<4>(x, o));
     return 0;
 }

@@ -117,52 +117,48 @@ __device__ void block_counts(Cnt c, Cnt* dst) {
 }
 
 // The running sums state[0..2] += block sums [lo, hi) of |d|, d^2, d, in order (from 0.0 when
-// lo == 0).  Waves 0-2 take one array each: 64 block sums per coalesced load (8 such loads in
-// flight), moved to the running sum one by one with v_readlane (SGPR operands, independent of
-// the sum), so the dependent chain is one float64 add per 8192 samples.  No barrier inside.
+// lo == 0).  Waves 0-2 take one array each: kChainDepth coalesced loads of 64 block sums in
+// flight, each group staged in the wave's LDS and read back in order by every lane at the same
+// address (a broadcast), so the dependent chain is one float64 add with a VGPR operand per 8192
+// samples (2.7 ns; fed by v_readlane instead: 8.7 ns, tools/microbench/chain_micro.hip).
+// `lds` holds 3 x kChainDepth x 64 doubles; no workgroup barrier inside.
 constexpr int kChainDepth = 8;
-__device__ double pw_lane(double v, int j) {
-    const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, j);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), j);
-    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-}
+constexpr int kChainLds = 3 * kChainDepth * kWave * (int)sizeof(double);
 __device__ void chain_range(const double* __restrict__ bsum, int64_t nb, int64_t lo, int64_t hi, double* state,
-                            double* out = nullptr) {
+                            uint8_t* lds, double* out = nullptr) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
     if (wv >= 3) return;
     const double* src = bsum + (int64_t)wv * nb;
+    double* sh = reinterpret_cast<double*>(lds) + wv * kChainDepth * kWave;
     double s = lo == 0 ? 0.0 : state[wv];
-    // groups of kChainDepth batches of 64: the next group's loads go out before this group's adds
-    // (one batch in flight took ~1.5 us of load latency per 64 adds)
     constexpr int D = kChainDepth;
     auto fetch = [&](int64_t c0, double (&q)[D]) {
 #pragma unroll
         for (int d = 0; d < D; ++d) q[d] = c0 + d * kWave + lane < hi ? src[c0 + d * kWave + lane] : 0.0;
     };
-    double q[D], r[D];
+    double q[D];
     fetch(lo, q);
     for (int64_t g0 = lo; g0 < hi; g0 += D * kWave) {
+        __builtin_amdgcn_wave_barrier();  // the previous group's reads are done (one wave: in order)
 #pragma unroll
-        for (int d = 0; d < D; ++d) r[d] = q[d];
-        fetch(g0 + D * kWave, q);
-        if (hi - g0 >= D * kWave) {
+        for (int d = 0; d < D; ++d) sh[d * kWave + lane] = q[d];
+        __builtin_amdgcn_wave_barrier();
+        fetch(g0 + D * kWave, q);  // the next group's loads, in flight during the adds
+        const int len = hi - g0 < D * kWave ? (int)(hi - g0) : D * kWave;
+        int e = 0;
+        for (; e + 16 <= len; e += 16) {
+            double v[16];
 #pragma unroll
-            for (int d = 0; d < D; ++d)
+            for (int j = 0; j < 16; ++j) v[j] = sh[e + j];
 #pragma unroll
-                for (int j = 0; j < kWave; ++j) s = __dadd_rn(s, pw_lane(r[d], j));
-        } else {
-            const int len = (int)(hi - g0);
-            for (int e = 0; e < len; ++e) {
-                double v = r[0];
-#pragma unroll
-                for (int d = 1; d < D; ++d) v = e / kWave == d ? r[d] : v;
-                s = __dadd_rn(s, pw_lane(v, e % kWave));
-            }
+            for (int j = 0; j < 16; ++j) s = __dadd_rn(s, v[j]);
         }
+        for (; e < len; ++e) s = __dadd_rn(s, sh[e]);
     }
-    if (lane == 0) state[wv] = s;
-    if (out && lane == 0) out[1 + wv] = s;
+    if (lane == 0) {
+        state[wv] = s;
+        if (out) out[1 + wv] = s;
+    }
 }
 
 // One WAVE per full block (no workgroup barrier: waves stream independently), grid-stride over
@@ -173,6 +169,7 @@ __device__ void chain_range(const double* __restrict__ bsum, int64_t nb, int64_t
 // straight from HBM touches 16 half lines per load and ran at 3.3 TB/s.)
 constexpr int kMetRow = 1024 + 64;                      // LDS bytes per leaf row (+64: conflict-free reads)
 constexpr int kMetWaveLds = 8 * kMetRow + 1024;         // + the round's 1 KiB of fixed bytes
+static_assert(kBlock / kWave * kMetWaveLds >= kChainLds, "the chain's staging shares the wave buffers");
 template <bool VEC>
 __global__ __launch_bounds__(kBlock, FIR_METRIC_MINB) void metrics_blocks(const double* __restrict__ ideal,
                                                                          const uint8_t* __restrict__ fixed,
@@ -185,7 +182,7 @@ __global__ __launch_bounds__(kBlock, FIR_METRIC_MINB) void metrics_blocks(const 
     __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock / kWave * kMetWaveLds];
     const bool chain = c_hi > c_lo;
     if (chain && blockIdx.x == 0) {  // dispatched first: the chain starts with the part
-        chain_range(bsum, nb, c_lo, c_hi, state);
+        chain_range(bsum, nb, c_lo, c_hi, state, smem);
         return;
     }
     const int wg = blockIdx.x - (chain ? 1 : 0);
@@ -326,6 +323,7 @@ __global__ __launch_bounds__(kBlock) void metrics_final(const double* __restrict
                                                         double* __restrict__ state, const Cnt* __restrict__ parts,
                                                         int nparts, int64_t n, double* __restrict__ out) {
     __shared__ Cnt red[kBlock];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kChainLds];
     const int t = threadIdx.x;
     Cnt c{0.0, 0, 0, 0};
     for (int i = t; i < nparts; i += kBlock) {
@@ -333,7 +331,7 @@ __global__ __launch_bounds__(kBlock) void metrics_final(const double* __restrict
         c.mx = fmax(c.mx, q.mx), c.lo += q.lo, c.hi += q.hi, c.clip += q.clip;
     }
     red[t] = c;
-    if (c_lo < nb) chain_range(bsum, nb, c_lo, nb, state, out);  // out[1..3]
+    if (c_lo < nb) chain_range(bsum, nb, c_lo, nb, state, smem, out);  // out[1..3]
     if (c_lo >= nb && t < 3) out[1 + t] = nb > 0 ? state[t] : 0.0;  // (no last part: n == 0)
     __syncthreads();
     for (int w = kBlock / 2; w > 0; w >>= 1) {
