@@ -216,15 +216,25 @@ __global__ __launch_bounds__(kBlock, FIR_METRIC_MINB) void metrics_blocks(const 
             __builtin_amdgcn_wave_barrier();  // the previous round's reads are done (one wave: in order)
 #pragma unroll
             for (int i = 0; i < 8; ++i) *reinterpret_cast<d2*>(wl + i * kMetRow + 16 * lane) = v[i];
-            *reinterpret_cast<u4*>(wl + 8 * kMetRow + 16 * lane) = fx;
+            // fixed bytes transposed to [leaf][accumulator j][step s]: lane (k', m) holds samples
+            // 16 m .. 16 m + 15 of leaf k', i.e. steps 2m, 2m + 1 of every j (bytes j, j + 8)
+            {
+                const uint32_t fw[4] = {fx.x, fx.y, fx.z, fx.w};
+                uint8_t* fdst = wl + 8 * kMetRow + 128 * (lane >> 3) + 2 * (lane & 7);
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj)
+                    *reinterpret_cast<uint16_t*>(fdst + 16 * jj) =
+                        (uint16_t)__builtin_amdgcn_perm(fw[2 + jj / 4], fw[jj / 4], (uint32_t)(jj % 4) | ((4u + jj % 4) << 8));
+            }
             __builtin_amdgcn_wave_barrier();
             const uint8_t* row = wl + k * kMetRow + 8 * j;
-            const uint8_t* frow = wl + 8 * kMetRow + 128 * k + j;
+            const u4 fr = *reinterpret_cast<const u4*>(wl + 8 * kMetRow + 128 * k + 16 * j);  // steps 0..15
+            const uint32_t frw[4] = {fr.x, fr.y, fr.z, fr.w};
             Term r{0.0, 0.0, 0.0};
 #pragma unroll
             for (int s = 0; s < 16; ++s) {
                 double id = *reinterpret_cast<const double*>(row + 64 * s);
-                uint32_t f = frow[8 * s];
+                uint32_t f = (frw[s / 4] >> (8 * (s % 4))) & 0xFFu;
                 asm volatile("" : "+v"(id), "+v"(f), "+v"(mx), "+v"(lo), "+v"(hi), "+v"(clip));
                 const Term t = metrics_term(id, f, mx, lo, hi, clip);
                 if (s == 0) r = t;
