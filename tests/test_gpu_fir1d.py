@@ -181,6 +181,22 @@ def test_long_filters_vs_oracle(L, dtype, stage, shape):
         assert np.array_equal(got, _co().fir1d_rows(x, hq, 12, acc, stage)), acc
 
 
+@pytest.mark.parametrize("L", [17, 31, 64])
+@pytest.mark.parametrize("shape", [(7, 3000), (1, 5128), (3, 1032), (2, 2056)])
+def test_long_filter_step_geometry(L, shape):
+    """The step-form MFMA kernel (fir1d_mfma.hip, two tiles per step) on rows whose tile count is
+    odd (the last step's second tile is empty or partial) and on single rows just past a step."""
+    rng = np.random.default_rng(L * 7 + shape[1])
+    hq = rng.integers(-3000, 3000, L).tolist()
+    co = _co()
+    for dtype in (np.int16, np.uint8):
+        info = np.iinfo(dtype)
+        x = rng.integers(info.min, info.max + 1, shape, dtype=dtype)
+        for stage in (fir_hip.OUT_I32, fir_hip.OUT_U8_SAT):
+            assert np.array_equal(fir_hip.fir1d_fixed_rows(x, hq, 12, 32, stage), co.fir1d_rows(x, hq, 12, 32, stage)), (
+                dtype, stage)
+
+
 @pytest.mark.parametrize("L", [10, 17, 32, 33, 48, 64])
 def test_long_filters_matrix_core_extremes(L):
     """The int8 matrix-core path (fir1d_mfma.hip) at the edges of its signed-byte splits: taps at

@@ -71,8 +71,28 @@ __device__ __forceinline__ void tadd(Term& s, const Term& t) {
 __device__ __forceinline__ Term tadd2(const Term& s, const Term& t) {
     return Term{__dadd_rn(s.a, t.a), __dadd_rn(s.q, t.q), __dadd_rn(s.d, t.d)};
 }
-__device__ __forceinline__ Term tshfl_xor(const Term& s, int m) {
-    return Term{__shfl_xor(s.a, m), __shfl_xor(s.q, m), __shfl_xor(s.d, m)};
+// lane i receives lane i + D's value (only the tree's leader lanes, multiples of 2D, are used):
+// DPP row_shl within 16-lane rows, v_permlane16/32_swap across rows (VALU, not the LDS unit
+// that __shfl_xor's ds_bpermute uses)
+template <int D>
+__device__ __forceinline__ double dshift(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    uint32_t lo = (uint32_t)b, hi = (uint32_t)(b >> 32);
+    if constexpr (D < 16) {
+        lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x100 + D, 0xF, 0xF, false);
+        hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x100 + D, 0xF, 0xF, false);
+    } else if constexpr (D == 16) {
+        lo = __builtin_amdgcn_permlane16_swap(lo, lo, false, false)[1];
+        hi = __builtin_amdgcn_permlane16_swap(hi, hi, false, false)[1];
+    } else {
+        lo = __builtin_amdgcn_permlane32_swap(lo, lo, false, false)[1];
+        hi = __builtin_amdgcn_permlane32_swap(hi, hi, false, false)[1];
+    }
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+template <int D>
+__device__ __forceinline__ Term tshift(const Term& s) {
+    return Term{dshift<D>(s.a), dshift<D>(s.q), dshift<D>(s.d)};
 }
 
 // pairwise_sum of one leaf (n <= 128) of samples [o, o + n), as NumPy's loop does it
@@ -242,8 +262,12 @@ __global__ __launch_bounds__(kBlock, FIR_METRIC_MINB) void metrics_blocks(const 
             }
             // leaf: ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the round's 8 leaves pairwise
             Term t = r;
-#pragma unroll
-            for (int m = 1; m < kWave; m <<= 1) t = tadd2(t, tshfl_xor(t, m));
+            t = tadd2(t, tshift<1>(t));
+            t = tadd2(t, tshift<2>(t));
+            t = tadd2(t, tshift<4>(t));
+            t = tadd2(t, tshift<8>(t));
+            t = tadd2(t, tshift<16>(t));
+            t = tadd2(t, tshift<32>(t));  // lane 0 holds the round's sum
             // fold into the block's tree: st[0] R_even, st[1] pairs, st[2] quads
             if ((rd & 1) == 0) {
                 st[0] = t;
