@@ -390,16 +390,14 @@ static int64_t metrics_nblocks(int64_t n) { return (n + kPwBlock - 1) / kPwBlock
 
 // Work buffer: Cnt per workgroup of every launch (+ the ragged block's), the 3 running sums, then
 // the block sums [3][nb].
-constexpr int64_t kLastPart = 512;  // blocks
-#ifndef FIR_METRIC_GROWTH
-#define FIR_METRIC_GROWTH 3
+#ifndef FIR_METRIC_TAIL  // blocks of the last part (its chain is the exposed one)
+#define FIR_METRIC_TAIL 2048
 #endif
-constexpr int64_t kPartGrowth = FIR_METRIC_GROWTH;  // / 2
+#ifndef FIR_METRIC_BODY  // blocks of every earlier part
+#define FIR_METRIC_BODY 8192
+#endif
+constexpr int64_t kTailPart = FIR_METRIC_TAIL, kBodyPart = FIR_METRIC_BODY;
 constexpr int kMaxParts = 16;
-#ifndef FIR_METRIC_EQUAL  // > 0: equal parts of that many blocks (default); 0: the geometric
-#define FIR_METRIC_EQUAL 4096  // schedule below (A/B, 2^28: 500 vs 631 us, 2^24: 50 vs 97 us;
-#endif                     // profiles/r03/metrics_exact_ab.txt)
-constexpr int64_t kEqualPart = FIR_METRIC_EQUAL > 0 ? FIR_METRIC_EQUAL : 4096;
 constexpr int64_t kCntSlots = (int64_t)kMaxParts * kMetricBlocks + 1;
 
 size_t metrics_work_bytes(int64_t n) {
@@ -415,21 +413,19 @@ int launch_metrics(const double* ideal, const uint8_t* fixed, int64_t n, double*
     double* state = (double*)((char*)work + sizeof(Cnt) * kCntSlots);
     double* bsum = state + 8;
     const bool vec = (uintptr_t)ideal % 16 == 0 && (uintptr_t)fixed % 16 == 0;
-    // parts of kEqualPart blocks (2^25 samples), the remainder first: the chain of a part (~9 ns
-    // per block) hides under the next part's streaming (~14 ns per block), only the last part's
-    // chain is exposed.  (A/B: sizes shrinking geometrically toward the end, kLastPart blocks
-    // last, each earlier part kPartGrowth / 2 x the next, lost to the extra launches.)
+    // parts from the end: kTailPart blocks last, kBodyPart before it, the first part the rest; the
+    // chain of a part (2.7 ns per block) hides under the next part's streaming (~14 ns per block),
+    // only the last part's chain is exposed (A/B, profiles/r03/metrics_exact_ab.txt: equal parts
+    // of 4096 blocks 472 us, sizes shrinking geometrically toward the end lost to the extra launches)
     int64_t bounds[kMaxParts + 1];
     int nparts = 0;
     {
-        int64_t sizes[kMaxParts], left = nbf, sz = kLastPart;
+        int64_t sizes[kMaxParts], left = nbf;
         while (left > 0) {
-            int64_t take = nparts == kMaxParts - 1 || sz >= left ? left : sz;
-            if (FIR_METRIC_EQUAL)  // A/B: equal parts of kEqualPart blocks
-                take = nparts == kMaxParts - 1 || left <= kEqualPart ? left : (left % kEqualPart ? left % kEqualPart : kEqualPart);
+            const int64_t want = nparts == 0 ? kTailPart : kBodyPart;
+            const int64_t take = nparts == kMaxParts - 1 || left <= want ? left : want;
             sizes[nparts++] = take;
             left -= take;
-            sz = sz * kPartGrowth / 2;
         }
         bounds[0] = 0;
         for (int q = 0; q < nparts; ++q) bounds[q + 1] = bounds[q] + sizes[nparts - 1 - q];
