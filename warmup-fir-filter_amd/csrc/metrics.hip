@@ -15,17 +15,17 @@
 // n2 = floor(n/2) rounded down to a multiple of 8, sum = pw(left) + pw(right).
 //
 //   pass 1 (metrics_blocks): one wave per full 8192-sample block, grid-stride; a full block is
-//     a balanced tree of 64 leaves of 128: 4 rounds of 16 leaves, 4 lanes a leaf (2 accumulators
-//     each, 16 steps of 16-byte loads), the leaf and round trees by lane shuffles (IEEE addition
-//     is commutative, so a lane adding its partner's value to its own matches either order);
-//     counts and max per workgroup; metrics_ragged: the ragged last block by the general
-//     recursion (leaves enumerated, summed one per thread, recombined in post-order).
+//     a balanced tree of 64 leaves of 128: 8 rounds of 8 leaves, each round loaded as contiguous
+//     1 KiB rows and transposed through the wave's LDS so that lane (leaf, j) adds accumulator
+//     r[j]'s 16 terms in order; the leaf and round trees by DPP row shifts and permlane swaps (IEEE
+//     addition is commutative, so a lane adding its partner's value matches either order); counts
+//     and max per workgroup.  metrics_ragged: the ragged last block by the general recursion
+//     (leaves enumerated, summed one per thread, recombined in post-order).
 //   the chain: waves 0-2 of one workgroup add the block sums of |d|, d^2 and d in order (a
-//     dependent float64 chain).  The full blocks are split
-//     into parts of one launch each, shrinking toward the end (last 512 blocks), and the chain
-//     over part k-1 runs as an extra workgroup of the launch that streams part k (2^28 samples:
-//     the chain's 168 us are hidden but for the last part's); metrics_final adds the last part
-//     (and the ragged block) and reduces the counts and max.
+//     dependent float64 chain, 2.7 ns per block).  The full blocks are split into parts of one
+//     launch each (8192 blocks, the last 2048), and the chain over part k-1 runs as an extra
+//     workgroup of the launch that streams part k, so only the last part's chain is exposed;
+//     metrics_final adds the last part (and the ragged block) and reduces the counts and max.
 #include <string>
 
 #include "fir_common.h"
