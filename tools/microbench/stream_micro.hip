@@ -574,6 +574,58 @@ __global__ __launch_bounds__(256, 4) void mfbig(const int16_t* __restrict__ x, u
                                         reinterpret_cast<u32x4*>(y + ((int64_t)t * TPS + k) * 1024) + lane);
     }
 }
+// The same big-step copy with DYNAMIC step order: each wave takes its next step from a global
+// ticket counter (one atomic per step, taken one step ahead), so the steps in flight stay a
+// compact, in-order window of addresses as in a one-shot grid.  NTL: non-temporal body loads.
+__device__ unsigned g_ticket;
+template <int TPS, bool NTL>
+__global__ __launch_bounds__(256, 4) void mfticket(const int16_t* __restrict__ x, uint8_t* __restrict__ y, uint32_t nsteps) {
+    constexpr int NL = 2 * TPS;
+    const int lane = threadIdx.x & 63;
+    u32x4 raw[NL], halo;
+    auto load = [&](uint32_t t) {
+        const u32x4* src = reinterpret_cast<const u32x4*>(x + (int64_t)t * 1024 * TPS);
+#pragma unroll
+        for (int k = 0; k < NL; ++k) raw[k] = NTL ? __builtin_nontemporal_load(src + 64 * k + lane) : src[64 * k + lane];
+        halo = t + 1 < nsteps ? src[64 * NL + (lane & 7)] : u32x4{0u, 0u, 0u, 0u};
+    };
+    auto take = [&]() {
+        unsigned v = 0;
+        if (lane == 0) v = atomicAdd(&g_ticket, 1u);
+        return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+    };
+    uint32_t t = take();
+    if (t >= nsteps) return;
+    load(t);
+    uint32_t nx = take();
+    for (;;) {
+        uint32_t h[2 * NL];
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+            h[2 * k] = __builtin_amdgcn_perm(raw[k].y, raw[k].x, 0x07050301u);
+            h[2 * k + 1] = __builtin_amdgcn_perm(raw[k].w, raw[k].z, 0x07050301u) ^ halo.x;
+        }
+        const uint32_t cur = t;
+        t = nx;
+        if (t < nsteps) {
+            load(t);
+            nx = take();
+        }
+#pragma unroll
+        for (int k = 0; k < TPS; ++k)
+            __builtin_nontemporal_store(u32x4{h[4 * k], h[4 * k + 1], h[4 * k + 2], h[4 * k + 3]},
+                                        reinterpret_cast<u32x4*>(y + ((int64_t)cur * TPS + k) * 1024) + lane);
+        if (t >= nsteps) break;
+    }
+}
+template <int TPS, bool NTL, int BLOCKS>
+void l_mfticket(const Bufs& b, hipStream_t s) {
+    const unsigned zero = 0;
+    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_ticket), &zero, sizeof(zero), 0, hipMemcpyHostToDevice, s);
+    hipLaunchKernelGGL((mfticket<TPS, NTL>), dim3(BLOCKS), dim3(256), 0, s, b.x, reinterpret_cast<uint8_t*>(b.y),
+                       (uint32_t)(b.n / 1024 / TPS));
+}
+
 template <int TPS, bool LDS, int BLOCKS, int WALK = 0>
 void l_mfbig(const Bufs& b, hipStream_t s) {
     const uint32_t ns = (uint32_t)(b.n / 1024 / TPS);
@@ -616,6 +668,11 @@ int main(int argc, char** argv) {
         {"split one-shot", l_mfsplit<0, 0, 4>, b.n * 3.0, false, {}},
         {"oneshot ntl", l_mfsplit<0, 3, 4, true>, b.n * 3.0, false, {}},
         {"mfpat win pf lds", l_mfpat<1, true, true>, b.n * 3.0, false, {}},
+        {"ticket1 b1k", l_mfticket<1, false, 1024>, b.n * 3.0, false, {}},
+        {"ticket1 ntl b1k", l_mfticket<1, true, 1024>, b.n * 3.0, false, {}},
+        {"ticket2 ntl b1k", l_mfticket<2, true, 1024>, b.n * 3.0, false, {}},
+        {"ticket2 ntl b2k", l_mfticket<2, true, 2048>, b.n * 3.0, false, {}},
+        {"ticket4 ntl b1k", l_mfticket<4, true, 1024>, b.n * 3.0, false, {}},
         {"big1 b1k", l_mfbig<1, false, 1024>, b.n * 3.0, false, {}},
         {"big2 b1k", l_mfbig<2, false, 1024>, b.n * 3.0, false, {}},
         {"big4 b1k", l_mfbig<4, false, 1024>, b.n * 3.0, false, {}},
