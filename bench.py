@@ -10,12 +10,19 @@ neighbours' HBM over xGMI, ordered per step (device atomics on mailboxes mapped 
 launch of the FIR kernel reading it (FIR_HALO=rccl: RCCL send/recv every step, overlapped with
 the bulk kernel, then an edge kernel).
 
-Contract: `python bench.py --gpus N --steps K --warmup W` (torchrun for N > 1); rank 0
-prints ONE JSON line.  Extra keys:
+Contract: `python bench.py --gpus N --steps K --warmup W`; rank 0 prints ONE JSON line.  For
+N > 1 either launch it under torch.distributed.run (RANK/WORLD_SIZE set), or run it as is: the
+parent then starts `torch.distributed.run --nproc-per-node N` as a child process before any GPU
+call of its own, forwards rank 0's JSON line and exits with the children's status.  A box with
+fewer GPUs than ranks rehearses over gloo (ranks share devices; config.rehearsal says so).
+Extra keys:
   roofline      dominant kernel's algorithmic bytes / its mean duration (HIP events on the
-                stream it runs on), vs the 8.0 TB/s HBM3E peak; `traffic` = PMC HBM bytes per
-                launch from the committed rocprofv3 summary in profiles/ (null if absent)
-  cpu_baseline  the C oracle (oracle/fir_oracle.c, OpenMP) on this host's cores, same input
+                stream it runs on: 100 untimed ramp launches, then 200 timed back to back,
+                whatever --steps/--warmup are), vs the 8.0 TB/s HBM3E peak; `traffic` = PMC
+                HBM bytes per launch from the committed rocprofv3 summary in profiles/ (null if
+                absent)
+  cpu_baseline  the C oracle (oracle/fir_oracle.c, OpenMP) on this host's cores, same input;
+                timed by rank 0 at every N, after the GPU legs, while the other ranks wait
   parity        every rank's full output compared bit-exactly with the C oracle
   cpu_baseline_numpy  the vectorised NumPy restatement (oracle/fir_oracle.py, one core) on a
                 bounded leading slice of the same input (BASELINE.md's "NumPy CPU path")
@@ -70,10 +77,14 @@ SELF_HALO = os.environ.get("FIR_SELF_HALO") == "1"
 # N > 1 halo source: "xgmi" (default: neighbours' HBM mapped once, read by the edge kernel) or
 # "rccl" (send/recv every step); xgmi falls back to rccl on every rank if any rank cannot map.
 HALO_PREF = os.environ.get("FIR_HALO", "xgmi")
+# xGMI step ordering: "overlap" (the gate on a high-priority side stream while the bulk kernel runs,
+# then a 4-output edge kernel) or "serial" (the gate, then ONE segment launch reading its halos)
+GATE_MODE = os.environ.get("FIR_GATE_MODE", "overlap")
 KERNELS = {"fir1d_i16": "fir1d_reg_kernel", "cplx_i16": "fir1d_reg_kernel", "fir2d_u8": "fir2d_pk16_strip_kernel",
            "fir1d_u8": "fir1d_reg_kernel", "ideal_u8": "fir1d_ideal_kernel", "bank_u8": "fir1d_reg_kernel",
            "restore_u8": "restore_map_kernel", "metrics_u8": "metrics_blocks+chain"}
 NUMPY_ONLY = ("restore_u8", "metrics_u8")  # no C oracle leg: the NumPy restatement is the CPU baseline
+ROOF_RAMP, ROOF_LAUNCHES = 100, 200  # roofline loop: untimed ramp, then timed launches of the dominant kernel
 
 
 def _env_int(name: str, default: int) -> int:
@@ -84,6 +95,52 @@ def _env_int(name: str, default: int) -> int:
 def _cpu_threads() -> int:
     n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     return max(1, min(16, _env_int("OMP_NUM_THREADS", n), n))
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def launch_ranks(n: int, script: str, argv: list[str], env: dict | None = None) -> int:
+    """Run ``script argv`` as n ranks under torch.distributed.run (a CHILD process: the caller
+    must not have touched the GPU, and nothing here execs).  Rank 0's JSON line is forwarded to
+    stdout; everything else the ranks print goes to stderr.  Returns the launcher's exit status
+    (non-zero if any rank failed, or if no JSON line came back)."""
+    import subprocess
+    import tempfile
+
+    env = dict(os.environ if env is None else env)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    with tempfile.TemporaryDirectory(prefix="fir_bench_") as tmp:
+        # rank 0 writes its line to a file (emit_result): torchrun runs the ranks unbuffered, so a
+        # line on a shared stdout pipe can interleave with another rank's output
+        result = Path(tmp) / "result.json"
+        env["FIR_BENCH_RESULT"] = str(result)
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), script, *argv]
+        # the ranks' own output goes to stderr: stdout carries only the result line
+        rc = subprocess.run(cmd, env=env, stdout=sys.stderr.fileno()).returncode
+        line = result.read_text().strip() if result.exists() else ""
+    if line:
+        print(line, flush=True)
+    elif rc == 0:
+        print("bench.py: the ranks exited without a result line", file=sys.stderr)
+        return 1
+    return rc
+
+
+def emit_result(line: str) -> None:
+    """Rank 0's one JSON line: to the launcher's result file when started by launch_ranks, else
+    stdout."""
+    path = os.environ.get("FIR_BENCH_RESULT")
+    if path:
+        Path(path).write_text(line + "\n")
+    else:
+        print(line, flush=True)
 
 
 class Workload:
@@ -226,9 +283,9 @@ class Workload:
             torch_ops.fir1d_fixed_rows_dev(self.x, self.taps, 12, 32, fir_hip.OUT_I32, self.channels, out=self.y)
 
     def dominant(self):
-        """The step's dominant kernel alone (roofline timing): the halo-reading launch of an
+        """The step's dominant kernel alone (roofline timing): the halo-reading launch of a serial
         xGMI-sharded step, else the bulk kernel."""
-        if self.sharded_1d and self.halo_kind == "xgmi":
+        if self.sharded_1d and self.halo_kind == "xgmi" and GATE_MODE == "serial":
             torch_ops.fir1d_fixed_segment_dev(self.x, self.taps, *self.halo_src.halos(), 12, 32, fir_hip.OUT_I32,
                                               self.channels, out=self.y)
         else:
@@ -240,9 +297,11 @@ class Workload:
             self.bulk()
             return
         if self.halo_src is None:  # set up once (collectively), used every step
-            if self.world == 1:  # FIR_SELF_HALO rehearsal: RCCL ring of one
-                self.halo_kind = "rccl"
-                self.halo_src = sharded.HaloExchange(self.x, self.taps.n, self.channels, self_ring=True)
+            if self.world == 1:  # FIR_SELF_HALO rehearsal: a ring of one (RCCL, or the gate on its own mailbox)
+                self.halo_kind = "xgmi" if HALO_PREF == "xgmi" else "rccl"
+                self.halo_src = (sharded.XgmiHalo(self.x, self.taps.n, self.channels, self_ring=True)
+                                 if self.halo_kind == "xgmi" else
+                                 sharded.HaloExchange(self.x, self.taps.n, self.channels, self_ring=True))
             else:
                 self.halo_kind, self.halo_src = sharded.make_halo_source(self.x, self.taps.n, self.channels,
                                                                          prefer=HALO_PREF)
@@ -250,10 +309,20 @@ class Workload:
                 f"contiguous shards x{self.world}, " + (
                     "halo handed over through the neighbours' HBM over xGMI, ordered per step: a one-wave gate "
                     "kernel publishes this rank's edge samples with the step's epoch, waits for both neighbours' "
-                    "epoch (device atomics on IPC-mapped mailboxes) and copies their edges; then one FIR launch "
-                    "reads them" if self.halo_kind == "xgmi"
+                    "epoch (device atomics on IPC-mapped mailboxes) and copies their edges; " + (
+                        "the gate runs on a high-priority side stream while the bulk FIR kernel runs, then a "
+                        "4-output edge kernel reads the halos" if GATE_MODE == "overlap" else
+                        "then one FIR launch reads them") if self.halo_kind == "xgmi"
                     else "halo exchanged by RCCL send/recv every step (ordered by the messages), overlapped with "
                          "the bulk kernel, then an edge kernel"))
+        if self.halo_kind == "xgmi" and GATE_MODE == "overlap":  # gate || bulk, then the edge kernel
+            self.halo_src.gate_async()
+            self.bulk()
+            self.halo_src.join()
+            self.left, self.right = self.halo_src.halos()
+            torch_ops.fir1d_fixed_edges_dev(self.x, self.taps, self.y, self.left, self.right, 12, 32, fir_hip.OUT_I32,
+                                            self.channels)
+            return
         if self.halo_kind == "xgmi":  # the ordered hand-off, then ONE FIR launch reading the received halos
             self.halo_src.gate()
             self.left, self.right = self.halo_src.halos()
@@ -386,13 +455,29 @@ def main() -> int:
     ap.add_argument("--no-parity", action="store_true", help="skip the full-size oracle comparison")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # started directly: spawn the ranks as children (nothing here has touched the GPU;
+        # device_count() does not initialise it on this image)
+        env = dict(os.environ)
+        if "FIR_DIST_BACKEND" not in env and torch.cuda.device_count() < args.gpus:
+            env["FIR_DIST_BACKEND"] = "gloo"
+            env["FIR_BENCH_REHEARSAL"] = f"{args.gpus} ranks on {torch.cuda.device_count()} GPU(s)"
+        return launch_ranks(args.gpus, str(Path(__file__).resolve()), sys.argv[1:], env)
+
     rank, world = _env_int("RANK", 0), _env_int("WORLD_SIZE", 1)
     local_rank = _env_int("LOCAL_RANK", 0)
     if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # FIR_DIST_BACKEND=gloo rehearses the N>1 flow on a box with fewer GPUs than ranks (ranks
     # share devices, halos staged through the host); the real multi-GPU run uses nccl (= RCCL).
-    backend = os.environ.get("FIR_DIST_BACKEND", "nccl")
+    # Started under torchrun with more ranks than GPUs, the same rehearsal is chosen here.
+    backend = os.environ.get("FIR_DIST_BACKEND", "")
+    if not backend:
+        backend = "nccl" if world == 1 or torch.cuda.device_count() >= world else "gloo"
+        if backend == "gloo":
+            os.environ["FIR_BENCH_REHEARSAL"] = f"{world} ranks on {torch.cuda.device_count()} GPU(s)"
     dev_index = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
@@ -441,17 +526,20 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # Roofline: the dominant kernel alone (wl.dominant), `steps` back-to-back launches on the stream it
-    # runs on, bracketed by two HIP events (events between launches would perturb the stream:
-    # each record adds a ~11 us gap).  Average duration = event time / launches.
+    # Roofline: the dominant kernel alone (wl.dominant), ROOF_RAMP untimed launches (clocks ramp over
+    # ~40) then ROOF_LAUNCHES back-to-back launches on the stream it runs on, bracketed by two HIP
+    # events (events between launches would perturb the stream: each record adds a ~11 us gap).
+    # Average duration = event time / launches.  Independent of --steps / --warmup.
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(ROOF_RAMP):
+        wl.dominant()
     torch.cuda.synchronize()
     ev0.record()
-    for _ in range(args.steps):
+    for _ in range(ROOF_LAUNCHES):
         wl.dominant()
     ev1.record()
     ev1.synchronize()
-    kern_avg_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
+    kern_avg_s = ev0.elapsed_time(ev1) / 1e3 / ROOF_LAUNCHES
 
     wl.step()  # restore the full step's output (the loop above ran the bulk kernel alone)
     torch.cuda.synchronize()
@@ -468,8 +556,9 @@ def main() -> int:
             ok = int(f.item()) == 0
         parity = "bit-exact vs oracle (full output, every rank)" if ok else "MISMATCH"
 
+    # CPU legs: rank 0 only, at every N, after the GPU legs (the other ranks wait at the barrier below)
     cpu = cpu_np = cpu_np_mt = cpu_loop = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    if rank == 0 and args.cpu_seconds > 0:
         nthr = _cpu_threads()
         wl.oracle(nthr)  # warm (page-in, thread pool)
         reps, tc0 = 0, time.perf_counter()
@@ -511,6 +600,8 @@ def main() -> int:
                         "sample": f"the reference's per-sample x per-tap Python loop (oracle.fir1d_loop, "
                                   f"fir_1d_fixed_ref.py:94-128) on the first {m} samples, {tl:.2f} s"}
 
+    barrier()  # rank 0's CPU legs are done
+
     traffic = None
     pmc = ROOT / "profiles" / f"pmc_{args.workload}{'_gen5x5' if wl.gen2d else ''}.json"
     if pmc.exists():
@@ -548,7 +639,8 @@ def main() -> int:
                                  "strips share are read once, PMC 1.001x; DESIGN.md §5)")
                      if args.workload == "fir2d_u8" else "HBM",
                      "kernel_avg_us": round(kern_avg_s * 1e6, 2), "algorithmic_bytes_per_launch": alg_bytes,
-                     "timing": f"HIP events around {args.steps} back-to-back launches of the kernel"},
+                     "timing": f"HIP events around {ROOF_LAUNCHES} back-to-back launches of the kernel after "
+                               f"{ROOF_RAMP} untimed ones"},
         "cpu_baseline": cpu,
         "cpu_baseline_numpy": cpu_np,
         "cpu_baseline_numpy_threads": cpu_np_mt,
@@ -556,11 +648,15 @@ def main() -> int:
         "parity": parity,
         "host_issue_us_per_step": round(t_issue / args.steps * 1e6, 1),
     }
+    if os.environ.get("FIR_BENCH_REHEARSAL"):
+        line["config"] = dict(line["config"], rehearsal=(
+            f"{os.environ['FIR_BENCH_REHEARSAL']}: gloo process group, ranks share the GPU's HBM; not a "
+            "scaling number"))
     if wl.sharded_1d and world == 1:
-        line["config"] = dict(wl.config, rehearsal="FIR_SELF_HALO=1: RCCL halo exchange with itself every step "
-                                                    "(ring of one) + edge kernel")
+        line["config"] = dict(wl.config, rehearsal=f"FIR_SELF_HALO=1: {wl.halo_kind} halo hand-off with itself every "
+                                                    f"step (ring of one), gate mode {GATE_MODE}")
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        emit_result(json.dumps(line))
     if dist.is_initialized():
         torch.cuda.synchronize()
         barrier()  # no rank unmaps or frees its segment while a neighbour may still read it

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define FIR_HIP_ABI_VERSION 3
+#define FIR_HIP_ABI_VERSION 4
 /* Tap counts: any length up to FIR_MAX_TAPS (1-D taps; 2-D tap_rows * tap_cols), like the
  * reference's Python loop (fir_1d_fixed_ref.py:83-107, fir_1d_ref.py:49-63).  Sums are exact in
  * 64 bits: mod 2^64 for acc_bits < 64; with acc_bits >= 64 (no wrap) sum|hq| * max|x| must stay
@@ -160,16 +160,24 @@ int fir1d_ideal_rows_dev(const uint8_t* x_dev, int64_t rows, int64_t width, cons
                          int taps, double* y_dev, void* stream);
 
 /* ---- fixed-vs-ideal comparison metrics -----------------------------
- * One pass over `n` samples of ideal (float64) and fixed (uint8) outputs.  out[9] =
+ * One pass over `n` samples of ideal (float64) and fixed outputs of `fixed_dtype` (the
+ * reference takes any dtype: y_fixed.astype(np.float64), gen_3tap_compare_report.py:84-86;
+ * its fixed stage writes uint8, FIR_DT_U8 is the bandwidth path).  out[9] =
  * {max|d|, sum|d|, sum d^2, sum d, #(fixed==0), #(fixed==255), #(ideal<0 or >255), n, 0}
- * with d = fixed - ideal; the report ratios are these over n.  The float64 sums are added in
- * NumPy's order (8192-sample blocks summed pairwise, block sums in order), so they equal the
- * reference's np.mean values bit for bit; counts and max are exact.  `work_dev` of the _dev
- * form holds at least fir_metrics_work_bytes(n) bytes (ABI 3: the size depends on n). */
+ * with d = float64(fixed) - ideal; the report ratios are these over n.  The float64 sums are
+ * added in NumPy's order (8192-sample blocks summed pairwise, block sums in order), so they equal
+ * the reference's np.mean values bit for bit; counts are exact; max|d| is NaN when any |d| is
+ * (np.max propagates NaN).  `work_dev` of the _dev form holds at least fir_metrics_work_bytes(n)
+ * bytes.  ABI 4: the fixed dtype argument. */
+typedef enum {
+    FIR_DT_U8 = 0, FIR_DT_I8 = 1, FIR_DT_U16 = 2, FIR_DT_I16 = 3, FIR_DT_U32 = 4, FIR_DT_I32 = 5,
+    FIR_DT_U64 = 6, FIR_DT_I64 = 7, FIR_DT_F16 = 8, FIR_DT_F32 = 9, FIR_DT_F64 = 10
+} fir_num_dtype;
 int64_t fir_metrics_work_bytes(int64_t n);
-int fir_compare_metrics(const double* ideal, const uint8_t* fixed, int64_t n, double* out, int device);
-int fir_compare_metrics_dev(const double* ideal_dev, const uint8_t* fixed_dev, int64_t n, double* out_dev,
-                            void* work_dev, void* stream);
+int fir_compare_metrics(const double* ideal, const void* fixed, int fixed_dtype, int64_t n, double* out,
+                        int device);
+int fir_compare_metrics_dev(const double* ideal_dev, const void* fixed_dev, int fixed_dtype, int64_t n,
+                            double* out_dev, void* work_dev, void* stream);
 
 /* ---- restore-stage u8 conversion -----------------------------------
  * out[i] = u8 of a[i] (float64), n samples:
@@ -226,11 +234,15 @@ int fir_peek(const void* dev_ptr, void* host_out, int64_t bytes);
  * touched by device atomics (performed at the memory side: coherent across XCDs and xGMI).
  * All ranks of a ring must use the same halo sizes and call the gate once per step.
  * fir_halo_mailbox_bytes: size of one mailbox; fir_halo_mailbox_init_dev: zero it on `stream`
- * (before it is exported; every rank's init must complete before any neighbour's first gate).
- * Mailboxes must be 128-byte aligned. */
+ * and record the halo sizes its slots are laid out for (before it is exported; every rank's init
+ * must complete before any neighbour's first gate).  A gate whose own or neighbours' mailboxes
+ * were laid out for other halo sizes touches no slot: *status_dev = FIR_GATE_LAYOUT, halos zero.
+ * Mailboxes must be 128-byte aligned; halo sizes below 2^31 bytes. */
 #define FIR_GATE_TIMEOUT 1
+#define FIR_GATE_LAYOUT 2
 int64_t fir_halo_mailbox_bytes(int64_t halo_left_bytes, int64_t halo_right_bytes);
-int fir_halo_mailbox_init_dev(void* mailbox_dev, int64_t bytes, void* stream);
+int fir_halo_mailbox_init_dev(void* mailbox_dev, int64_t bytes, int64_t halo_left_bytes, int64_t halo_right_bytes,
+                              void* stream);
 int fir_halo_gate_dev(const void* x_dev, int64_t seg_bytes, int64_t halo_left_bytes, int64_t halo_right_bytes,
                       void* mailbox_dev, const void* left_mailbox_dev, const void* right_mailbox_dev,
                       void* halo_left_dev, void* halo_right_dev, int32_t* status_dev, double timeout_s,

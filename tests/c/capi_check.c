@@ -80,7 +80,7 @@ int main(void) {
         const double hd[3] = {0.25, 0.5, 0.25};
         expect(fir1d_ideal_rows(x8, rows, w, hd, 3, yd, 0) == FIR_OK, "ideal");
         double m[9];
-        expect(fir_compare_metrics(yd, x8, n, m, 0) == FIR_OK, "metrics");
+        expect(fir_compare_metrics(yd, x8, FIR_DT_U8, n, m, 0) == FIR_OK, "metrics");
         expect(fir_restore_u8(yd, n, FIR_RESTORE_NORMALIZE, y8, 0) == FIR_OK, "restore");
         const int32_t k2[9] = {1, 2, 1, 2, 4, 2, 1, 2, 1};
         expect(fir2d_fixed(x8, rows, w, k2, 3, 3, 4, 32, FIR_OUT_U8_SAT, y8, 0) == FIR_OK, "2d");

@@ -71,6 +71,34 @@ def load_image_outputs() -> dict:
     return json.loads((GOLDEN / "image_outputs.json").read_text())
 
 
+def load_metrics_dtypes():
+    """[(name, ideal, fixed, reference metrics)] of metrics_dtypes.{npz,json}; floats decoded from
+    hex, NaN as float('nan')."""
+    recs = json.loads((GOLDEN / "metrics_dtypes.json").read_text())
+    with np.load(GOLDEN / "metrics_dtypes.npz") as d:
+        out = []
+        for r in recs:
+            m = {k: (v if isinstance(v, int) else (float("nan") if v == "nan" else float.fromhex(v)))
+                 for k, v in r["metrics"].items()}
+            out.append((r["name"], d[r["name"] + "__ideal"], d[r["name"] + "__fixed"], m))
+    return out
+
+
+def same_metrics(got: dict, want: dict) -> list[str]:
+    """Keys whose values differ bit for bit (NaN equals NaN)."""
+    import math
+
+    bad = []
+    for k, w in want.items():
+        g = got[k]
+        if isinstance(w, float) and math.isnan(w):
+            if not (isinstance(g, float) and math.isnan(g)):
+                bad.append(k)
+        elif g != w or (isinstance(w, float) and math.copysign(1.0, g) != math.copysign(1.0, w)):
+            bad.append(k)
+    return bad
+
+
 @pytest.fixture(scope="session")
 def images():
     return load_images()

@@ -24,6 +24,9 @@ Files written:
   small_image_outputs.npz            full fixed/ideal outputs of the two 64x64 cases
   restore_u8.npz                     restore conversions (clip / normalize) of the 16 small
                                      ideal outputs and of edge-case arrays (ties, +-0, range ends)
+  metrics_dtypes.npz/.json           _compute_metrics on fixed arrays of every dtype it accepts
+                                     (int8..uint64, float16/32/64, bool; NaN/inf/-0.0, values
+                                     outside [0, 255]) with the reference's outputs
   long_taps.npz                      long filters (257 / 1000 / 2048 / 4099 taps, shorter and
                                      longer than x): fir_1d_fixed_golden and fir_1d_ideal outputs
   meta.json                          generator environment
@@ -325,6 +328,64 @@ def gen_restore():
     return len(arrays)
 
 
+def _metrics_cases(rng):
+    """(name, ideal, fixed) pairs for _compute_metrics beyond the u8 fixed stage: every dtype its
+    astype(np.float64) accepts, values outside [0, 255], NaN / inf / -0.0, sizes across the
+    8192-sample block boundary (NumPy's summation buffer) with a ragged tail."""
+    n1, n2 = 1000, 2 * 8192 + 77
+    cases = []
+
+    def ideal(n, lo=-64.0, hi=320.0):
+        return rng.uniform(lo, hi, n)
+
+    cases.append(("i16_wide", ideal(n2), rng.integers(-300, 600, n2).astype(np.int16)))
+    cases.append(("i16_small", ideal(n1), rng.integers(-2, 260, n1).astype(np.int16)))
+    cases.append(("i32_full", ideal(n2, -3e9, 3e9), rng.integers(-(1 << 31), 1 << 31, n2, dtype=np.int64).astype(np.int32)))
+    cases.append(("i8", ideal(n1, -200.0, 200.0), rng.integers(-128, 128, n1).astype(np.int8)))
+    cases.append(("u16", ideal(n2, 0.0, 70000.0), rng.integers(0, 65536, n2).astype(np.uint16)))
+    cases.append(("u32", ideal(n1, 0.0, 5e9), rng.integers(0, 1 << 32, n1, dtype=np.uint64).astype(np.uint32)))
+    big = rng.integers(-(1 << 62), 1 << 62, n1, dtype=np.int64)
+    big[:8] = [0, 255, -1, (1 << 53) + 1, (1 << 53) + 3, -(1 << 53) - 1, (1 << 63) - 1, -(1 << 63)]
+    cases.append(("i64_rounding", ideal(n1, -1e18, 1e18), big))
+    ubig = rng.integers(0, 1 << 63, n1, dtype=np.uint64) * np.uint64(2) + np.uint64(1)
+    ubig[:4] = [0, 255, (1 << 64) - 1, (1 << 53) + 1]
+    cases.append(("u64_rounding", ideal(n1, 0.0, 1.9e19), ubig))
+    f32 = rng.uniform(-300.0, 600.0, n2).astype(np.float32)
+    f32[:6] = [np.nan, -0.0, 0.0, 255.0, np.inf, -np.inf]
+    cases.append(("f32_specials", ideal(n2), f32))
+    f64 = np.rint(rng.uniform(-10.0, 270.0, n2))
+    f64[100:110] = -0.0
+    cases.append(("f64_rounded", ideal(n2), f64))
+    cases.append(("f16", ideal(n1), rng.uniform(-300.0, 600.0, n1).astype(np.float16)))
+    cases.append(("bool", ideal(n1, -1.0, 2.0), rng.integers(0, 2, n1).astype(bool)))
+    yi = ideal(n2)
+    yi[5000] = np.nan  # np.max propagates NaN; the means become NaN too
+    cases.append(("u8_nan_ideal", yi, rng.integers(0, 256, n2).astype(np.uint8)))
+    yi = ideal(n1)
+    yi[[3, 700]] = [np.inf, -np.inf]
+    cases.append(("u8_inf_ideal", yi, rng.integers(0, 256, n1).astype(np.uint8)))
+    cases.append(("f64_negzero_all", np.zeros(n2), np.full(n2, -0.0)))
+    cases.append(("i16_2d", ideal(37 * 53).reshape(37, 53), rng.integers(-300, 600, (37, 53)).astype(np.int16)))
+    return cases
+
+
+def gen_metrics_dtypes(rep, seed=8486):
+    """metrics_dtypes.npz (inputs) + metrics_dtypes.json (the reference's _compute_metrics
+    outputs, floats as exact hex; NaN as 'nan')."""
+    rng = np.random.default_rng(seed)
+    arrays, recs = {}, []
+    for name, yi, yf in _metrics_cases(rng):
+        arrays[f"{name}__ideal"] = yi
+        arrays[f"{name}__fixed"] = yf
+        m = rep._compute_metrics(yi, yf)
+        recs.append({"name": name, "fixed_dtype": str(yf.dtype),
+                     "metrics": {k: (v if isinstance(v, int) else ("nan" if math.isnan(v) else _enc_float(v)))
+                                 for k, v in m.items()}})
+    np.savez_compressed(OUT / "metrics_dtypes.npz", **arrays)
+    (OUT / "metrics_dtypes.json").write_text(json.dumps(recs, indent=1) + "\n")
+    return len(recs)
+
+
 # (L, n, frac, acc, coeff, tap scale): every tap count the reference accepts is a legal input
 # (its loop runs over any len(h), fir_1d_fixed_ref.py:83-107; fir_1d_ref.py:49-63)
 LONG_FIXED = [(257, 3000, 12, 32, 16, 1e-2), (257, 50, 4, 32, 8, 1e-1), (1000, 2000, 20, 48, 32, 1e-3),
@@ -377,11 +438,15 @@ def main():
     ap.add_argument("--skip-images", action="store_true")
     ap.add_argument("--only-restore", action="store_true")
     ap.add_argument("--only-long", action="store_true")
+    ap.add_argument("--only-metrics", action="store_true")
     args = ap.parse_args()
     if args.only_restore:
         print("restore", gen_restore())
         return
-    fixed_ref, ideal_ref, *_ = _ref_imports()
+    fixed_ref, ideal_ref, _gf, _gi, _gv, rep, _h = _ref_imports()
+    if args.only_metrics:
+        print("metrics_dtypes", gen_metrics_dtypes(rep))
+        return
     if args.only_long:
         print("long_taps", gen_long_taps(fixed_ref, ideal_ref))
         return
@@ -395,6 +460,7 @@ def main():
         print("images", gen_images(args.jobs))
     print("restore", gen_restore())
     print("long_taps", gen_long_taps(fixed_ref, ideal_ref))
+    print("metrics_dtypes", gen_metrics_dtypes(rep))
     (OUT / "meta.json").write_text(json.dumps(meta, indent=1) + "\n")
 
 

@@ -1,0 +1,100 @@
+"""bench.py's N > 1 self-launch (CPU, no GPU): `python bench.py --gpus N` started directly
+spawns N ranks under torch.distributed.run as a child process, forwards rank 0's ONE JSON line
+and exits with the ranks' status.  A stub rank script (gloo, CPU only) stands in for the GPU
+workload; the launcher function is bench.launch_ranks itself."""
+from __future__ import annotations
+
+import json
+import subprocess
+import sys
+import textwrap
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+STUB = textwrap.dedent("""
+    import json, os, sys
+    import torch, torch.distributed as dist
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    t = torch.tensor([float(rank + 1)])
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)   # the bench's max-over-ranks timing
+    print(f"rank {rank} noise on stdout")      # not a result line: goes to stderr
+    if rank == 0:   # bench.emit_result's protocol
+        line = json.dumps({"metric": "stub", "value": float(t.item()), "n_gpus": world,
+                           "argv": sys.argv[1:], "backend": os.environ.get("FIR_DIST_BACKEND")})
+        open(os.environ["FIR_BENCH_RESULT"], "w").write(line + "\\n")
+    dist.barrier()
+    dist.destroy_process_group()
+    sys.exit(int(os.environ.get("STUB_EXIT_RANK", "-1")) == rank)
+""")
+
+
+@pytest.fixture(scope="module")
+def bench():
+    sys.path.insert(0, str(ROOT))
+    import bench as b
+
+    return b
+
+
+def _run(bench, tmp_path, n, env_extra=None, capsys=None):
+    stub = tmp_path / "stub_rank.py"
+    stub.write_text(STUB)
+    import os
+
+    env = dict(os.environ, FIR_DIST_BACKEND="gloo", **(env_extra or {}))
+    return bench.launch_ranks(n, str(stub), ["--gpus", str(n), "--steps", "3"], env)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_launch_ranks_forwards_rank0_line(bench, tmp_path, capfd, n):
+    rc = _run(bench, tmp_path, n)
+    out, err = capfd.readouterr()
+    assert rc == 0
+    lines = [ln for ln in out.splitlines() if ln.strip()]
+    assert len(lines) == 1, out  # exactly one JSON line on stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == n and rec["value"] == float(n)  # the all-reduce saw every rank
+    assert rec["argv"] == ["--gpus", str(n), "--steps", "3"]
+    assert "rank 0 noise on stdout" in err and "rank 1 noise on stdout" in err  # ranks' stdout -> stderr
+
+
+def test_launch_ranks_fails_when_a_rank_fails(bench, tmp_path, capfd):
+    rc = _run(bench, tmp_path, 2, {"STUB_EXIT_RANK": "1"})
+    capfd.readouterr()
+    assert rc != 0
+
+
+def test_bench_main_self_launches_before_any_gpu_call(bench, monkeypatch):
+    """`--gpus 2` without WORLD_SIZE goes to launch_ranks with the same argv, choosing the gloo
+    rehearsal when the host has fewer GPUs than ranks (here: none)."""
+    calls = []
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.delenv("FIR_DIST_BACKEND", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "7", "--warmup", "1"])
+    monkeypatch.setattr(bench, "launch_ranks", lambda n, script, argv, env: calls.append((n, script, argv, env)) or 0)
+    assert bench.main() == 0
+    (n, script, argv, env), = calls
+    assert n == 2 and Path(script).name == "bench.py"
+    assert argv == ["--gpus", "2", "--steps", "7", "--warmup", "1"]
+    assert env["FIR_DIST_BACKEND"] == "gloo" and "2 ranks" in env["FIR_BENCH_REHEARSAL"]
+
+
+def test_bench_rejects_world_mismatch(bench, monkeypatch):
+    monkeypatch.setenv("WORLD_SIZE", "3")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    with pytest.raises(SystemExit, match="WORLD_SIZE=3"):
+        bench.main()
+
+
+def test_bench_script_runs_launcher_end_to_end(tmp_path):
+    """The real entry: `python bench.py --gpus 2` on a host without GPUs spawns 2 ranks; each
+    fails at its first GPU call (no device here), so the parent exits non-zero and prints no
+    result line — the launcher neither hangs nor claims a result."""
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
+                        "--cpu-seconds", "0"], capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0
+    assert p.stdout == ""

@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.fir_abi_version() == fir_hip.ABI_VERSION == 3
+    assert lib.fir_abi_version() == fir_hip.ABI_VERSION == 4
 
 
 def test_invalid_arguments_are_rejected_without_device(lib):

@@ -44,6 +44,35 @@ def test_metrics_kernel_matches_reference_metrics(images, image_outputs):
         _check_metrics(fir_hip.compare_metrics(yi, yf), o["metrics"], o["case_stem"])
 
 
+def test_metrics_every_fixed_dtype_matches_reference():
+    """The reference's _compute_metrics takes any fixed dtype (astype(np.float64),
+    gen_3tap_compare_report.py:84-86): int8..uint64, float16/32/64 and bool fixed arrays, values
+    outside [0, 255], NaN / inf / -0.0 (np.max propagates NaN), against the reference's own
+    outputs (tests/golden/metrics_dtypes.*), bit for bit."""
+    from conftest import load_metrics_dtypes, same_metrics
+
+    for name, yi, yf, want in load_metrics_dtypes():
+        got = fir_hip.compare_metrics(yi, yf)
+        assert not same_metrics(got, want), (name, {k: (got[k], want[k]) for k in same_metrics(got, want)})
+
+
+def test_metrics_dev_fixed_dtypes():
+    """torch_ops.compare_metrics_dev with int16 / float32 / bool fixed tensors = the oracle."""
+    import torch
+
+    from conftest import same_metrics
+    from fir_hip import torch_ops
+
+    rng = np.random.default_rng(77)
+    n = 3 * 8192 + 11
+    yi = rng.uniform(-64.0, 320.0, n)
+    for yf in (rng.integers(-300, 600, n).astype(np.int16), rng.uniform(-9.0, 300.0, n).astype(np.float32),
+               rng.integers(0, 2, n).astype(bool), rng.integers(0, 256, n).astype(np.uint8)):
+        sums = torch_ops.compare_metrics_dev(torch.from_numpy(yi).cuda(), torch.from_numpy(yf).cuda())
+        got = fir_hip.metrics_from_sums(sums.cpu().numpy(), n)
+        assert not same_metrics(got, fo.compute_metrics(yi, yf)), yf.dtype
+
+
 def test_metrics_edge_cases():
     assert fir_hip.compare_metrics(np.zeros(0), np.zeros(0, np.uint8))["num_samples"] == 0
     rng = np.random.default_rng(1)

@@ -223,7 +223,7 @@ def test_xgmi_peer_halos_across_processes(world, taps, ch):
 
 def _gate_buffers(hl_bytes, hr_bytes):
     mb = torch.empty(fir_hip.halo_mailbox_bytes(hl_bytes, hr_bytes), dtype=torch.uint8, device=DEV)
-    return torch_ops.halo_mailbox_init_dev(mb)
+    return torch_ops.halo_mailbox_init_dev(mb, hl_bytes, hr_bytes)
 
 
 def test_halo_gate_two_streams_and_timeout():

@@ -53,6 +53,18 @@ for s in $STEPS; do
                      --output-format csv -- python bench.py --workload "$wl" --steps 10 --warmup 2 --cpu-seconds 0 \
                      --no-parity; fatal $? || exit
              done ;;
+        pytestsub) run pytest_sub 600 python -u -m pytest -x -q -p no:cacheprovider --timeout 120 \
+                 --timeout-method thread ${PYTEST_FILES}; fatal $? ;;
+        benchdrv) run bench_drv 300 python bench.py --gpus 1 --steps 20 --warmup 5; fatal $? ;;
+        launch2|launch4) n=${s#launch}
+             run "launch$n" 400 python bench.py --gpus "$n" --steps 20 --warmup 5; fatal $? ;;
+        self_serial|self_overlap) m=${s#self_}
+             run "self_$m" 300 env FIR_SELF_HALO=1 FIR_HALO=xgmi FIR_GATE_MODE=$m python bench.py --cpu-seconds 0; fatal $? ;;
+        self_rccl) run self_rccl 300 env FIR_SELF_HALO=1 FIR_HALO=rccl python bench.py --cpu-seconds 0; fatal $? ;;
+        profself_serial|profself_overlap) m=${s#profself_}
+             run "profself_$m" 300 env FIR_SELF_HALO=1 FIR_HALO=xgmi FIR_GATE_MODE=$m rocprofv3 --kernel-trace --stats \
+                 -d "$OUT/profself_$m" -o run --output-format csv -- python bench.py --steps 200 --warmup 100 \
+                 --cpu-seconds 0 --no-parity; fatal $? ;;
         asan) run asan 600 make -C warmup-fir-filter_amd/csrc asan-check; fatal $? ;;
         micro) run micro 300 tools/microbench/fir_micro 28 20; fatal $? ;;
         micro2d) run micro2d 300 tools/microbench/fir2d_micro 15; fatal $? ;;

@@ -647,16 +647,19 @@ int fir1d_ideal_rows_dev(const uint8_t* x_dev, int64_t rows, int64_t width, cons
 
 int64_t fir_metrics_work_bytes(int64_t n) { return (int64_t)fir::metrics_work_bytes(n); }
 
-int fir_compare_metrics(const double* ideal, const uint8_t* fixed, int64_t n, double* out, int device) {
+int fir_compare_metrics(const double* ideal, const void* fixed, int fixed_dtype, int64_t n, double* out,
+                        int device) {
     try {
         if (n < 0 || !out || (n > 0 && (!ideal || !fixed))) return fail(FIR_EINVAL, "invalid arguments");
+        const int es = fir::metrics_dtype_size(fixed_dtype);
+        if (!es) return fail(FIR_EINVAL, "unknown fixed dtype");
         DeviceRestore restore;
         DeviceState* st = nullptr;
         int rc = device_state(device, &st);
         if (rc) return rc;
         std::lock_guard<std::mutex> lk(st->mu);
         if ((rc = init_locked(st, device))) return rc;
-        const size_t ib = (size_t)n * 8, fb = (size_t)n;
+        const size_t ib = (size_t)n * 8, fb = (size_t)n * es;
         const size_t fo = (ib + 255) / 256 * 256;
         if ((rc = ensure(st->in, fo + fb + 1)) || (rc = ensure(st->out, fir::metrics_work_bytes(n) + 256))) return rc;
         char* din = (char*)st->in.ptr;
@@ -666,7 +669,7 @@ int fir_compare_metrics(const double* ideal, const uint8_t* fixed, int64_t n, do
         }
         double* dout = (double*)st->out.ptr;
         std::string err;
-        rc = fir::launch_metrics((const double*)din, (const uint8_t*)(din + fo), n, dout, (char*)st->out.ptr + 256,
+        rc = fir::launch_metrics((const double*)din, din + fo, fixed_dtype, n, dout, (char*)st->out.ptr + 256,
                                  st->stream, &err);
         if (rc) {
             (void)hipStreamSynchronize(st->stream);
@@ -680,11 +683,11 @@ int fir_compare_metrics(const double* ideal, const uint8_t* fixed, int64_t n, do
     }
 }
 
-int fir_compare_metrics_dev(const double* ideal_dev, const uint8_t* fixed_dev, int64_t n, double* out_dev,
-                            void* work_dev, void* stream) {
+int fir_compare_metrics_dev(const double* ideal_dev, const void* fixed_dev, int fixed_dtype, int64_t n,
+                            double* out_dev, void* work_dev, void* stream) {
     try {
         std::string err;
-        int rc = fir::launch_metrics(ideal_dev, fixed_dev, n, out_dev, work_dev, (hipStream_t)stream, &err);
+        int rc = fir::launch_metrics(ideal_dev, fixed_dev, fixed_dtype, n, out_dev, work_dev, (hipStream_t)stream, &err);
         return rc ? fail(rc, err) : FIR_OK;
     } catch (...) {
         return fail(FIR_EHIP, "internal error");
@@ -850,10 +853,12 @@ int64_t fir_halo_mailbox_bytes(int64_t halo_left_bytes, int64_t halo_right_bytes
     return fir::halo_mailbox_bytes(halo_left_bytes, halo_right_bytes);
 }
 
-int fir_halo_mailbox_init_dev(void* mailbox_dev, int64_t bytes, void* stream) {
+int fir_halo_mailbox_init_dev(void* mailbox_dev, int64_t bytes, int64_t halo_left_bytes, int64_t halo_right_bytes,
+                              void* stream) {
     try {
         std::string err;
-        int rc = fir::launch_halo_mailbox_init(mailbox_dev, bytes, (hipStream_t)stream, &err);
+        int rc = fir::launch_halo_mailbox_init(mailbox_dev, bytes, halo_left_bytes, halo_right_bytes,
+                                               (hipStream_t)stream, &err);
         return rc ? fail(rc, err) : FIR_OK;
     } catch (...) {
         return fail(FIR_EHIP, "internal error");

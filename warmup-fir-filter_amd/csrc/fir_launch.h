@@ -50,7 +50,8 @@ int launch_fir1d_segment(const void* x, int in_dtype, int64_t n, int ch, const i
 // the one-wave gate kernel (publish own edges, wait for both neighbours' epoch, copy their
 // edges into the local halo buffers).
 int64_t halo_mailbox_bytes(int64_t hl_bytes, int64_t hr_bytes);
-int launch_halo_mailbox_init(void* mailbox, int64_t bytes, hipStream_t stream, std::string* err);
+int launch_halo_mailbox_init(void* mailbox, int64_t bytes, int64_t hl_bytes, int64_t hr_bytes, hipStream_t stream,
+                             std::string* err);
 int launch_halo_gate(const void* x, int64_t seg_bytes, int64_t hl_bytes, int64_t hr_bytes, void* mailbox,
                      const void* left_mailbox, const void* right_mailbox, void* halo_left, void* halo_right,
                      int32_t* status, double timeout_s, hipStream_t stream, std::string* err);
@@ -69,7 +70,8 @@ int launch_fir1d_ideal(const uint8_t* x, int64_t rows, int64_t width, const doub
 
 // Fixed-vs-ideal comparison metrics (one pass); `work` >= metrics_work_bytes(n).
 size_t metrics_work_bytes(int64_t n);
-int launch_metrics(const double* ideal, const uint8_t* fixed, int64_t n, double* out, void* work,
+int metrics_dtype_size(int fixed_dtype);  // bytes per element of a fir_num_dtype, 0 if unknown
+int launch_metrics(const double* ideal, const void* fixed, int fixed_dtype, int64_t n, double* out, void* work,
                    hipStream_t stream, std::string* err);
 
 // f64 -> u8 restore conversion (FIR_RESTORE_*); `work` >= restore_work_bytes() for normalize.

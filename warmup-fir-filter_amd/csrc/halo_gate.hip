@@ -31,6 +31,9 @@
 // Mailbox layout (dwords; every field starts a 128-byte line):
 //   [0]            the owner's gate count (steps published so far)
 //   [1]            status: 0 ok, FIR_GATE_TIMEOUT after a wait gave up (later gates skip waiting)
+//   [2], [3]       the halo sizes (HL, HR bytes) the slots are laid out for, written at init; a gate
+//                  compares its own sizes with its mailbox's and both neighbours' before it
+//                  computes any slot address (a mismatch would index past a smaller mailbox)
 //   slot s at dword 32 + s * slot_dw:   [0] epoch, [32 ..] head (HR samples), then tail (HL samples)
 #include <algorithm>
 #include <string>
@@ -92,11 +95,23 @@ __global__ __launch_bounds__(kWave) void halo_gate_kernel(const uint8_t* __restr
     const uint32_t head0 = kGateLine, tail0 = kGateLine + gate_round_dw(hr_bytes);
     const int64_t hr_dw = (hr_bytes + 3) / 4, hl_dw = (hl_bytes + 3) / 4;
 
-    // lane 0 reads the gate count and status (the same for every lane after the broadcast)
-    uint32_t cnt = 0, status = 0;
+    // lane 0 reads the gate count and status (the same for every lane after the broadcast), and
+    // checks that every mailbox this gate indexes is laid out for its halo sizes
+    uint32_t cnt = 0, status = 0, layout_ok = 1;
     if (lane == 0) {
+        const uint32_t* mbs[3] = {own, left, right};
+        for (int m = 0; m < 3; ++m)
+            if (mbs[m] && (mb_read(&mbs[m][2], zero) != (uint32_t)hl_bytes || mb_read(&mbs[m][3], zero) != (uint32_t)hr_bytes))
+                layout_ok = 0;
         cnt = mb_read(&own[0], zero);
         status = mb_read(&own[1], zero);
+    }
+    layout_ok = __shfl(layout_ok, 0);
+    if (!layout_ok) {  // no slot is touched; the halos are zeroed
+        if (lane == 0 && status_out) *status_out = (int32_t)FIR_GATE_LAYOUT;
+        for (int64_t i = lane; out_l && i < hl_bytes; i += kWave) out_l[i] = 0;
+        for (int64_t i = lane; out_r && i < hr_bytes; i += kWave) out_r[i] = 0;
+        return;
     }
     cnt = __shfl(cnt, 0);
     status = __shfl(status, 0);
@@ -150,9 +165,10 @@ __global__ __launch_bounds__(kWave) void halo_gate_kernel(const uint8_t* __restr
     if (sink == 0x9E3779B9u && seg_bytes < 0 && status_out) *status_out = (int32_t)sink;
 }
 
-__global__ __launch_bounds__(kBlock) void halo_mailbox_init_kernel(uint32_t* mb, int64_t ndw) {
+__global__ __launch_bounds__(kBlock) void halo_mailbox_init_kernel(uint32_t* mb, int64_t ndw, uint32_t hl_bytes,
+                                                                   uint32_t hr_bytes) {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < ndw; i += (int64_t)gridDim.x * kBlock)
-        (void)mb_write(&mb[i], 0u);
+        (void)mb_write(&mb[i], i == 2 ? hl_bytes : i == 3 ? hr_bytes : 0u);
 }
 
 }  // namespace
@@ -161,12 +177,17 @@ int64_t halo_mailbox_bytes(int64_t hl_bytes, int64_t hr_bytes) {
     return 4 * (32 + 2 * (int64_t)gate_slot_dw(hl_bytes, hr_bytes));
 }
 
-int launch_halo_mailbox_init(void* mailbox, int64_t bytes, hipStream_t stream, std::string* err) {
-    if (!mailbox || bytes < 128 || bytes % 4) return *err = "mailbox must be >= 128 bytes, a multiple of 4", FIR_EINVAL;
+int launch_halo_mailbox_init(void* mailbox, int64_t bytes, int64_t hl_bytes, int64_t hr_bytes, hipStream_t stream,
+                             std::string* err) {
+    if (hl_bytes < 0 || hr_bytes < 0 || hl_bytes >= (1ll << 31) || hr_bytes >= (1ll << 31))
+        return *err = "halo byte counts must be in [0, 2^31)", FIR_EINVAL;
+    if (!mailbox || bytes < halo_mailbox_bytes(hl_bytes, hr_bytes) || bytes % 4)
+        return *err = "mailbox must hold fir_halo_mailbox_bytes(halo sizes) bytes, a multiple of 4", FIR_EINVAL;
     if ((uintptr_t)mailbox % 128) return *err = "mailbox must be 128-byte aligned", FIR_EINVAL;
     const int64_t ndw = bytes / 4;
     const int64_t blocks = std::min<int64_t>((ndw + kBlock - 1) / kBlock, 1024);
-    hipLaunchKernelGGL(halo_mailbox_init_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, (uint32_t*)mailbox, ndw);
+    hipLaunchKernelGGL(halo_mailbox_init_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, (uint32_t*)mailbox, ndw,
+                       (uint32_t)hl_bytes, (uint32_t)hr_bytes);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return *err = std::string("halo mailbox init launch failed: ") + hipGetErrorString(e), FIR_EHIP;
     return FIR_OK;
@@ -175,8 +196,9 @@ int launch_halo_mailbox_init(void* mailbox, int64_t bytes, hipStream_t stream, s
 int launch_halo_gate(const void* x, int64_t seg_bytes, int64_t hl_bytes, int64_t hr_bytes, void* mailbox,
                      const void* left_mailbox, const void* right_mailbox, void* halo_left, void* halo_right,
                      int32_t* status, double timeout_s, hipStream_t stream, std::string* err) {
-    if (hl_bytes < 0 || hr_bytes < 0 || seg_bytes < hl_bytes || seg_bytes < hr_bytes)
-        return *err = "halo byte counts must be in [0, seg_bytes]", FIR_EINVAL;
+    if (hl_bytes < 0 || hr_bytes < 0 || seg_bytes < hl_bytes || seg_bytes < hr_bytes || hl_bytes >= (1ll << 31) ||
+        hr_bytes >= (1ll << 31))
+        return *err = "halo byte counts must be in [0, min(seg_bytes, 2^31 - 1)]", FIR_EINVAL;
     if (!mailbox) return *err = "mailbox must not be NULL", FIR_EINVAL;
     if ((!x && (hl_bytes || hr_bytes)) || (left_mailbox && hl_bytes && !halo_left) ||
         (right_mailbox && hr_bytes && !halo_right))

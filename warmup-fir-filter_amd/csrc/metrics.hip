@@ -27,6 +27,7 @@
 //     workgroup of the launch that streams part k, so only the last part's chain is exposed;
 //     metrics_final adds the last part (and the ragged block) and reduces the counts and max.
 #include <string>
+#include <type_traits>
 
 #include "fir_common.h"
 #include "fir_launch.h"
@@ -53,15 +54,26 @@ struct Cnt {
 struct Term {
     double a, q, d;
 };
-__device__ __forceinline__ Term metrics_term(double id, uint32_t fx, double& mx, uint32_t& lo, uint32_t& hi,
+// F = uint32_t (u8 samples, integer compares) or double (any other fixed dtype converted as
+// astype(np.float64) does; fixed == 0 / == 255 on the original values equal the same compares on
+// the converted ones for every integer and float dtype: the conversion is exact near 0 and 255).
+// max drops a NaN here (v_max_f64); metrics_final restores NumPy's NaN from sum|d| (below).
+template <typename F>
+__device__ __forceinline__ Term metrics_term(double id, F fx, double& mx, uint32_t& lo, uint32_t& hi,
                                              uint32_t& clip) {
     const double d = __dsub_rn((double)fx, id);
     const double ad = fabs(d);
     mx = fmax(mx, ad);
-    lo += fx == 0;
-    hi += fx == 255;
+    lo += fx == (F)0;
+    hi += fx == (F)255;
     clip += (id < 0.0) | (id > 255.0);
     return Term{ad, __dmul_rn(d, d), d};
+}
+// fixed sample -> the value metrics_term compares (u8: the integer; others: the float64 value)
+template <typename FT>
+__device__ __forceinline__ auto fixed_val(FT v) {
+    if constexpr (std::is_same_v<FT, uint8_t>) return (uint32_t)v;
+    else return (double)v;
 }
 __device__ __forceinline__ void tadd(Term& s, const Term& t) {
     s.a = __dadd_rn(s.a, t.a);
@@ -96,23 +108,25 @@ __device__ __forceinline__ Term tshift(const Term& s) {
 }
 
 // pairwise_sum of one leaf (n <= 128) of samples [o, o + n), as NumPy's loop does it
-__device__ Term pw_leaf(const double* ideal, const uint8_t* fixed, int64_t o, int n, double& mx, uint32_t& lo,
+template <typename FT>
+__device__ Term pw_leaf(const double* ideal, const FT* fixed, int64_t o, int n, double& mx, uint32_t& lo,
                         uint32_t& hi, uint32_t& clip) {
+    auto term = [&](int64_t i) { return metrics_term(ideal[i], fixed_val(fixed[i]), mx, lo, hi, clip); };
     if (n < 8) {
         Term res{0.0, 0.0, 0.0};
-        for (int i = 0; i < n; ++i) tadd(res, metrics_term(ideal[o + i], fixed[o + i], mx, lo, hi, clip));
+        for (int i = 0; i < n; ++i) tadd(res, term(o + i));
         return res;
     }
     Term r[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = metrics_term(ideal[o + j], fixed[o + j], mx, lo, hi, clip);
+    for (int j = 0; j < 8; ++j) r[j] = term(o + j);
     int i = 8;
     for (; i < n - (n % 8); i += 8) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) tadd(r[j], metrics_term(ideal[o + i + j], fixed[o + i + j], mx, lo, hi, clip));
+        for (int j = 0; j < 8; ++j) tadd(r[j], term(o + i + j));
     }
     Term res = tadd2(tadd2(tadd2(r[0], r[1]), tadd2(r[2], r[3])), tadd2(tadd2(r[4], r[5]), tadd2(r[6], r[7])));
-    for (; i < n; ++i) tadd(res, metrics_term(ideal[o + i], fixed[o + i], mx, lo, hi, clip));
+    for (; i < n; ++i) tadd(res, term(o + i));
     return res;
 }
 
@@ -178,6 +192,33 @@ __device__ void chain_range(const double* __restrict__ bsum, int64_t nb, int64_t
     if (lane == 0) {
         state[wv] = s;
         if (out) out[1 + wv] = s;
+    }
+}
+
+// A round's 64 lane sums (lane (leaf k, accumulator j)) -> lane 0: each leaf's
+// ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the round's 8 leaves pairwise.
+__device__ __forceinline__ Term round_tree(Term t) {
+    t = tadd2(t, tshift<1>(t));
+    t = tadd2(t, tshift<2>(t));
+    t = tadd2(t, tshift<4>(t));
+    t = tadd2(t, tshift<8>(t));
+    t = tadd2(t, tshift<16>(t));
+    return tadd2(t, tshift<32>(t));
+}
+// Round rd's sum into the block's tree ((R0+R1)+(R2+R3))+((R4+R5)+(R6+R7)): st[0] R_even,
+// st[1] pairs, st[2] quads, st[3] the block after round 7.
+__device__ __forceinline__ void fold_round(Term (&st)[4], int rd, const Term& t) {
+    if ((rd & 1) == 0) {
+        st[0] = t;
+    } else {
+        const Term pr = tadd2(st[0], t);
+        if ((rd & 2) == 0) {
+            st[1] = pr;
+        } else {
+            const Term q = tadd2(st[1], pr);
+            if ((rd & 4) == 0) st[2] = q;
+            else st[3] = tadd2(st[2], q);
+        }
     }
 }
 
@@ -260,27 +301,7 @@ __global__ __launch_bounds__(kBlock, FIR_METRIC_MINB) void metrics_blocks(const 
                 if (s == 0) r = t;
                 else tadd(r, t);
             }
-            // leaf: ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the round's 8 leaves pairwise
-            Term t = r;
-            t = tadd2(t, tshift<1>(t));
-            t = tadd2(t, tshift<2>(t));
-            t = tadd2(t, tshift<4>(t));
-            t = tadd2(t, tshift<8>(t));
-            t = tadd2(t, tshift<16>(t));
-            t = tadd2(t, tshift<32>(t));  // lane 0 holds the round's sum
-            // fold into the block's tree: st[0] R_even, st[1] pairs, st[2] quads
-            if ((rd & 1) == 0) {
-                st[0] = t;
-            } else {
-                const Term pr = tadd2(st[0], t);
-                if ((rd & 2) == 0) {
-                    st[1] = pr;
-                } else {
-                    const Term q = tadd2(st[1], pr);
-                    if ((rd & 4) == 0) st[2] = q;
-                    else st[3] = tadd2(st[2], q);
-                }
-            }
+            fold_round(st, rd, round_tree(r));
         }
         const Term s = st[3];
         if (lane == 0) bsum[b] = s.a, bsum[nb + b] = s.q, bsum[2 * nb + b] = s.d;
@@ -288,9 +309,50 @@ __global__ __launch_bounds__(kBlock, FIR_METRIC_MINB) void metrics_blocks(const 
     block_counts(Cnt{mx, lo, hi, clip}, parts + wg);
 }
 
+// Fixed arrays of any other dtype (int8..int64, uint16..uint64, float16/32/64: the reference's
+// astype(np.float64) accepts them all): the same blocks, rounds, leaves and trees, each lane
+// reading its accumulator's 16 samples (stride 8) straight from memory.  Not a bandwidth path.
+template <typename FT>
+__global__ __launch_bounds__(kBlock) void metrics_blocks_any(const double* __restrict__ ideal,
+                                                             const FT* __restrict__ fixed, double* __restrict__ bsum,
+                                                             int64_t nb, int64_t b_lo, int64_t b_hi, int64_t c_lo,
+                                                             int64_t c_hi, double* __restrict__ state,
+                                                             Cnt* __restrict__ parts) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kChainLds];
+    const bool chain = c_hi > c_lo;
+    if (chain && blockIdx.x == 0) {
+        chain_range(bsum, nb, c_lo, c_hi, state, smem);
+        return;
+    }
+    const int wg = blockIdx.x - (chain ? 1 : 0);
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x >> 6;
+    const int k = lane >> 3, j = lane & 7;
+    const int64_t nwaves = (int64_t)(gridDim.x - (chain ? 1 : 0)) * (kBlock / kWave);
+    double mx = 0.0;
+    uint32_t lo = 0, hi = 0, clip = 0;
+    for (int64_t b = b_lo + (int64_t)wg * (kBlock / kWave) + wv; b < b_hi; b += nwaves) {
+        Term st[4];
+#pragma unroll 1
+        for (int rd = 0; rd < 8; ++rd) {
+            const int64_t o = b * kPwBlock + rd * 1024 + k * kPwLeaf + j;
+            Term r{0.0, 0.0, 0.0};
+#pragma unroll 4
+            for (int s = 0; s < 16; ++s) {
+                const Term t = metrics_term(ideal[o + 8 * s], fixed_val(fixed[o + 8 * s]), mx, lo, hi, clip);
+                if (s == 0) r = t;
+                else tadd(r, t);
+            }
+            fold_round(st, rd, round_tree(r));
+        }
+        if (lane == 0) bsum[b] = st[3].a, bsum[nb + b] = st[3].q, bsum[2 * nb + b] = st[3].d;
+    }
+    block_counts(Cnt{mx, lo, hi, clip}, parts + wg);
+}
+
 // The ragged last block [nbf * 8192, n) (0 < m < 8192 samples): NumPy's recursion over it, one
 // workgroup (leaves enumerated, summed one per thread, recombined in post-order).
-__global__ __launch_bounds__(kBlock) void metrics_ragged(const double* __restrict__ ideal, const uint8_t* __restrict__ fixed,
+template <typename FT>
+__global__ __launch_bounds__(kBlock) void metrics_ragged(const double* __restrict__ ideal, const FT* __restrict__ fixed,
                                                          int64_t n, double* __restrict__ bsum, int64_t nb,
                                                          Cnt* __restrict__ part) {
     __shared__ int leaf_off[kPwMaxLeaves], leaf_len[kPwMaxLeaves];
@@ -376,8 +438,11 @@ __global__ __launch_bounds__(kBlock) void metrics_final(const double* __restrict
         }
         __syncthreads();
     }
+    __syncthreads();  // out[1] (the chain's sum|d|) is written
     if (t == 0) {
-        out[0] = red[0].mx;
+        // np.max propagates NaN; fmax dropped it.  sum|d| is NaN exactly when some |d| is (|d| >= 0:
+        // no inf - inf), and its order is NumPy's, so NaN there = NaN in the reference's max.
+        out[0] = out[1] != out[1] ? out[1] : red[0].mx;
         out[4] = (double)red[0].lo;
         out[5] = (double)red[0].hi;
         out[6] = (double)red[0].clip;
@@ -404,10 +469,11 @@ size_t metrics_work_bytes(int64_t n) {
     return sizeof(Cnt) * kCntSlots + 64 + 3 * sizeof(double) * (size_t)metrics_nblocks(n < 0 ? 0 : n);
 }
 
-int launch_metrics(const double* ideal, const uint8_t* fixed, int64_t n, double* out, void* work,
-                   hipStream_t stream, std::string* err) {
-    if (n < 0) return *err = "n must be >= 0", FIR_EINVAL;
-    if (!out || !work || (n > 0 && (!ideal || !fixed))) return *err = "null pointer argument", FIR_EINVAL;
+namespace {
+
+template <typename FT>
+int launch_metrics_t(const double* ideal, const FT* fixed, int64_t n, double* out, void* work, hipStream_t stream,
+                     std::string* err) {
     const int64_t nb = metrics_nblocks(n), nbf = n / kPwBlock;
     Cnt* parts = (Cnt*)work;
     double* state = (double*)((char*)work + sizeof(Cnt) * kCntSlots);
@@ -437,17 +503,23 @@ int launch_metrics(const double* ideal, const uint8_t* fixed, int64_t n, double*
         const int64_t want = (hi - lo + kBlock / kWave - 1) / (kBlock / kWave);
         const int g = (int)(want > kMetricBlocks ? kMetricBlocks : want);
         const unsigned grid = (unsigned)g + (prev_hi > prev_lo ? 1u : 0u);
-        if (vec)
-            hipLaunchKernelGGL(metrics_blocks<true>, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, lo, hi,
-                               prev_lo, prev_hi, state, parts + slot);
-        else
-            hipLaunchKernelGGL(metrics_blocks<false>, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, lo, hi,
-                               prev_lo, prev_hi, state, parts + slot);
+        if constexpr (std::is_same_v<FT, uint8_t>) {
+            if (vec)
+                hipLaunchKernelGGL(metrics_blocks<true>, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, lo,
+                                   hi, prev_lo, prev_hi, state, parts + slot);
+            else
+                hipLaunchKernelGGL(metrics_blocks<false>, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, lo,
+                                   hi, prev_lo, prev_hi, state, parts + slot);
+        } else {
+            (void)vec;
+            hipLaunchKernelGGL(metrics_blocks_any<FT>, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, lo,
+                               hi, prev_lo, prev_hi, state, parts + slot);
+        }
         slot += g;
         prev_lo = lo, prev_hi = hi;
     }
     if (nb > nbf) {  // the ragged last block (its sum is the last in order)
-        hipLaunchKernelGGL(metrics_ragged, dim3(1), dim3(kBlock), 0, stream, ideal, fixed, n, bsum, nb, parts + slot);
+        hipLaunchKernelGGL(metrics_ragged<FT>, dim3(1), dim3(kBlock), 0, stream, ideal, fixed, n, bsum, nb, parts + slot);
         ++slot;
     }
     hipLaunchKernelGGL(metrics_final, dim3(1), dim3(kBlock), 0, stream, (const double*)bsum, nb, prev_lo, state,
@@ -455,6 +527,39 @@ int launch_metrics(const double* ideal, const uint8_t* fixed, int64_t n, double*
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return *err = std::string("metrics launch failed: ") + hipGetErrorString(e), FIR_EHIP;
     return FIR_OK;
+}
+
+}  // namespace
+
+int metrics_dtype_size(int dt) {
+    switch (dt) {
+        case FIR_DT_U8: case FIR_DT_I8: return 1;
+        case FIR_DT_U16: case FIR_DT_I16: case FIR_DT_F16: return 2;
+        case FIR_DT_U32: case FIR_DT_I32: case FIR_DT_F32: return 4;
+        case FIR_DT_U64: case FIR_DT_I64: case FIR_DT_F64: return 8;
+        default: return 0;
+    }
+}
+
+int launch_metrics(const double* ideal, const void* fixed, int fixed_dtype, int64_t n, double* out, void* work,
+                   hipStream_t stream, std::string* err) {
+    if (n < 0) return *err = "n must be >= 0", FIR_EINVAL;
+    if (!out || !work || (n > 0 && (!ideal || !fixed))) return *err = "null pointer argument", FIR_EINVAL;
+    const int es = metrics_dtype_size(fixed_dtype);
+    if (!es) return *err = "unknown fixed dtype", FIR_EINVAL;
+    switch (fixed_dtype) {
+        case FIR_DT_U8: return launch_metrics_t(ideal, (const uint8_t*)fixed, n, out, work, stream, err);
+        case FIR_DT_I8: return launch_metrics_t(ideal, (const int8_t*)fixed, n, out, work, stream, err);
+        case FIR_DT_U16: return launch_metrics_t(ideal, (const uint16_t*)fixed, n, out, work, stream, err);
+        case FIR_DT_I16: return launch_metrics_t(ideal, (const int16_t*)fixed, n, out, work, stream, err);
+        case FIR_DT_U32: return launch_metrics_t(ideal, (const uint32_t*)fixed, n, out, work, stream, err);
+        case FIR_DT_I32: return launch_metrics_t(ideal, (const int32_t*)fixed, n, out, work, stream, err);
+        case FIR_DT_U64: return launch_metrics_t(ideal, (const uint64_t*)fixed, n, out, work, stream, err);
+        case FIR_DT_I64: return launch_metrics_t(ideal, (const int64_t*)fixed, n, out, work, stream, err);
+        case FIR_DT_F16: return launch_metrics_t(ideal, (const _Float16*)fixed, n, out, work, stream, err);
+        case FIR_DT_F32: return launch_metrics_t(ideal, (const float*)fixed, n, out, work, stream, err);
+        default: return launch_metrics_t(ideal, (const double*)fixed, n, out, work, stream, err);
+    }
 }
 
 }  // namespace fir

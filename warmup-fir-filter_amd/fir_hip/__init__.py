@@ -25,7 +25,7 @@ __all__ = [
     "fir1d_fixed_rows_sharded", "fir2d_fixed", "fir1d_ideal_rows", "compare_metrics", "restore_u8", "IN_U8", "IN_I16",
     "OUT_U8_SAT", "OUT_I32", "RESTORE_CLIP", "RESTORE_NORMALIZE", "MAX_TAPS", "EXPORTS", "ipc_export", "ipc_import",
     "ipc_close", "peek", "IPC_HANDLE_BYTES", "device_bus_id", "peer_access", "peer_atomics", "halo_mailbox_bytes",
-    "GATE_TIMEOUT", "build_id", "parse_devices",
+    "GATE_TIMEOUT", "GATE_LAYOUT", "build_id", "parse_devices", "METRIC_DTYPES",
 ]
 
 IN_U8, IN_I16 = 0, 1
@@ -33,8 +33,9 @@ OUT_U8_SAT, OUT_I32 = 0, 1
 RESTORE_CLIP, RESTORE_NORMALIZE = 0, 1
 MAX_TAPS = 1 << 24  # FIR_MAX_TAPS: any practical length (the reference has no limit)
 IPC_HANDLE_BYTES = 64
-ABI_VERSION = 3
+ABI_VERSION = 4
 GATE_TIMEOUT = 1  # FIR_GATE_TIMEOUT
+GATE_LAYOUT = 2  # FIR_GATE_LAYOUT
 
 _HERE = Path(__file__).resolve().parent
 
@@ -68,8 +69,8 @@ EXPORTS = {
     "fir1d_ideal_rows": (_i32, [_vp, _i64, _i64, _vp, _i32, _vp, _i32]),
     "fir1d_ideal_rows_dev": (_i32, [_vp, _i64, _i64, _vp, _i32, _vp, _vp]),
     "fir_metrics_work_bytes": (_i64, [_i64]),
-    "fir_compare_metrics": (_i32, [_vp, _vp, _i64, _vp, _i32]),
-    "fir_compare_metrics_dev": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp]),
+    "fir_compare_metrics": (_i32, [_vp, _vp, _i32, _i64, _vp, _i32]),
+    "fir_compare_metrics_dev": (_i32, [_vp, _vp, _i32, _i64, _vp, _vp, _vp]),
     "fir1d_fixed_rows_sharded": (_i32, [_vp, _i32, _i64, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _i32]),
     "fir_restore_work_bytes": (_i64, []),
     "fir_restore_u8": (_i32, [_vp, _i64, _i32, _vp, _i32]),
@@ -82,7 +83,7 @@ EXPORTS = {
     "fir_peer_access": (_i32, [_i32, ctypes.c_char_p, ctypes.POINTER(_i32)]),
     "fir_peer_atomics": (_i32, [_i32, ctypes.c_char_p, ctypes.POINTER(_i32)]),
     "fir_halo_mailbox_bytes": (_i64, [_i64, _i64]),
-    "fir_halo_mailbox_init_dev": (_i32, [_vp, _i64, _vp]),
+    "fir_halo_mailbox_init_dev": (_i32, [_vp, _i64, _i64, _i64, _vp]),
     "fir_halo_gate_dev": (_i32, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_double, _vp]),
 }
 
@@ -379,14 +380,35 @@ def metrics_from_sums(s, n: int) -> dict:
             "sat_high_ratio": hi, "sat_ratio": lo + hi, "clip_needed_ratio": float(s[6]) / n}
 
 
+# fixed-array dtypes of the metrics kernel (fir_num_dtype); bool goes as its uint8 bytes (0/1)
+METRIC_DTYPES = {np.dtype(np.uint8): 0, np.dtype(np.int8): 1, np.dtype(np.uint16): 2, np.dtype(np.int16): 3,
+                 np.dtype(np.uint32): 4, np.dtype(np.int32): 5, np.dtype(np.uint64): 6, np.dtype(np.int64): 7,
+                 np.dtype(np.float16): 8, np.dtype(np.float32): 9, np.dtype(np.float64): 10}
+
+
+def metrics_fixed_view(y_fixed: np.ndarray):
+    """(flat contiguous array, fir_num_dtype code) of a fixed output for the metrics kernel: its
+    own values in native byte order, as the reference's y_fixed.astype(np.float64) reads them."""
+    yf = np.asarray(y_fixed)
+    if yf.dtype == np.bool_:
+        yf = yf.view(np.uint8)
+    dt = yf.dtype.newbyteorder("=") if yf.dtype.byteorder not in ("=", "|") else yf.dtype
+    if dt not in METRIC_DTYPES:
+        raise FirHipError(f"fixed dtype {yf.dtype} is not supported (integer, bool or float16/32/64)")
+    yf = np.ascontiguousarray(yf, dtype=dt).reshape(-1)
+    return yf, METRIC_DTYPES[dt]
+
+
 def compare_metrics(y_ideal: np.ndarray, y_fixed: np.ndarray, device: int = 0) -> dict:
-    """_compute_metrics (gen_3tap_compare_report.py:67-112) in one GPU pass."""
+    """_compute_metrics (gen_3tap_compare_report.py:67-112) in one GPU pass, for a fixed array of
+    any integer / bool / float dtype (the reference converts it with astype(np.float64), :85)."""
     if y_ideal.shape != y_fixed.shape:
         raise ValueError(f"Shape mismatch: ideal={y_ideal.shape}, fixed={y_fixed.shape}")
     yi = np.ascontiguousarray(y_ideal, dtype=np.float64).reshape(-1)
-    yf = np.ascontiguousarray(y_fixed, dtype=np.uint8).reshape(-1)
+    yf, code = metrics_fixed_view(y_fixed)
     out = np.zeros(9, dtype=np.float64)
-    _check(lib().fir_compare_metrics(_ptr(yi), _ptr(yf), yi.size, _ptr(out), int(device)), "fir_compare_metrics")
+    _check(lib().fir_compare_metrics(_ptr(yi), _ptr(yf), code, yi.size, _ptr(out), int(device)),
+           "fir_compare_metrics")
     return metrics_from_sums(out, yi.size)
 
 

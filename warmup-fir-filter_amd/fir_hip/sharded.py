@@ -127,7 +127,8 @@ class XgmiHalo:
     :func:`make_halo_source` falls back to RCCL on every rank otherwise, or if the first gated
     hand-off, checked against the edges every rank reported, does not arrive)."""
 
-    def __init__(self, seg: torch.Tensor, taps: int, channels: int = 1, group=None, timeout_s: float | None = None):
+    def __init__(self, seg: torch.Tensor, taps: int, channels: int = 1, group=None, timeout_s: float | None = None,
+                 self_ring: bool = False):
         import os
 
         import fir_hip
@@ -137,8 +138,12 @@ class XgmiHalo:
         seg = seg.reshape(-1)
         if not seg.is_cuda or not seg.is_contiguous():
             raise ValueError("XgmiHalo needs a contiguous device segment")
-        world = dist.get_world_size(group)
-        rank = dist.get_rank(group)
+        # self_ring: a ring of one on one GPU (no process group needed): the rank is its own left and
+        # right neighbour, its own mailbox stands in for both mapped ones, so the gate publishes,
+        # waits and copies exactly as across GPUs (left <- seg[-HL:], right <- seg[:HR]); it times
+        # the gate's per-step cost without other processes sharing the GPU
+        world = 1 if self_ring else dist.get_world_size(group)
+        rank = 0 if self_ring else dist.get_rank(group)
         hl, hr = halo_sizes(taps, channels)
         if seg.numel() < max(hl, hr):
             raise ValueError("segment shorter than the filter halo")
@@ -149,11 +154,21 @@ class XgmiHalo:
         dev = seg.device.index
         self.mailbox = torch.empty(fir_hip.halo_mailbox_bytes(self.hl_bytes, self.hr_bytes), dtype=torch.uint8,
                                    device=seg.device)
-        torch_ops.halo_mailbox_init_dev(self.mailbox)
+        torch_ops.halo_mailbox_init_dev(self.mailbox, self.hl_bytes, self.hr_bytes)
         self.status = torch.zeros(1, dtype=torch.int32, device=seg.device)
-        self.left = torch.zeros(hl, dtype=seg.dtype, device=seg.device) if rank > 0 and hl else None
-        self.right = torch.zeros(hr, dtype=seg.dtype, device=seg.device) if rank < world - 1 and hr else None
+        has_l, has_r = (rank > 0 or self_ring), (rank < world - 1 or self_ring)
+        self.left = torch.zeros(hl, dtype=seg.dtype, device=seg.device) if has_l and hl else None
+        self.right = torch.zeros(hr, dtype=seg.dtype, device=seg.device) if has_r and hr else None
+        self._side = self._ev_seg = self._ev_gate = None  # overlapped form (gate_async / join)
         torch.cuda.synchronize(seg.device)  # zeroed before any neighbour can map it
+        self._mapped = []
+        if self_ring:
+            own = self.mailbox.data_ptr()
+            self.left_mb = own if has_l else None
+            self.right_mb = own if has_r else None
+            self._expect = (seg[seg.numel() - hl:].cpu().numpy().tobytes() if has_l else None,
+                            seg[:hr].cpu().numpy().tobytes() if has_r else None)
+            return
         handle, off = fir_hip.ipc_export(self.mailbox.data_ptr())
         mine = {"handle": handle, "offset": off, "bus": fir_hip.device_bus_id(dev),
                 "first": seg[:hr].cpu().numpy().tobytes(), "last": seg[seg.numel() - hl:].cpu().numpy().tobytes()}
@@ -161,7 +176,6 @@ class XgmiHalo:
         dist.all_gather_object(infos, mine, group=group)
         self._expect = (infos[rank - 1]["last"] if rank > 0 else None, infos[rank + 1]["first"] if rank < world - 1 else None)
         self.left_mb = self.right_mb = None
-        self._mapped = []
         # the gate's kernel loads from and performs atomics on the neighbours' HBM: refuse (-> RCCL
         # on every rank) unless this process sees both GPUs with peer access and peer atomics
         for r in (rank - 1, rank + 1):
@@ -188,6 +202,25 @@ class XgmiHalo:
 
         torch_ops.halo_gate_dev(self.seg, self.hl_bytes, self.hr_bytes, self.mailbox, self.left_mb, self.right_mb,
                                 self.left, self.right, self.status, self.timeout_s, stream)
+
+    def gate_async(self, stream=None) -> None:
+        """The overlapped form of :meth:`gate`: the gate runs on a high-priority side stream (its
+        own hardware queue) after everything enqueued so far on ``stream`` (the step's segment is
+        written), so the bulk kernel enqueued next on ``stream`` runs while the gate waits for the
+        neighbours; :meth:`join` makes ``stream`` wait for the gate before the edge kernel."""
+        main = stream if stream is not None else torch.cuda.current_stream(self.seg.device)
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.seg.device, priority=-1)
+            self._ev_seg, self._ev_gate = torch.cuda.Event(), torch.cuda.Event()
+        self._ev_seg.record(main)
+        self._side.wait_event(self._ev_seg)
+        self.gate(self._side)
+        self._ev_gate.record(self._side)
+
+    def join(self, stream=None) -> None:
+        """``stream`` waits for the last :meth:`gate_async` (the halos are then this step's)."""
+        main = stream if stream is not None else torch.cuda.current_stream(self.seg.device)
+        main.wait_event(self._ev_gate)
 
     def halos(self):
         """(left, right) halo tensors of the last gate (None at the global ends)."""

@@ -16,6 +16,9 @@ from . import (IN_I16, IN_U8, OUT_I32, OUT_U8_SAT, RESTORE_CLIP, RESTORE_NORMALI
 
 _IN = {torch.uint8: IN_U8, torch.int16: IN_I16}
 _OUT_DTYPE = {OUT_U8_SAT: torch.uint8, OUT_I32: torch.int32}
+# fixed-output dtypes of the metrics kernel (fir_num_dtype codes; bool = its 0/1 bytes)
+_METRIC_DT = {torch.uint8: 0, torch.bool: 0, torch.int8: 1, torch.uint16: 2, torch.int16: 3, torch.uint32: 4,
+              torch.int32: 5, torch.uint64: 6, torch.int64: 7, torch.float16: 8, torch.float32: 9, torch.float64: 10}
 
 
 class Taps:
@@ -152,11 +155,13 @@ def fir1d_fixed_segment_dev(x: torch.Tensor, hq, halo_left, halo_right, frac_bit
     return out
 
 
-def halo_mailbox_init_dev(mailbox: torch.Tensor, stream=None) -> torch.Tensor:
-    """Zero a halo-gate mailbox (a 128-byte-aligned uint8 device tensor) with device atomics."""
+def halo_mailbox_init_dev(mailbox: torch.Tensor, hl_bytes: int, hr_bytes: int, stream=None) -> torch.Tensor:
+    """Zero a halo-gate mailbox (a 128-byte-aligned uint8 device tensor) with device atomics and
+    record the halo sizes its slots are laid out for (every gate on it checks them)."""
     _check_dev(mailbox, "mailbox")
     _check(lib().fir_halo_mailbox_init_dev(ctypes.c_void_p(mailbox.data_ptr()), mailbox.numel() * mailbox.element_size(),
-                                           _stream_ptr(mailbox, stream)), "fir_halo_mailbox_init_dev")
+                                           int(hl_bytes), int(hr_bytes), _stream_ptr(mailbox, stream)),
+           "fir_halo_mailbox_init_dev")
     return mailbox
 
 
@@ -240,8 +245,10 @@ def compare_metrics_dev(ideal: torch.Tensor, fixed: torch.Tensor, out: torch.Ten
     tensors, into a float64 device tensor of 9 (see fir_hip.metrics_from_sums)."""
     _check_dev(ideal, "ideal")
     _check_dev(fixed, "fixed")
-    if ideal.dtype != torch.float64 or fixed.dtype != torch.uint8 or ideal.shape != fixed.shape:
-        raise FirHipError("ideal must be float64 and fixed uint8 of the same shape")
+    if ideal.dtype != torch.float64 or fixed.dtype not in _METRIC_DT or ideal.shape != fixed.shape:
+        raise FirHipError("ideal must be float64 and fixed an integer/bool/float tensor of the same shape")
+    if not ideal.is_contiguous() or not fixed.is_contiguous():
+        raise FirHipError("ideal and fixed must be contiguous")
     if out is None:
         out = torch.empty(9, dtype=torch.float64, device=ideal.device)
     need = int(lib().fir_metrics_work_bytes(ideal.numel()))
@@ -250,7 +257,7 @@ def compare_metrics_dev(ideal: torch.Tensor, fixed: torch.Tensor, out: torch.Ten
     elif work.numel() * work.element_size() < need or not work.is_contiguous():
         raise FirHipError(f"work must be a contiguous device buffer of >= {need} bytes for {ideal.numel()} samples")
     _check(lib().fir_compare_metrics_dev(ctypes.c_void_p(ideal.data_ptr()), ctypes.c_void_p(fixed.data_ptr()),
-                                         ideal.numel(), ctypes.c_void_p(out.data_ptr()),
+                                         _METRIC_DT[fixed.dtype], ideal.numel(), ctypes.c_void_p(out.data_ptr()),
                                          ctypes.c_void_p(work.data_ptr()), _stream_ptr(ideal, stream)),
            "fir_compare_metrics_dev")
     return out
