@@ -65,6 +65,8 @@ for s in $STEPS; do
              run "profself_$m" 300 env FIR_SELF_HALO=1 FIR_HALO=xgmi FIR_GATE_MODE=$m rocprofv3 --kernel-trace --stats \
                  -d "$OUT/profself_$m" -o run --output-format csv -- python bench.py --steps 200 --warmup 100 \
                  --cpu-seconds 0 --no-parity; fatal $? ;;
+        metab) run metab 300 python tools/metrics_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_old.so \
+                 abrun/libfir_hip_oldnoasm.so abrun/libfir_hip_glds0.so abrun/libfir_hip_glds768.so abrun/libfir_hip_glds256.so; fatal $? ;;
         asan) run asan 600 make -C warmup-fir-filter_amd/csrc asan-check; fatal $? ;;
         micro) run micro 300 tools/microbench/fir_micro 28 20; fatal $? ;;
         micro2d) run micro2d 300 tools/microbench/fir2d_micro 15; fatal $? ;;

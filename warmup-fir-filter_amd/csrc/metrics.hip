@@ -38,6 +38,10 @@ namespace fir {
 #define FIR_METRIC_BLOCKS 512  // of an 8192-block part; 2^28: 453 -> 430 us vs 2048, 4096 slower)
 #endif
 constexpr int kMetricBlocks = FIR_METRIC_BLOCKS;
+#ifndef FIR_METRIC_GLDS  // 1: the LDS-DMA double-buffered block pass (metrics_blocks_glds)
+#define FIR_METRIC_GLDS 1
+#endif
+constexpr bool kMetricGlds = FIR_METRIC_GLDS;
 #ifndef FIR_METRIC_MINB  // waves per SIMD the block kernel's registers must allow
 #define FIR_METRIC_MINB 4
 #endif
@@ -296,7 +300,9 @@ __global__ __launch_bounds__(kBlock, FIR_METRIC_MINB) void metrics_blocks(const 
             for (int s = 0; s < 16; ++s) {
                 double id = *reinterpret_cast<const double*>(row + 64 * s);
                 uint32_t f = (frw[s / 4] >> (8 * (s % 4))) & 0xFFu;
+#if !FIR_METRIC_OLD_NOASM  // (A/B only) the register form as round 3 shipped it: one LDS read per term
                 asm volatile("" : "+v"(id), "+v"(f), "+v"(mx), "+v"(lo), "+v"(hi), "+v"(clip));
+#endif
                 const Term t = metrics_term(id, f, mx, lo, hi, clip);
                 if (s == 0) r = t;
                 else tadd(r, t);
@@ -305,6 +311,106 @@ __global__ __launch_bounds__(kBlock, FIR_METRIC_MINB) void metrics_blocks(const 
         }
         const Term s = st[3];
         if (lane == 0) bsum[b] = s.a, bsum[nb + b] = s.q, bsum[2 * nb + b] = s.d;
+    }
+    block_counts(Cnt{mx, lo, hi, clip}, parts + wg);
+}
+
+// The same block pass with the rounds streamed by LDS-DMA (global_load_lds_dwordx4: a load that
+// writes the wave's LDS directly, holding no VGPRs while in flight), double-buffered: round t+1's
+// 8 KiB of ideal values and 1 KiB of fixed bytes are in flight while round t is reduced, so each
+// wave always has one round outstanding (the register-staged form above loads, waits, then
+// computes; prefetching into registers spilled, profiles/r03/metrics_exact_ab.txt).  A wave walks
+// its blocks' rounds as one sequence t (block t / 8 of the wave's grid-stride list, round t % 8).
+// Ordering: round t's 9 DMAs are the wave's oldest outstanding VMEM ops once round t+1's are
+// issued, so `s_waitcnt vmcnt(9)` retires exactly them (explicit: hipcc does not count LDS-DMA
+// for the ds_reads that follow); a buffer is refilled two rounds after its last ds_read, whose
+// results the VALU has consumed by then.  The fixed bytes land linearly and are transposed in
+// place (one ds_read_b128 per lane, all of the wave's reads before any of its writes).
+// LDS: 2 x (8 rows of 1 KiB + 64 B pad + 1 KiB fixed) per wave = 76 KiB per workgroup, 2 per CU.
+constexpr int kGRow = 1024 + 64;
+constexpr int kGBuf = 8 * kGRow + 1024;
+constexpr int kGWaveLds = 2 * kGBuf;
+static_assert(kBlock / kWave * kGWaveLds >= kChainLds, "the chain's staging shares the wave buffers");
+#ifndef FIR_METRIC_AUX  // cache policy of the DMA loads (2 = nt: every byte is read once)
+#define FIR_METRIC_AUX 2
+#endif
+__device__ __forceinline__ void glds16(const void* g, uint8_t* lds) {
+    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 16, 0, FIR_METRIC_AUX);
+}
+__global__ __launch_bounds__(kBlock, 2) void metrics_blocks_glds(const double* __restrict__ ideal,
+                                                                              const uint8_t* __restrict__ fixed,
+                                                                              double* __restrict__ bsum, int64_t nb,
+                                                                              int64_t b_lo, int64_t b_hi, int64_t c_lo,
+                                                                              int64_t c_hi, double* __restrict__ state,
+                                                                              Cnt* __restrict__ parts) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock / kWave * kGWaveLds];
+    const bool chain = c_hi > c_lo;
+    if (chain && blockIdx.x == 0) {
+        chain_range(bsum, nb, c_lo, c_hi, state, smem);
+        return;
+    }
+    const int wg = blockIdx.x - (chain ? 1 : 0);
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x >> 6;
+    const int k = lane >> 3, j = lane & 7;
+    uint8_t* wl = smem + wv * kGWaveLds;
+    const int64_t nwaves = (int64_t)(gridDim.x - (chain ? 1 : 0)) * (kBlock / kWave);
+    const int64_t b0 = b_lo + (int64_t)wg * (kBlock / kWave) + wv;
+    const int64_t nrounds = b0 < b_hi ? ((b_hi - 1 - b0) / nwaves + 1) * 8 : 0;
+    double mx = 0.0;
+    uint32_t lo = 0, hi = 0, clip = 0;
+
+    auto issue = [&](int64_t t) {
+        const int64_t base = (b0 + (t >> 3) * nwaves) * kPwBlock + (t & 7) * 1024;
+        uint8_t* buf = wl + (t & 1) * kGBuf;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) glds16(ideal + base + 128 * i + 2 * lane, buf + i * kGRow);
+        glds16(fixed + base + 16 * lane, buf + 8 * kGRow);
+    };
+    if (nrounds) issue(0);
+    Term st[4];
+#pragma unroll 1
+    for (int64_t t = 0; t < nrounds; ++t) {
+        if (t + 1 < nrounds) {
+            issue(t + 1);
+            asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        uint8_t* buf = wl + (t & 1) * kGBuf;
+        uint8_t* fb = buf + 8 * kGRow;
+        {  // fixed bytes -> [leaf][accumulator j][step s], in place (see metrics_blocks)
+            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+            const u4 fx = *reinterpret_cast<const u4*>(fb + 16 * lane);
+            const uint32_t fw[4] = {fx.x, fx.y, fx.z, fx.w};
+            uint8_t* fdst = fb + 128 * (lane >> 3) + 2 * (lane & 7);
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj)
+                *reinterpret_cast<uint16_t*>(fdst + 16 * jj) =
+                    (uint16_t)__builtin_amdgcn_perm(fw[2 + jj / 4], fw[jj / 4], (uint32_t)(jj % 4) | ((4u + jj % 4) << 8));
+        }
+        __builtin_amdgcn_wave_barrier();
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        const uint8_t* row = buf + k * kGRow + 8 * j;
+        const u4 fr = *reinterpret_cast<const u4*>(fb + 128 * k + 16 * j);
+        const uint32_t frw[4] = {fr.x, fr.y, fr.z, fr.w};
+        double idv[16];  // all 16 reads issued together (one LDS round trip per round, not 16)
+#pragma unroll
+        for (int s = 0; s < 16; ++s) idv[s] = *reinterpret_cast<const double*>(row + 64 * s);
+        Term r{0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            const uint32_t f = (frw[s / 4] >> (8 * (s % 4))) & 0xFFu;
+            const Term tt = metrics_term(idv[s], f, mx, lo, hi, clip);
+            if (s == 0) r = tt;
+            else tadd(r, tt);
+        }
+        const int rd = (int)(t & 7);
+        fold_round(st, rd, round_tree(r));
+        if (rd == 7 && lane == 0) {
+            const int64_t b = b0 + (t >> 3) * nwaves;
+            bsum[b] = st[3].a, bsum[nb + b] = st[3].q, bsum[2 * nb + b] = st[3].d;
+        }
+        __builtin_amdgcn_wave_barrier();
     }
     block_counts(Cnt{mx, lo, hi, clip}, parts + wg);
 }
@@ -504,7 +610,10 @@ int launch_metrics_t(const double* ideal, const FT* fixed, int64_t n, double* ou
         const int g = (int)(want > kMetricBlocks ? kMetricBlocks : want);
         const unsigned grid = (unsigned)g + (prev_hi > prev_lo ? 1u : 0u);
         if constexpr (std::is_same_v<FT, uint8_t>) {
-            if (vec)
+            if (vec && kMetricGlds)
+                hipLaunchKernelGGL(metrics_blocks_glds, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, lo,
+                                   hi, prev_lo, prev_hi, state, parts + slot);
+            else if (vec)
                 hipLaunchKernelGGL(metrics_blocks<true>, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, lo,
                                    hi, prev_lo, prev_hi, state, parts + slot);
             else
