@@ -1,13 +1,15 @@
 """GPU: BASELINE configs[3] on the HIP path — 5-tap FIR-1D over 2^31 int16 samples sharded as
 8 ranks x 2^28 samples, the (L-1)-sample halo handed over between neighbours every step.
 
-The box has one GPU, so the 8 ranks are 8 processes sharing it (a gloo group for the host-side
-collectives).  Each rank owns its own 2^28-sample segment (512 MiB in, 1 GiB out) in HBM, and
+On a one-GPU box the 8 ranks are 8 processes sharing it (a gloo group for the host-side
+collectives); with several GPUs rank r runs on device r % device_count.  Each rank owns its own 2^28-sample segment (512 MiB in, 1 GiB out) in HBM, and
 EVERY step changes every segment (``seg.add_``, a different amount per rank and step) before
 filtering it, so a halo read that is not ordered against the neighbours' writes would show up:
 
 * ``xgmi``: fir_hip.sharded.XgmiHalo — the halo gate (csrc/halo_gate.hip) hands the edges over
   through IPC-mapped mailboxes with device atomics, then ONE FIR launch reads them;
+* ``xgmi_overlap``: the same gate on a high-priority side stream while the bulk kernel runs
+  (XgmiHalo.gate_async / join), then the edge kernel (bench.py's default N > 1 step);
 * ``rccl``: fir_hip.sharded.HaloExchange — the message path (on this box over gloo, staged
   through the host, since RCCL refuses several ranks on one GPU; across GPUs the same op list
   runs on RCCL), bulk kernel then edge kernel.
@@ -56,7 +58,10 @@ def _worker(rank, world, port, kind, log2n, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     msgs = []
     try:
-        dev = torch.device("cuda", 0)
+        # one GPU per rank when the box has several (the xGMI path then runs across GPUs); on a
+        # one-GPU box every rank shares device 0
+        dev = torch.device("cuda", rank % torch.cuda.device_count())
+        torch.cuda.set_device(dev)
         stream = torch.cuda.Stream(device=dev)
         torch.cuda.set_stream(stream)
         n = 1 << log2n
@@ -71,7 +76,7 @@ def _worker(rank, world, port, kind, log2n, q):
             seg.copy_(torch.from_numpy(x0))
             torch.cuda.synchronize()
             dist.barrier()
-            if kind == "xgmi":
+            if kind.startswith("xgmi"):
                 got_kind, src = sharded.make_halo_source(seg, len(taps))
                 if got_kind != "xgmi":
                     msgs.append(f"rank {rank}: halo source {got_kind}, expected xgmi")
@@ -80,10 +85,16 @@ def _worker(rank, world, port, kind, log2n, q):
             recorded = []
             for step in range(STEPS):
                 seg.add_((step + 1) * (rank + 1))  # every segment changes every step
-                if kind == "xgmi":
+                if kind == "xgmi":  # serial: the gate, then one launch reading its halos
                     src.gate()
                     left, right = src.halos()
                     to.fir1d_fixed_segment_dev(seg, taps, left, right, 12, 32, fh.OUT_I32, out=y)
+                elif kind == "xgmi_overlap":  # the gate on its side stream || the bulk kernel, then edges
+                    src.gate_async()
+                    to.fir1d_fixed_rows_dev(seg, taps, 12, 32, fh.OUT_I32, out=y)
+                    src.join()
+                    left, right = src.halos()
+                    to.fir1d_fixed_edges_dev(seg, taps, y, left, right, 12, 32, fh.OUT_I32)
                 else:
                     works = src.post()
                     to.fir1d_fixed_rows_dev(seg, taps, 12, 32, fh.OUT_I32, out=y)
@@ -92,7 +103,7 @@ def _worker(rank, world, port, kind, log2n, q):
                     to.fir1d_fixed_edges_dev(seg, taps, y, left, right, 12, 32, fh.OUT_I32)
                 recorded.append(torch.cat([y[:EDGE], y[n - EDGE:]]).clone())  # stream-ordered snapshot
             torch.cuda.synchronize()
-            if kind == "xgmi":
+            if kind.startswith("xgmi"):
                 src.check()
             for s in range(STEPS):  # every step's halo-dependent outputs, with that step's neighbours
                 own_head = _wrap16(x0[:EDGE + hr], _add(rank, s))
@@ -114,7 +125,7 @@ def _worker(rank, world, port, kind, log2n, q):
                 msgs.append(f"rank {rank} taps {taps}: full final output differs from the oracle")
             del xf, full
             dist.barrier()  # nobody unmaps or reuses its segment while a neighbour may read it
-            if kind == "xgmi":
+            if kind.startswith("xgmi"):
                 src.close()
         q.put((rank, msgs))
     except Exception as e:  # noqa: BLE001 - reported to the parent
@@ -124,7 +135,7 @@ def _worker(rank, world, port, kind, log2n, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind", ["xgmi", "rccl"])
+@pytest.mark.parametrize("kind", ["xgmi", "xgmi_overlap", "rccl"])
 def test_config3_8_ranks_2p28_changing_segments(kind):
     import socket
 

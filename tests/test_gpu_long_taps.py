@@ -148,3 +148,53 @@ def test_acc64_overflow_is_refused():
         fir_hip.fir1d_fixed_rows(x, hq, 12, 64, fir_hip.OUT_I32)
     # the same taps with a wrap to 64 - 1 bits are exact mod 2^64 and accepted
     assert fir_hip.fir1d_fixed_rows(x, hq, 12, 63, fir_hip.OUT_I32).tolist() == [0] * 16
+
+
+def test_table_cache_evicts_only_idle_tables():
+    """More distinct long tap tables than the per-device cache budget (256 MiB): 20 filters of
+    2^22 taps (16 MiB each) on the generic kernel, plus MFMA fragment tables, from two host
+    threads on two streams; every result bit-exact (dev_tables.hip frees a table only after the
+    launches that used it completed, never under a launch in flight)."""
+    import threading
+
+    co = c_oracle()
+    rng = np.random.default_rng(2222)
+    x = rng.integers(0, 256, 96, dtype=np.uint8)
+    L = 1 << 22
+    results, errors = {}, []
+
+    def worker(tid):
+        try:
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream(device=DEV)
+            with torch.cuda.stream(s):
+                xd = torch.from_numpy(x).to(DEV)
+                for k in range(10):
+                    hq = np.zeros(L, dtype=np.int32)
+                    idx = np.random.default_rng(100 * tid + k).integers(0, L, 64)
+                    hq[idx] = np.random.default_rng(7 + 100 * tid + k).integers(-4096, 4096, 64)
+                    hq[L // 2 - 2:L // 2 + 3] += np.array([-256, -1024, 6656, -1024, -256], dtype=np.int32)
+                    y = torch_ops.fir1d_fixed_rows_dev(xd, hq, 12, 32, fir_hip.OUT_U8_SAT)
+                    results[(tid, k)] = (hq, y)
+                s.synchronize()
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    ts = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+    for (tid, k), (hq, y) in sorted(results.items(), key=lambda kv: kv[0]):
+        want = co.fir1d_rows(x.reshape(1, -1), hq, 12, 32, co.OUT_U8_SAT).reshape(-1)
+        assert np.array_equal(y.cpu().numpy(), want), (tid, k)
+    # matrix-core fragment tables keyed by the taps: 300 distinct 257-tap filters, each exact
+    xs = rng.integers(0, 256, (4, 4096), dtype=np.uint8)
+    for k in range(300):
+        hq = np.random.default_rng(9000 + k).integers(-300, 300, 257).astype(np.int32)
+        if k % 37 == 0:
+            got = fir_hip.fir1d_fixed_rows(xs, hq, 12, 32, fir_hip.OUT_U8_SAT)
+            assert np.array_equal(got, co.fir1d_rows(xs, hq, 12, 32, co.OUT_U8_SAT)), k
+        else:
+            fir_hip.fir1d_fixed_rows(xs, hq, 12, 32, fir_hip.OUT_U8_SAT)

@@ -78,6 +78,15 @@ def test_input_prep_matches_oracle():
     assert np.array_equal(_prepare_x_u8(x.tolist()), fo.prep_x(x))
     xi = rng.integers(-1000, 1000, 100)
     assert np.array_equal(_prepare_x_u8(xi.tolist()), np.clip(xi, 0, 255).astype(np.uint8))
+    # the u8-range int list fast path (bytearray) and everything it must hand to the general path
+    xb = rng.integers(0, 256, 4499)
+    for lst in (xb.tolist(), tuple(xb.tolist()), list(xb.astype(np.uint8)), [True, False, 0, 255],
+                xb.tolist() + [256], [-1] + xb.tolist(), xb.tolist() + [3.5], [255.49, 7], []):
+        got = _prepare_x_u8(lst)
+        assert got.dtype == np.uint8 and got.flags.writeable
+        assert np.array_equal(got, fo.prep_x(np.asarray(lst, dtype=np.float64))), lst[:4]
+    with pytest.raises(ValueError, match=r"Invalid x\[2\]=nan: x must be finite"):
+        _prepare_x_u8([1, 2, float("nan")])
 
 
 def test_quantization_matches_oracle_on_random_sweep():
@@ -123,7 +132,9 @@ def test_parse_devices():
     assert parse_devices("2") == [0, 1]
     assert parse_devices("0,0,3") == [0, 0, 3]
     assert parse_devices([1, 1]) == [1, 1]
-    for bad in (0, "0", [], [-1]):
+    assert parse_devices("3,") == [3]  # one non-zero device id
+    assert parse_devices("1,2,") == [1, 2]
+    for bad in (0, "0", [], [-1], ","):
         with pytest.raises(ValueError):
             parse_devices(bad)
 

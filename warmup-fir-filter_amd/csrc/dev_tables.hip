@@ -3,13 +3,26 @@
 // Short filters travel in the kernel arguments; a filter of any length (the reference accepts
 // any len(h), fir_1d/model/python/fir_1d_fixed_ref.py:83-107) does not fit there, so its taps
 // are read from HBM.  The C ABI keeps taking host pointers; this cache uploads each distinct
-// table once per device and hands out its device address.
+// table once per device and hands out its device address for one launch at a time (TableHold):
+//
+//   * a table is keyed by a 128-bit hash of its content (or of the inputs it is built from, so a
+//     large derived table is built only on a miss) and its size;
+//   * every hold counts as in use until the launch it was taken for has been enqueued, and each
+//     use then records an event on the launch's stream; a table is freed only when it has no
+//     hold and every use event has completed, never by a device-wide sync (which would also
+//     invalidate another thread's stream capture);
+//   * a table used by a launch that was captured into a hipGraph is pinned for the process life
+//     (the graph keeps its address);
+//   * past kTableBudget bytes per device the cache frees idle tables; when none is idle it grows
+//     past the budget rather than fail a call.
 #include <hip/hip_runtime.h>
 
+#include <cstring>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "fir_launch.h"
@@ -18,12 +31,24 @@ namespace fir {
 
 namespace {
 
-constexpr size_t kTableBudget = size_t(256) << 20;  // bytes cached per device before a flush
+constexpr size_t kTableBudget = size_t(256) << 20;  // idle bytes kept per device
+
+struct Entry {
+    void* d = nullptr;
+    size_t bytes = 0;
+    int holds = 0;                  // acquired, launch not yet enqueued
+    bool pinned = false;            // used by a captured graph
+    std::vector<hipEvent_t> uses;   // one per enqueued use, pruned when complete
+};
+
+using Key = std::tuple<uint64_t, uint64_t, size_t>;
 
 struct TableCache {
     std::mutex mu;
     hipStream_t stream = nullptr;
-    std::map<std::string, void*> tables;  // content -> device copy
+    std::map<Key, Entry> tables;
+    std::map<const void*, Key> by_ptr;
+    std::vector<hipEvent_t> free_events;
     size_t bytes = 0;
 };
 
@@ -37,10 +62,43 @@ TableCache* cache_for(int dev) {
     return c.get();
 }
 
+// true when every recorded use of e has completed (completed events go back to the pool)
+bool idle(TableCache* c, Entry& e) {
+    size_t k = 0;
+    for (hipEvent_t ev : e.uses) {
+        if (hipEventQuery(ev) == hipSuccess) c->free_events.push_back(ev);
+        else e.uses[k++] = ev;
+    }
+    e.uses.resize(k);
+    return e.holds == 0 && !e.pinned && e.uses.empty();
+}
+
+void evict_idle(TableCache* c, size_t need) {
+    for (auto it = c->tables.begin(); it != c->tables.end() && c->bytes + need > kTableBudget;) {
+        if (idle(c, it->second)) {
+            (void)hipFree(it->second.d);
+            c->bytes -= it->second.bytes;
+            c->by_ptr.erase(it->second.d);
+            it = c->tables.erase(it);
+        } else {
+            ++it;
+        }
+    }
+}
+
 }  // namespace
 
-const void* device_table(const void* host, size_t bytes, std::string* err) {
-    if (!host || bytes == 0) {
+void TableHash::add(const void* p, size_t n) {
+    const uint8_t* b = (const uint8_t*)p;
+    for (size_t i = 0; i < n; ++i) {
+        a = (a ^ b[i]) * 0x100000001b3ull;                          // FNV-1a 64
+        c = (c + b[i] + 0x9E3779B97F4A7C15ull) * 0xff51afd7ed558ccdull;  // an independent mix
+        c ^= c >> 29;
+    }
+}
+
+const void* table_acquire(const TableHash& h, size_t bytes, const std::function<void(void*)>& fill, std::string* err) {
+    if (bytes == 0) {
         *err = "device_table: empty table";
         return nullptr;
     }
@@ -51,39 +109,81 @@ const void* device_table(const void* host, size_t bytes, std::string* err) {
         return nullptr;
     }
     TableCache* c = cache_for(dev);
-    std::string key((const char*)host, bytes);
+    const Key key{h.a, h.c, bytes};
     std::lock_guard<std::mutex> lk(c->mu);
     auto it = c->tables.find(key);
-    if (it != c->tables.end()) return it->second;
+    if (it != c->tables.end()) {
+        ++it->second.holds;
+        return it->second.d;
+    }
     if (!c->stream && (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
         *err = std::string("hipStreamCreateWithFlags: ") + hipGetErrorString(e);
         return nullptr;
     }
-    if (c->bytes + bytes > kTableBudget && !c->tables.empty()) {
-        // every launch that may still read a cached table must have finished before it is freed
-        if ((e = hipDeviceSynchronize()) != hipSuccess) {
-            *err = std::string("hipDeviceSynchronize: ") + hipGetErrorString(e);
-            return nullptr;
-        }
-        for (auto& kv : c->tables) (void)hipFree(kv.second);
-        c->tables.clear();
-        c->bytes = 0;
-    }
+    evict_idle(c, bytes);
+    std::vector<uint8_t> host(bytes);
+    fill(host.data());
     void* d = nullptr;
     if ((e = hipMalloc(&d, bytes)) != hipSuccess) {
         *err = std::string("hipMalloc(") + std::to_string(bytes) + "): " + hipGetErrorString(e);
         return nullptr;
     }
     // complete before this returns, so any later launch on any stream sees the whole table
-    if ((e = hipMemcpyAsync(d, host, bytes, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+    if ((e = hipMemcpyAsync(d, host.data(), bytes, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
         (e = hipStreamSynchronize(c->stream)) != hipSuccess) {
         (void)hipFree(d);
         *err = std::string("table upload: ") + hipGetErrorString(e);
         return nullptr;
     }
-    c->tables.emplace(std::move(key), d);
+    Entry& en = c->tables[key];
+    en.d = d;
+    en.bytes = bytes;
+    en.holds = 1;
+    c->by_ptr[d] = key;
     c->bytes += bytes;
     return d;
+}
+
+void table_release(const void* d, hipStream_t stream, bool launched) {
+    if (!d) return;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    TableCache* c = cache_for(dev);
+    std::lock_guard<std::mutex> lk(c->mu);
+    auto pit = c->by_ptr.find(d);
+    if (pit == c->by_ptr.end()) return;
+    Entry& en = c->tables[pit->second];
+    if (en.holds > 0) --en.holds;
+    if (!launched) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+        en.pinned = true;  // a graph holds the address for as long as it lives
+        return;
+    }
+    hipEvent_t ev = nullptr;
+    if (!c->free_events.empty()) {
+        ev = c->free_events.back();
+        c->free_events.pop_back();
+    } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+        en.pinned = true;  // cannot track the use: never free it
+        return;
+    }
+    if (hipEventRecord(ev, stream) != hipSuccess) {
+        c->free_events.push_back(ev);
+        en.pinned = true;
+        return;
+    }
+    en.uses.push_back(ev);
+}
+
+const void* device_table(const void* host, size_t bytes, std::string* err) {
+    if (!host) {
+        *err = "device_table: empty table";
+        return nullptr;
+    }
+    TableHash h;
+    h.add(host, bytes);
+    return table_acquire(h, bytes, [&](void* dst) { std::memcpy(dst, host, bytes); }, err);
 }
 
 }  // namespace fir

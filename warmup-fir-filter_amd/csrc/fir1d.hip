@@ -149,6 +149,7 @@ static hipError_t launch_generic(const void* x, void* y, int64_t start, int64_t 
     std::string err;
     const int32_t* td = (const int32_t*)device_table(hq, sizeof(int32_t) * (size_t)L, &err);
     if (!td) return hipErrorOutOfMemory;
+    TableHold hold(td, stream);
     const int64_t blocks = (end - start + kGenTile - 1) / kGenTile;
     if (blocks >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
     hipLaunchKernelGGL((fir1d_generic_kernel<InT, STAGE>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
@@ -349,6 +350,7 @@ int launch_fir1d_edges(const void* x, int in_dtype, int64_t n, int ch, const int
     } else if (hle + hre > 0) {  // both edges, one launch
         const int32_t* td = (const int32_t*)device_table(hq, sizeof(int32_t) * (size_t)L, err);
         if (!td) return FIR_ENOMEM;
+        TableHold hold(td, stream);
         if (in_dtype == FIR_IN_U8)
             e = stage == FIR_OUT_U8_SAT
                     ? launch_edges<uint8_t, FIR_OUT_U8_SAT>(x, y, total, ch, hl, hr, td, L, hle, hre, frac, acc_bits, stream)

@@ -59,6 +59,9 @@ constexpr int kMfMaxBlocks = FIR_MFMA_MAXBLOCKS;
 #ifndef FIR_MFMA_LONG_FROM           // filters longer than this take the chunked kernel (A/B: lower)
 #define FIR_MFMA_LONG_FROM 64
 #endif
+#ifndef FIR_MFMA_MAX_TAPS            // longest filter on the matrix cores (fragment table <= 4 MiB)
+#define FIR_MFMA_MAX_TAPS 65536
+#endif
 #ifndef FIR_MFMA_LONG_BLOCKS         // grid-stride blocks of the chunked kernel
 #define FIR_MFMA_LONG_BLOCKS 2048
 #endif
@@ -831,20 +834,26 @@ __global__ __launch_bounds__(kBlock) void fir1d_mfma_long_kernel(const InT* __re
 
 // frag[s][p][lane] = bytes j = 0..15 of plane p (0: hl, 1: hh) of the diagonal entries
 // e = 31 - r + 32 s + 16 hf + j (lane = r + 32 hf), as MfmaTaps lays them out
+// (keyed by the taps and the geometry: the table is built only on a cache miss)
 static const mf_i32x4* mfma_frag_table(const int32_t* hq, int L, int P, int KS, std::string* err) {
     const int c = L / 2;
-    std::vector<int8_t> tab((size_t)KS * 2 * kWave * 16);
-    for (int st = 0; st < KS; ++st)
-        for (int lane = 0; lane < kWave; ++lane)
-            for (int j = 0; j < 16; ++j) {
-                const int e = 31 - (lane & 31) + 32 * st + 16 * (lane >> 5) + j;
-                const int tap = 31 - e + c + P;
-                const int v = tap >= 0 && tap < L ? hq[tap] : 0;
-                const int lo = ((v + 128) & 255) - 128;
-                tab[(((size_t)st * 2 + 0) * kWave + lane) * 16 + j] = (int8_t)lo;
-                tab[(((size_t)st * 2 + 1) * kWave + lane) * 16 + j] = (int8_t)((v - lo) / 256);
-            }
-    return (const mf_i32x4*)device_table(tab.data(), tab.size(), err);
+    TableHash h;
+    h.add(hq, sizeof(int32_t) * (size_t)L);
+    h.add_val(L), h.add_val(P), h.add_val(KS);
+    const size_t bytes = (size_t)KS * 2 * kWave * 16;
+    return (const mf_i32x4*)table_acquire(h, bytes, [&](void* dst) {
+        int8_t* tab = (int8_t*)dst;
+        for (int st = 0; st < KS; ++st)
+            for (int lane = 0; lane < kWave; ++lane)
+                for (int j = 0; j < 16; ++j) {
+                    const int e = 31 - (lane & 31) + 32 * st + 16 * (lane >> 5) + j;
+                    const int tap = 31 - e + c + P;
+                    const int v = tap >= 0 && tap < L ? hq[tap] : 0;
+                    const int lo = ((v + 128) & 255) - 128;
+                    tab[(((size_t)st * 2 + 0) * kWave + lane) * 16 + j] = (int8_t)lo;
+                    tab[(((size_t)st * 2 + 1) * kWave + lane) * 16 + j] = (int8_t)((v - lo) / 256);
+                }
+    }, err);
 }
 
 template <typename InT, int STAGE>
@@ -854,6 +863,7 @@ static hipError_t launch_mfma_long(const void* x, void* y, int64_t rl, int64_t t
     std::string err;
     const mf_i32x4* fr = mfma_frag_table(hq, L, P, KS, &err);
     if (!fr) return hipErrorOutOfMemory;
+    TableHold hold(fr, s);
     const int64_t want = (ntiles + kMfWaves - 1) / kMfWaves;
     const unsigned blocks = (unsigned)(want < FIR_MFMA_LONG_BLOCKS ? want : FIR_MFMA_LONG_BLOCKS);
     if (fast)
@@ -908,6 +918,7 @@ static hipError_t launch_mfma_ks(const void* x, void* y, int64_t rowlen, int64_t
     else
         hipLaunchKernelGGL((fir1d_mfma_kernel<InT, STAGE, KS, false, false>), dim3(blocks), dim3(kBlock), 0, s,
                            (const InT*)x, (OutT*)y, rowlen, tpr, ntiles, t, fr, P, bias, 32 - acc_bits, frac);
+    if (fr) table_release(fr, s);  // (A/B variant's table) after the launch that reads it
     return hipGetLastError();
 }
 
@@ -946,7 +957,9 @@ bool mfma_path_ok(const void* x, const void* y, int in_dtype, int64_t rows, int6
     for (int k = 0; k < L; ++k) taps_ok &= hq[k] >= -32768 && hq[k] <= 32639;
     // the tile index is a uint32 (one tile = 1024 outputs of one row)
     const int64_t ntiles = rows > 1 ? rows * ((rowlen + kMfTile - 1) / kMfTile) : (total + kMfTile - 1) / kMfTile;
-    return L >= 2 && ch == 1 && taps_ok && acc_bits <= 32 && frac <= 31 &&
+    // filters up to FIR_MFMA_MAX_TAPS (fragment table KS x 2 KiB <= ~4 MiB); longer ones take the
+    // generic kernel (a table near the 2^24-tap limit would be 512 MiB)
+    return L >= 2 && L <= FIR_MFMA_MAX_TAPS && ch == 1 && taps_ok && acc_bits <= 32 && frac <= 31 &&
            (rows == 1 ? total : rowlen) % 8 == 0 &&  // row and tile edges on 8-sample vectors
            (uintptr_t)x % (in_dtype == FIR_IN_U8 ? 8 : 16) == 0 && (uintptr_t)y % 16 == 0 && total >= 8 &&
            total < ((int64_t)1 << 40) && ntiles < ((int64_t)1 << 32) - kMfMaxBlocks * kMfWaves;

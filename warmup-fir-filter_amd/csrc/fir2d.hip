@@ -330,6 +330,7 @@ int launch_fir2d(const uint8_t* x, int64_t frames, int64_t H, int64_t W, const i
         if ((W + kBlock - 1) / kBlock >= ((int64_t)1 << 31)) return *err = "width too large", FIR_EINVAL;
         const int32_t* td = (const int32_t*)device_table(hq, sizeof(int32_t) * (size_t)ntaps, err);
         if (!td) return FIR_ENOMEM;
+        TableHold hold(td, stream);
         dim3 grid((unsigned)((W + kBlock - 1) / kBlock), (unsigned)std::min<int64_t>(H, 65535), (unsigned)frames);
         if (stage == FIR_OUT_U8_SAT)
             hipLaunchKernelGGL((fir2d_generic_kernel<FIR_OUT_U8_SAT>), grid, dim3(kBlock), 0, stream, x, (uint8_t*)y, H,

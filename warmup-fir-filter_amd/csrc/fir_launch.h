@@ -4,15 +4,36 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <functional>
 #include <string>
 
 namespace fir {
 
-// Device copy of a host table (long tap sets, matrix-core tap fragments) on the current device,
-// cached by content: uploaded once (complete before this returns), kept for the process life
-// (dev_tables.hip).  nullptr + *err on failure.  The first use of a table cannot be captured
-// in a hipGraph (warm up before capturing).
-const void* device_table(const void* host, size_t bytes, std::string* err);
+// Device copies of host tables (long tap sets, matrix-core tap fragments) on the current device
+// (dev_tables.hip): cached by a 128-bit hash of their content, or of the inputs they are built
+// from (table_acquire builds the table with `fill` only on a miss), uploaded once (complete
+// before the call returns).  Every acquire is a hold on the table for ONE launch, released by
+// table_release after that launch is enqueued on `stream` (TableHold does it at scope exit): the
+// cache frees a table only when no hold is outstanding and every launch that used it has
+// completed; a table used inside a stream capture is kept for the process life.  nullptr + *err
+// on failure.  The first use of a table cannot be captured in a hipGraph (warm up before capturing).
+struct TableHash {
+    uint64_t a = 0xcbf29ce484222325ull, c = 0x84222325cbf29ce4ull;
+    void add(const void* p, size_t n);
+    template <typename T>
+    void add_val(const T& v) { add(&v, sizeof(v)); }
+};
+const void* table_acquire(const TableHash& h, size_t bytes, const std::function<void(void*)>& fill, std::string* err);
+void table_release(const void* d, hipStream_t stream, bool launched = true);
+const void* device_table(const void* host, size_t bytes, std::string* err);  // table_acquire by content
+struct TableHold {  // one launch's hold: released (its use recorded on `s`) when the scope ends
+    const void* p;
+    hipStream_t s;
+    TableHold(const void* p_, hipStream_t s_) : p(p_), s(s_) {}
+    TableHold(const TableHold&) = delete;
+    TableHold& operator=(const TableHold&) = delete;
+    ~TableHold() { table_release(p, s); }
+};
 
 // Enqueue the row-wise 1-D fixed FIR on `stream`; device pointers.  Returns fir_status.
 int launch_fir1d_rows(const void* x, int in_dtype, int64_t rows, int64_t width, int ch, const int32_t* hq, int L,

@@ -122,6 +122,7 @@ int launch_fir1d_ideal(const uint8_t* x, int64_t rows, int64_t width, const doub
     }
     const double* td = (const double*)device_table(h, sizeof(double) * (size_t)L, err);
     if (!td) return FIR_ENOMEM;
+    TableHold hold(td, stream);
     const int64_t blocks = (total + kIdealTile - 1) / kIdealTile;
     if (blocks >= ((int64_t)1 << 31)) return *err = "too many samples for one launch", FIR_EINVAL;
     hipLaunchKernelGGL(fir1d_ideal_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, x, y, total, width,

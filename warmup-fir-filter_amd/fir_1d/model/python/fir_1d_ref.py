@@ -67,7 +67,17 @@ def _clamp_x(x: np.ndarray) -> np.ndarray:
 
 
 def _prepare_x_u8(x) -> np.ndarray:
-    """Validation + round-half-up + clamp + uint8 cast (fir_1d_fixed_ref.py:34-36,75)."""
+    """Validation + round-half-up + clamp + uint8 cast (fir_1d_fixed_ref.py:34-36,75).
+
+    A list / tuple whose samples are all ints in [0, 255] (the reference's row driver passes
+    ``row.tolist()`` of a uint8 image, gen_fixed_output.py:44-52) has nothing to validate,
+    round or clamp: it converts in one C loop (bytearray), ~15x faster than np.asarray of the
+    list; any other list (floats, values outside [0, 255]) takes the general path below."""
+    if isinstance(x, (list, tuple)):
+        try:
+            return np.frombuffer(bytearray(x), dtype=np.uint8)
+        except (TypeError, ValueError):
+            pass
     x1 = _validate_x(x)
     return np.ascontiguousarray(_clamp_x(_round_half_up_x(x1)), dtype=np.uint8)
 

@@ -231,11 +231,12 @@ def fir1d_fixed_rows_sharded(x: np.ndarray, hq, frac_bits: int = 12, acc_bits: i
 
 def parse_devices(spec) -> list[int]:
     """A ``--devices`` value: N (devices 0..N-1), a comma list of ids (repeats allowed: a
-    device then takes several row blocks in turn), or a sequence of ids; None = [0]."""
+    device then takes several row blocks in turn; a trailing comma makes one id a list, so
+    "3," is device 3 alone), or a sequence of ids; None = [0]."""
     if spec is None:
         return [0]
     if isinstance(spec, str):
-        spec = [int(v) for v in spec.split(",")] if "," in spec else int(spec)
+        spec = [int(v) for v in spec.split(",") if v.strip()] if "," in spec else int(spec)
     if isinstance(spec, (int, np.integer)):
         if spec < 1:
             raise ValueError("--devices N needs N >= 1")
@@ -285,7 +286,9 @@ def fir1d_fixed_rows_multi(x: np.ndarray, hq2, frac_bits: int = 12, acc_bits: in
     """F filters (rows of the F x L array hq2) over the same x in one call; returns an
     array of shape (F, *x.shape).  u8 input is read once per 4 filters on the GPU.
     ``devices`` (a list, see parse_devices) spreads the rows over several devices."""
-    if devices is not None and len(parse_devices(devices)) > 1 and np.ndim(x) >= 2:
+    if devices is not None and len(parse_devices(devices)) == 1:
+        device = parse_devices(devices)[0]  # one id: that device (as fir1d_ideal_rows does)
+    elif devices is not None and np.ndim(x) >= 2:
         x = np.ascontiguousarray(x)
         rowlen = x.shape[-1]
         x2 = x.reshape(-1, rowlen)
