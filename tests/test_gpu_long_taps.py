@@ -198,3 +198,22 @@ def test_table_cache_evicts_only_idle_tables():
             assert np.array_equal(got, co.fir1d_rows(xs, hq, 12, 32, co.OUT_U8_SAT)), k
         else:
             fir_hip.fir1d_fixed_rows(xs, hq, 12, 32, fir_hip.OUT_U8_SAT)
+
+
+@pytest.mark.parametrize("L", [65, 66, 100, 129, 257, 449, 450, 500, 1000, 2048, 4099])
+def test_u8_long_filter_run_kernel_vs_oracle(L):
+    """u8 filters past 64 taps (fir1d_mfma_run_kernel: runs of 4 tiles, k-step chunks of 16,
+    LDS-DMA windows): single-chunk and multi-chunk tap counts on both sides of KS = 16, rows
+    whose runs cross row ends (tiles per row not a multiple of 4), one long row, both stages,
+    the no-wrap fast form, 24-bit wrap and 32-bit taps near the int16 byte-split limit."""
+    rng = np.random.default_rng(L)
+    co = c_oracle()
+    shapes = [(16, 4096), (5, 5 * 1024 + 8), (1, (1 << 18) + 64)]
+    for shape in shapes:
+        x = rng.integers(0, 256, shape, dtype=np.uint8)
+        for frac, acc, amp in ((12, 32, 400), (16, 24, 3000), (12, 32, 32639)):
+            hq = rng.integers(-amp, amp + 1, L)
+            for stage in (fir_hip.OUT_U8_SAT, fir_hip.OUT_I32):
+                got = fir_hip.fir1d_fixed_rows(x, hq, frac, acc, stage)
+                want = co.fir1d_rows(x, hq, frac, acc, stage)
+                assert np.array_equal(got, want), (shape, frac, acc, amp, stage)

@@ -68,6 +68,7 @@ for s in $STEPS; do
         metab) run metab 300 python tools/metrics_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_old.so \
                  abrun/libfir_hip_oldnoasm.so abrun/libfir_hip_glds0.so abrun/libfir_hip_glds768.so abrun/libfir_hip_glds256.so; fatal $? ;;
         rowlat) run rowlat 300 python tools/row_call_latency.py "$OUT/row_call_latency.json"; fatal $? ;;
+        ltr) run long_taps_rate 300 python tools/long_taps_rate.py 31,64,65,66,128,257,450,500,1000,2048,4099; fatal $? ;;
         asan) run asan 600 make -C warmup-fir-filter_amd/csrc asan-check; fatal $? ;;
         micro) run micro 300 tools/microbench/fir_micro 28 20; fatal $? ;;
         micro2d) run micro2d 300 tools/microbench/fir2d_micro 15; fatal $? ;;

@@ -25,6 +25,7 @@
 // loop.  Outputs go back through the same LDS as whole 1 KiB rows.  Rows (images) whose length
 // is a multiple of 8 are tiled row by row, samples of other rows zeroed while staging.
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "fir_common.h"
@@ -56,8 +57,11 @@ constexpr int kMfMaxBlocks = FIR_MFMA_MAXBLOCKS;
 #ifndef FIR_MFMA_XCD                 // XCD-major tile order (A/B)
 #define FIR_MFMA_XCD 0
 #endif
-#ifndef FIR_MFMA_LONG_FROM           // filters longer than this take the chunked kernel (A/B: lower)
-#define FIR_MFMA_LONG_FROM 64
+#ifndef FIR_MFMA_LONG_FROM           // filters longer than this take the chunked kernels (A/B: lower);
+#define FIR_MFMA_LONG_FROM 65        // 65 taps still fit the step kernel's 3 k-steps (K = 96)
+#endif
+#ifndef FIR_MR                       // 0: u8 long filters on fir1d_mfma_long_kernel (A/B)
+#define FIR_MR 1
 #endif
 #ifndef FIR_MFMA_MAX_TAPS            // longest filter on the matrix cores (fragment table <= 4 MiB)
 #define FIR_MFMA_MAX_TAPS 65536
@@ -878,6 +882,212 @@ static hipError_t launch_mfma_long(const void* x, void* y, int64_t rl, int64_t t
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------
+// u8 filters past the step kernel's 3 k-steps (round 4; fir1d_mfma_long_kernel stays for int16).
+// The long kernel above re-fetches every k-step's tap fragments from L2 for every tile: 2 KiB
+// per k-step and tile, i.e. (4099 taps, 130 k-steps) 260 KiB of L2 reads per 1 KiB of samples,
+// an L2-bound loop at 2.5-28 % of the HBM roofline.  Here a wave owns a RUN of
+// kMrTps consecutive tiles (of any rows: each tile keeps its own window and row bounds) and
+// walks the k-steps in chunks of kMrC: a chunk's tap fragments (kMrC x 2 x 16 B per lane, 128
+// VGPRs) are loaded once and feed all the run's tiles, so fragment traffic drops kMrTps-fold,
+// and when KS <= kMrC (up to ~450 taps) they are loaded once per wave for the whole grid-stride
+// loop.  The run's accumulators (2 x 16 int32 per tile) stay in AGPRs across chunks; one wave per
+// SIMD.  Windows (1024 + 32 kMrC - 32 samples per tile and chunk) arrive by LDS-DMA
+// (buffer_load ... lds, the descriptor's range check zero-fills samples outside the tile's row),
+// double-buffered: the next iteration's windows are in flight while this one's MFMAs run, with
+// no VGPRs held.  The bytes land unsigned; the B fragment is XORed with 0x80 after its LDS read
+// (xs = x - 128, as in every other kernel here).  The left halo P is rounded to 16 so a window
+// vector never straddles a row start.
+#ifndef FIR_MR_BLOCKS                // grid-stride blocks (4 waves, one per SIMD)
+#define FIR_MR_BLOCKS 256
+#endif
+#ifndef FIR_MR_TPS                   // tiles per run
+#define FIR_MR_TPS 4
+#endif
+#ifndef FIR_MR_C                     // k-steps per chunk
+#define FIR_MR_C 16
+#endif
+constexpr int kMrTps = FIR_MR_TPS, kMrC = FIR_MR_C;
+constexpr int kMrTileLds = 2048;     // LDS bytes per tile window (128 vectors of 16 samples)
+
+template <int STAGE, bool ACC32, bool FAST, bool MULTI>
+__global__ __launch_bounds__(kBlock, 1) void fir1d_mfma_run_kernel(const uint8_t* __restrict__ x,
+                                                                   typename OutTraits<STAGE>::T* __restrict__ y,
+                                                                   int64_t rowlen, uint32_t tiles_per_row, uint32_t ntiles,
+                                                                   const mf_i32x4* __restrict__ frag, int KS, int P,
+                                                                   uint32_t bias, int shl, int frac) {
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    constexpr int TPS = kMrTps, C = kMrC;
+    constexpr int WT = kMfTile + 32 * C - 32;  // window samples per tile and chunk
+    constexpr int NVT = (WT + 15) / 16;         // 16-sample vectors per tile window
+    static_assert(NVT > kWave && NVT <= 2 * kWave && 16 * 2 * kWave <= kMrTileLds, "two DMAs per tile window");
+    constexpr bool OLDS = STAGE == FIR_OUT_I32;
+    constexpr int BUF = TPS * kMrTileLds;
+    constexpr int NDMA = 2 * TPS;               // DMA instructions per iteration
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kMfWaves][2 * BUF + (OLDS ? 4608 : 16)];
+
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & 31, hf = lane >> 5;
+    uint32_t* ob = reinterpret_cast<uint32_t*>(lds[wv] + 2 * BUF);
+    const int32_t sat_hi = FAST ? (int32_t)((256u << (frac & 31)) - 1u) : 0;
+    const int nch = (KS + C - 1) / C;
+    const uint32_t nruns = (ntiles + TPS - 1) / TPS;
+    const uint32_t stride = gridDim.x * kMfWaves;
+    uint32_t rn = blockIdx.x * kMfWaves + wv;
+    if (rn >= nruns) return;  // wave-uniform: nothing issued yet
+
+    mf_i32x4 a_lo[C], a_hi[C];
+    auto load_a = [&](int c) __attribute__((always_inline)) {
+        const mf_i32x4* f = frag + (int64_t)c * C * 2 * kWave + lane;
+#pragma unroll
+        for (int s = 0; s < C; ++s) a_lo[s] = f[(2 * s) * kWave], a_hi[s] = f[(2 * s + 1) * kWave];
+    };
+    // the run's TPS tile windows of chunk c into LDS buffer `buf`: per tile two 1 KiB DMAs
+    // (vectors lane and lane + 64; the second past the window's NVT vectors reads zeros)
+    auto issue_win = [&](uint32_t run, int c, int buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int q = 0; q < TPS; ++q) {
+            const uint32_t t = run < nruns ? run * TPS + q : ntiles;
+            const MfTile tl = mf_tile(t < ntiles ? t : ntiles - 1, rowlen, tiles_per_row);
+            const int64_t w0 = tl.ts - P + 32 * (int64_t)C * c;
+            const int64_t base = w0 > tl.rs ? w0 : tl.rs, end = tl.re < w0 + WT ? tl.re : w0 + WT;
+            const __amdgpu_buffer_rsrc_t rd = mf_rsrc(x + base, (uint32_t)(end > base && t < ntiles ? end - base : 0));
+            const uint32_t skip = (uint32_t)(base - w0);  // samples of the window before the row (multiple of 16)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const uint32_t v16 = 16u * (uint32_t)(lane + kWave * i);
+                const uint32_t off = v16 >= skip && (i == 0 || lane + kWave < NVT) ? v16 - skip : kMfOff;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rd, (__attribute__((address_space(3))) void*)(lds[wv] + buf * BUF + q * kMrTileLds + 1024 * i), 16, off,
+                    0, 0, 0);
+            }
+        }
+    };
+
+    mf_i32x16 acc_ll[TPS], acc_mid[TPS];
+#pragma unroll
+    for (int q = 0; q < TPS; ++q) acc_ll[q] = mf_i32x16{}, acc_mid[q] = mf_i32x16{};
+    if constexpr (!MULTI) load_a(0);  // KS <= C: one chunk, fragments loaded once
+    int c = 0, buf = 0;
+    issue_win(rn, 0, 0);
+    for (;;) {
+        // the next iteration: the next chunk of this run, or chunk 0 of the next run (past the
+        // last: a run past nruns, whose zero-size descriptors move nothing -- every path issues the
+        // same NDMA operations, so the counted wait below is exact)
+        int nc = c + 1;
+        uint32_t nr = rn;
+        if (nc == nch) nc = 0, nr = rn + stride;
+        if constexpr (MULTI) load_a(c);  // issued before the next windows: its wait leaves them in flight
+        issue_win(nr, nc, buf ^ 1);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");  // this iteration's windows (and A) landed
+        __builtin_amdgcn_wave_barrier();
+        const uint8_t* pl = lds[wv] + buf * BUF;
+        const int steps = min(C, KS - C * c);
+#pragma unroll
+        for (int s = 0; s < C; ++s) {
+            if (s < steps) {
+#pragma unroll
+                for (int q = 0; q < TPS; ++q) {
+                    const mf_i32x4 bu = *reinterpret_cast<const mf_i32x4*>(&pl[q * kMrTileLds + 32 * r + 32 * s + 16 * hf]);
+                    const mf_i32x4 b = bu ^ (int)0x80808080;
+                    acc_ll[q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_lo[s], b, acc_ll[q], 0, 0, 0);
+                    acc_mid[q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_hi[s], b, acc_mid[q], 0, 0, 0);
+                }
+            }
+        }
+        if (c == nch - 1) {  // the run's tiles are complete: combine, round, stage, store
+#pragma unroll
+            for (int q = 0; q < TPS; ++q) {
+                const uint32_t t = rn * TPS + q;
+                const MfTile tl = mf_tile(t < ntiles ? t : ntiles - 1, rowlen, tiles_per_row);
+                const int m = t < ntiles ? (int)min((int64_t)kMfTile, tl.re - tl.ts) : 0;
+                int32_t o[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const uint32_t a = (((uint32_t)acc_mid[q][i] << 8) + (uint32_t)acc_ll[q][i]) + bias;
+                    if constexpr (FAST)
+                        o[i] = STAGE == FIR_OUT_U8_SAT ? (int32_t)mf_med3_0(a, sat_hi) : (int32_t)a >> frac;
+                    else
+                        o[i] = round_acc<ACC32>(a, shl, frac);
+                }
+                acc_ll[q] = mf_i32x16{}, acc_mid[q] = mf_i32x16{};
+                if constexpr (STAGE == FIR_OUT_U8_SAT) {
+                    uint32_t w[4];
+#pragma unroll
+                    for (int g4 = 0; g4 < 4; ++g4) {
+                        if constexpr (FAST)
+                            w[g4] = mf_shr_byte<3>(mf_shr_byte<2>(mf_shr_byte<1>((uint32_t)o[4 * g4] >> frac, (uint32_t)o[4 * g4 + 1], frac),
+                                                                  (uint32_t)o[4 * g4 + 2], frac),
+                                                   (uint32_t)o[4 * g4 + 3], frac);
+                        else
+                            w[g4] = (uint32_t)stage_out32<STAGE>(o[4 * g4]) | ((uint32_t)stage_out32<STAGE>(o[4 * g4 + 1]) << 8) |
+                                    ((uint32_t)stage_out32<STAGE>(o[4 * g4 + 2]) << 16) |
+                                    ((uint32_t)stage_out32<STAGE>(o[4 * g4 + 3]) << 24);
+                    }
+                    const auto s02 = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
+                    const auto s13 = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
+                    __builtin_amdgcn_raw_buffer_store_b128(mf_i32x4{(int)s02[0], (int)s02[1], (int)s13[0], (int)s13[1]},
+                                                           mf_rsrc(y + tl.ts, (uint32_t)m), (uint32_t)(32 * r + 16 * hf), 0,
+                                                           kMfAuxNt);
+                } else {
+                    __builtin_amdgcn_wave_barrier();
+                    asm volatile("" ::: "memory");
+#pragma unroll
+                    for (int g4 = 0; g4 < 4; ++g4)
+                        *reinterpret_cast<u4*>(&ob[36 * r + 8 * g4 + 4 * hf]) =
+                            u4{(uint32_t)o[4 * g4], (uint32_t)o[4 * g4 + 1], (uint32_t)o[4 * g4 + 2], (uint32_t)o[4 * g4 + 3]};
+                    __builtin_amdgcn_wave_barrier();
+                    asm volatile("" ::: "memory");
+                    const __amdgpu_buffer_rsrc_t rd = mf_rsrc(y + tl.ts, (uint32_t)m * 4u);
+#pragma unroll
+                    for (int rho = 0; rho < 4; ++rho) {
+                        const int oo = 256 * rho + 4 * lane;
+                        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const mf_i32x4*>(&ob[36 * (oo >> 5) + (oo & 31)]),
+                                                               rd, (uint32_t)oo * 4u, 0, kMfAuxNt);
+                    }
+                }
+            }
+        }
+        if (nr >= nruns) break;
+        rn = nr, c = nc, buf ^= 1;
+        __builtin_amdgcn_wave_barrier();  // this iteration's B reads are done before its buffer is refilled
+        asm volatile("" ::: "memory");
+    }
+}
+
+template <int STAGE>
+static hipError_t launch_mfma_run(const void* x, void* y, int64_t rl, int64_t tpr, int64_t ntiles, const int32_t* hq,
+                                  int L, int P, int KS, uint32_t bias, bool fast, int frac, int acc_bits, hipStream_t s) {
+    using OutT = typename OutTraits<STAGE>::T;
+    std::string err;
+    const int ksp = (KS + kMrC - 1) / kMrC * kMrC;  // the table padded to whole chunks (zero fragments)
+    const mf_i32x4* fr = mfma_frag_table(hq, L, P, ksp, &err);
+    if (!fr) return hipErrorOutOfMemory;
+    TableHold hold(fr, s);
+    const int64_t nruns = (ntiles + kMrTps - 1) / kMrTps;
+    const int64_t want = (nruns + kMfWaves - 1) / kMfWaves;
+    const unsigned blocks = (unsigned)(want < FIR_MR_BLOCKS ? want : FIR_MR_BLOCKS);
+    const uint32_t tp = (uint32_t)tpr, nt = (uint32_t)ntiles;
+    auto go = [&](auto multi) {
+        constexpr bool M = decltype(multi)::value;
+        if (fast)
+            hipLaunchKernelGGL((fir1d_mfma_run_kernel<STAGE, true, true, M>), dim3(blocks), dim3(kBlock), 0, s,
+                               (const uint8_t*)x, (OutT*)y, rl, tp, nt, fr, KS, P, bias, 0, frac);
+        else if (acc_bits == 32)
+            hipLaunchKernelGGL((fir1d_mfma_run_kernel<STAGE, true, false, M>), dim3(blocks), dim3(kBlock), 0, s,
+                               (const uint8_t*)x, (OutT*)y, rl, tp, nt, fr, KS, P, bias, 0, frac);
+        else
+            hipLaunchKernelGGL((fir1d_mfma_run_kernel<STAGE, false, false, M>), dim3(blocks), dim3(kBlock), 0, s,
+                               (const uint8_t*)x, (OutT*)y, rl, tp, nt, fr, KS, P, bias, 32 - acc_bits, frac);
+    };
+    if (KS > kMrC)
+        go(std::true_type{});
+    else
+        go(std::false_type{});
+    return hipGetLastError();
+}
+
 template <typename InT, int STAGE, int KS>
 static hipError_t launch_mfma_ks(const void* x, void* y, int64_t rowlen, int64_t tpr, int64_t ntiles, const MfmaTaps& t,
                                  const int32_t* hq, int L, int P, uint32_t bias, bool fast, int frac, int acc_bits,
@@ -938,7 +1148,14 @@ static hipError_t launch_mfma_t(const void* x, void* y, int64_t rows, int64_t ro
     const int64_t rl = rows > 1 ? rowlen : total;
     const int64_t tpr = (rl + kMfTile - 1) / kMfTile;
     const int64_t ntiles = (rows > 1 ? rows : 1) * tpr;
-    if (L > FIR_MFMA_LONG_FROM) return launch_mfma_long<InT, STAGE>(x, y, rl, tpr, ntiles, hq, L, P, KS, bias, fast, frac, acc_bits, s);
+    if constexpr (sizeof(InT) == 1) {
+        if (KS > 3 && FIR_MR) {  // u8 past the step kernel: the run kernel (halo rounded to 16)
+            const int P16 = (hl + 15) & ~15, K16 = 32 + c + P16, KS16 = (K16 + 31) / 32;
+            return launch_mfma_run<STAGE>(x, y, rl, tpr, ntiles, hq, L, P16, KS16, bias, fast, frac, acc_bits, s);
+        }
+    }
+    if (KS > 3 || L > FIR_MFMA_LONG_FROM)
+        return launch_mfma_long<InT, STAGE>(x, y, rl, tpr, ntiles, hq, L, P, KS, bias, fast, frac, acc_bits, s);
     MfmaTaps t;
     for (int e = 0; e < 128; ++e) {
         const int tap = 31 - e + c + P;
