@@ -453,6 +453,9 @@ def main() -> int:
     ap.add_argument("--log2n", type=int, default=28, help="int16 values per GPU (2^28 = BASELINE configs[1])")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0 = skip)")
     ap.add_argument("--no-parity", action="store_true", help="skip the full-size oracle comparison")
+    ap.add_argument("--roofline-launches", type=int, default=ROOF_LAUNCHES,
+                    help="timed launches of the dominant kernel (after as many as --roofline-ramp untimed)")
+    ap.add_argument("--roofline-ramp", type=int, default=ROOF_RAMP)
     args = ap.parse_args()
 
     if args.gpus < 1:
@@ -531,15 +534,16 @@ def main() -> int:
     # events (events between launches would perturb the stream: each record adds a ~11 us gap).
     # Average duration = event time / launches.  Independent of --steps / --warmup.
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for _ in range(ROOF_RAMP):
+    n_roof = max(1, args.roofline_launches)
+    for _ in range(max(0, args.roofline_ramp)):
         wl.dominant()
     torch.cuda.synchronize()
     ev0.record()
-    for _ in range(ROOF_LAUNCHES):
+    for _ in range(n_roof):
         wl.dominant()
     ev1.record()
     ev1.synchronize()
-    kern_avg_s = ev0.elapsed_time(ev1) / 1e3 / ROOF_LAUNCHES
+    kern_avg_s = ev0.elapsed_time(ev1) / 1e3 / n_roof
 
     wl.step()  # restore the full step's output (the loop above ran the bulk kernel alone)
     torch.cuda.synchronize()
@@ -639,8 +643,8 @@ def main() -> int:
                                  "strips share are read once, PMC 1.001x; DESIGN.md §5)")
                      if args.workload == "fir2d_u8" else "HBM",
                      "kernel_avg_us": round(kern_avg_s * 1e6, 2), "algorithmic_bytes_per_launch": alg_bytes,
-                     "timing": f"HIP events around {ROOF_LAUNCHES} back-to-back launches of the kernel after "
-                               f"{ROOF_RAMP} untimed ones"},
+                     "timing": f"HIP events around {n_roof} back-to-back launches of the kernel after "
+                               f"{max(0, args.roofline_ramp)} untimed ones"},
         "cpu_baseline": cpu,
         "cpu_baseline_numpy": cpu_np,
         "cpu_baseline_numpy_threads": cpu_np_mt,

@@ -40,7 +40,8 @@ for s in $STEPS; do
                   python bench.py --steps 200 --warmup 100 --cpu-seconds 0 --no-parity; fatal $? ;;
         pmc) for c in FETCH_SIZE WRITE_SIZE; do
                  run "pmc_$c" 300 rocprofv3 --pmc "$c" --kernel-trace -d "$OUT/pmc_$c" -o run --output-format csv -- \
-                     python bench.py --steps 10 --warmup 2 --cpu-seconds 0 --no-parity; fatal $? || exit
+                     python bench.py --steps 10 --warmup 2 --cpu-seconds 0 --no-parity --roofline-launches 5 \
+                     --roofline-ramp 0; fatal $? || exit
              done ;;
         bench_*) wl=${s#bench_}
              run "bench_$wl" 300 python bench.py --workload "$wl" --cpu-seconds 5; fatal $? ;;
@@ -51,7 +52,7 @@ for s in $STEPS; do
              for c in FETCH_SIZE WRITE_SIZE; do
                  run "pmc_${wl}_$c" 300 rocprofv3 --pmc "$c" --kernel-trace -d "$OUT/pmc_${wl}_$c" -o run \
                      --output-format csv -- python bench.py --workload "$wl" --steps 10 --warmup 2 --cpu-seconds 0 \
-                     --no-parity; fatal $? || exit
+                     --no-parity --roofline-launches 5 --roofline-ramp 0; fatal $? || exit
              done ;;
         pytestsub) run pytest_sub 600 python -u -m pytest -x -q -p no:cacheprovider --timeout 120 \
                  --timeout-method thread ${PYTEST_FILES}; fatal $? ;;
@@ -69,6 +70,11 @@ for s in $STEPS; do
                  abrun/libfir_hip_oldnoasm.so abrun/libfir_hip_glds0.so abrun/libfir_hip_glds768.so abrun/libfir_hip_glds256.so; fatal $? ;;
         rowlat) run rowlat 300 python tools/row_call_latency.py "$OUT/row_call_latency.json"; fatal $? ;;
         ltr) run long_taps_rate 300 python tools/long_taps_rate.py 31,64,65,66,128,257,450,500,1000,2048,4099; fatal $? ;;
+        sq_*) wl=${s#sq_}
+             run "sq_$wl" 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+                 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU --kernel-trace \
+                 -d "$OUT/sq_$wl" -o run --output-format csv -- python bench.py --workload "$wl" --steps 10 \
+                 --warmup 2 --cpu-seconds 0 --no-parity --roofline-launches 5 --roofline-ramp 0; fatal $? ;;
         asan) run asan 600 make -C warmup-fir-filter_amd/csrc asan-check; fatal $? ;;
         micro) run micro 300 tools/microbench/fir_micro 28 20; fatal $? ;;
         micro2d) run micro2d 300 tools/microbench/fir2d_micro 15; fatal $? ;;
