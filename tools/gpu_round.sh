@@ -75,6 +75,12 @@ for s in $STEPS; do
                  SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU --kernel-trace \
                  -d "$OUT/sq_$wl" -o run --output-format csv -- python bench.py --workload "$wl" --steps 10 \
                  --warmup 2 --cpu-seconds 0 --no-parity --roofline-launches 5 --roofline-ramp 0; fatal $? ;;
+        dist2prof_serial|dist2prof_overlap) m=${s#dist2prof_}
+             run "dist2prof_$m" 300 tools/dist2_prof.sh "$OUT/dist2prof_$m" "$m"; fatal $? ;;
+        bankab) for v in u2 xcd persist u2xcd; do
+                 run "bankab_$v" 200 python tools/lib_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so \
+                     abrun/libfir_hip_bank_$v.so 10 bank; fatal $? || exit
+             done ;;
         asan) run asan 600 make -C warmup-fir-filter_amd/csrc asan-check; fatal $? ;;
         micro) run micro 300 tools/microbench/fir_micro 28 20; fatal $? ;;
         micro2d) run micro2d 300 tools/microbench/fir2d_micro 15; fatal $? ;;

@@ -28,6 +28,9 @@ namespace fir {
 #define FIR_REG_EDGE_DWORD 1
 #endif
 constexpr int kRegFlags = kCoal | kNtStore | (FIR_REG_EDGE_DWORD ? kEdgeDword : 0);
+#ifndef FIR_REG_BANK_FLAGS  // extra flags of fused banks (F > 1; A/B builds: kXcd = 8, kPersist = 4)
+#define FIR_REG_BANK_FLAGS 0
+#endif
 constexpr int kPersistBlocks = 2048;
 
 template <typename InT, int STAGE, int L, int CH, int F, int FL>
@@ -58,6 +61,13 @@ static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t
         }
     } else if (hl != nullptr || hr != nullptr) {
         return hipErrorInvalidValue;  // shards with halos are single-filter calls
+    }
+    if constexpr (F > 1 && FIR_REG_BANK_FLAGS != 0) {
+        constexpr int FB = FL | FIR_REG_BANK_FLAGS;
+        reg_launch_geometry<InT, kRegU<InT, F>, FB>(total, kPersistBlocks, &ntiles, &blocks);
+        hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, kRegU<InT, F>, FB, F>), dim3((unsigned)blocks), dim3(kBlock),
+                           0, stream, (const InT*)x, (OutT*)y, g, t, 32 - acc_bits, frac, ntiles);
+        return hipGetLastError();
     }
     hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, kRegU<InT, F>, FL, F>), dim3((unsigned)blocks), dim3(kBlock), 0,
                        stream, (const InT*)x, (OutT*)y, g, t, 32 - acc_bits, frac, ntiles);
