@@ -7,8 +7,9 @@ saturation) over 2^28 synthetic samples PER GPU (weak scaling: 2^31 samples on 8
 inputs resident in HBM before the timed region.  For N > 1 each rank owns one contiguous
 segment; a step is a one-wave gate kernel that hands the 2+2-sample halo over through the
 neighbours' HBM over xGMI, ordered per step (device atomics on mailboxes mapped once), then ONE
-launch of the FIR kernel reading it (FIR_HALO=rccl: RCCL send/recv every step, overlapped with
-the bulk kernel, then an edge kernel).
+launch of the FIR kernel reading it (FIR_GATE_MODE=overlap: the gate beside the bulk kernel, then
+an edge kernel; FIR_HALO=rccl: RCCL send/recv every step, overlapped with the bulk kernel, then an
+edge kernel).
 
 Contract: `python bench.py --gpus N --steps K --warmup W`; rank 0 prints ONE JSON line.  For
 N > 1 either launch it under torch.distributed.run (RANK/WORLD_SIZE set), or run it as is: the
@@ -77,9 +78,13 @@ SELF_HALO = os.environ.get("FIR_SELF_HALO") == "1"
 # N > 1 halo source: "xgmi" (default: neighbours' HBM mapped once, read by the edge kernel) or
 # "rccl" (send/recv every step); xgmi falls back to rccl on every rank if any rank cannot map.
 HALO_PREF = os.environ.get("FIR_HALO", "xgmi")
-# xGMI step ordering: "overlap" (the gate on a high-priority side stream while the bulk kernel runs,
-# then a 4-output edge kernel) or "serial" (the gate, then ONE segment launch reading its halos)
-GATE_MODE = os.environ.get("FIR_GATE_MODE", "overlap")
+# xGMI step ordering: "serial" (the gate, then ONE segment launch reading its halos; default) or
+# "overlap" (the gate on a high-priority side stream while the bulk kernel runs, then a 4-output edge
+# kernel).  Measured (profiles/r04): serial 253.5 us per step against 268.5 us for
+# overlap with the segment as its own neighbour, and 513 vs 608 us with 2 ranks sharing one GPU:
+# a gate running beside the bulk kernel is slowed by it (9 -> 35 us, up to 320 us while it polls a
+# neighbour) and the edge launch adds its own gap, so overlapping costs more than it hides.
+GATE_MODE = os.environ.get("FIR_GATE_MODE", "serial")
 KERNELS = {"fir1d_i16": "fir1d_reg_kernel", "cplx_i16": "fir1d_reg_kernel", "fir2d_u8": "fir2d_pk16_strip_kernel",
            "fir1d_u8": "fir1d_reg_kernel", "ideal_u8": "fir1d_ideal_kernel", "bank_u8": "fir1d_reg_kernel",
            "restore_u8": "restore_map_kernel", "metrics_u8": "metrics_blocks+chain"}
