@@ -51,10 +51,11 @@ extern "C" {
 
 #define FIR_HIP_ABI_VERSION 4
 /* Tap counts: any length up to FIR_MAX_TAPS (1-D taps; 2-D tap_rows * tap_cols), like the
- * reference's Python loop (fir_1d_fixed_ref.py:83-107, fir_1d_ref.py:49-63).  Sums are exact in
- * 64 bits: mod 2^64 for acc_bits < 64; with acc_bits >= 64 (no wrap) sum|hq| * max|x| must stay
- * below 2^63 (FIR_EINVAL otherwise; u8 samples with coeff_bits <= 32 always do). */
-#define FIR_MAX_TAPS (1 << 24)
+ * reference's Python loop (fir_1d_fixed_ref.py:83-107, fir_1d_ref.py:49-63); the bound is the
+ * int taps argument and device memory (4 B per tap), not the arithmetic.  Sums are exact as the
+ * reference's unbounded Python ints: mod 2^64 for acc_bits < 64, 64-bit while sum|hq| * max|x|
+ * < 2^63, 128-bit otherwise (ABI 4; < 2^127 for every legal input). */
+#define FIR_MAX_TAPS (1 << 30)
 
 typedef enum {
     FIR_OK = 0,

@@ -61,7 +61,7 @@ def test_errors_surface_as_firhiperror():
     with pytest.raises(fir_hip.FirHipError):
         fir_hip._taps_i32([])
     with pytest.raises(fir_hip.FirHipError):
-        fir_hip._taps_i32(np.ones(fir_hip.MAX_TAPS + 1, np.int64))
+        fir_hip._taps_i32(np.broadcast_to(np.int64(1), (fir_hip.MAX_TAPS + 1,)))  # refused before any copy
     assert fir_hip._taps_i32(np.ones(4099, np.int64)).size == 4099  # long filters are legal
 
 

@@ -140,14 +140,65 @@ def test_fir2d_many_taps_vs_oracle(R, C, shape):
         assert np.array_equal(got, co.fir2d(x, hq, 12, 32, stage)), stage
 
 
-def test_acc64_overflow_is_refused():
-    """acc_bits >= 64 promises the exact sum: refused when it could exceed 64 bits."""
-    x = np.zeros(16, np.int16)
-    hq = np.full((1 << 17) + 1000, (1 << 31) - 1, np.int64)
-    with pytest.raises(fir_hip.FirHipError, match="exceeds 64 bits"):
-        fir_hip.fir1d_fixed_rows(x, hq, 12, 64, fir_hip.OUT_I32)
-    # the same taps with a wrap to 64 - 1 bits are exact mod 2^64 and accepted
-    assert fir_hip.fir1d_fixed_rows(x, hq, 12, 63, fir_hip.OUT_I32).tolist() == [0] * 16
+def _exact_out(x, h, idx, frac, acc_bits, stage):
+    """The reference's arithmetic (fir_1d_fixed_ref.py:94-126, unbounded ints) at outputs idx:
+    chunked int64 partial sums (each < 2^57) added as Python ints, masked to acc_bits, sign
+    restored, rounded, staged (OUT_I32: the int32 the library stores, its low 32 bits)."""
+    x = np.asarray(x, np.int64)
+    h = np.asarray(h, np.int64)
+    c, out = h.size // 2, []
+    xp = np.concatenate([np.zeros(h.size, np.int64), x, np.zeros(h.size, np.int64)])
+    for n in idx:
+        # sum_k h[k] x[n - k + c]: window x[n + c - L + 1 .. n + c] reversed
+        w = xp[h.size + n + c - h.size + 1:h.size + n + c + 1][::-1]
+        acc = sum(int(np.dot(h[i:i + 1024], w[i:i + 1024])) for i in range(0, h.size, 1024))
+        acc &= (1 << acc_bits) - 1
+        if acc & (1 << (acc_bits - 1)):
+            acc -= 1 << acc_bits
+        v = (acc + (1 << (frac - 1))) >> frac
+        out.append(min(max(v, 0), 255) if stage == fo.OUT_U8_SAT else ((v + (1 << 31)) & 0xFFFFFFFF) - (1 << 31))
+    return out
+
+
+def test_acc64_wide_sums_are_exact():
+    """acc_bits >= 64 means the reference's unbounded sum (fir_1d_fixed_ref.py:94-115): past
+    2^63 the library sums in 128 bits.  int16 samples of the taps' alternating sign times
+    alternating taps of +-2^31 make every full-window sum about 2^63.1; checked against the
+    reference's arithmetic on Python ints; then a shard's edges and the 2-D generic kernel."""
+    rng = np.random.default_rng(64)
+    L = (1 << 17) + 1001
+    n = (1 << 17) + 2048
+    hq = np.full(L, (1 << 31) - 1, np.int64)
+    hq[1::2] = -(1 << 31)
+    x = np.where(np.arange(n) % 2 == 0, 32767, -32768).astype(np.int16)
+    x[rng.integers(0, n, 500)] = rng.integers(-32768, 32768, 500)
+    idx = list(range(0, 32)) + list(range(n // 2 - 32, n // 2 + 32)) + list(range(n - 32, n))
+    for frac, acc in ((12, 64), (12, 100), (40, 128), (70, 96), (12, 63)):
+        for stage in (fir_hip.OUT_U8_SAT, fir_hip.OUT_I32):
+            got = fir_hip.fir1d_fixed_rows(x, hq, frac, acc, stage)
+            want = _exact_out(x, hq, idx, frac, acc, stage)
+            assert [int(got[i]) for i in idx] == want, (frac, acc, stage)
+    # a shard's edge outputs through the same 128-bit sums (fir1d_fixed_edges_dev)
+    m = 4096
+    xs = x[:m].copy()
+    hl_n, hr_n = fo.halo_sizes(L)
+    hlv = x[m:m + hl_n].copy()
+    hrv = x[m + hl_n:m + hl_n + hr_n].copy()
+    y = torch_ops.fir1d_fixed_segment_dev(torch.from_numpy(xs).to(DEV), hq, torch.from_numpy(hlv).to(DEV),
+                                          torch.from_numpy(hrv).to(DEV), 12, 80, fir_hip.OUT_U8_SAT)
+    full = np.concatenate([hlv, xs, hrv])
+    eidx = list(range(0, 32)) + list(range(m - 32, m))
+    want = _exact_out(full, hq, [hl_n + i for i in eidx], 12, 80, fo.OUT_U8_SAT)
+    got = y.cpu().numpy()
+    assert [int(got[i]) for i in eidx] == want
+    # 2-D: 2^23 taps of near-2^31 on u8 pixels reach 2^62 * 255 > 2^63
+    img = np.full((3, 5), 255, np.uint8)
+    k2 = np.full((1 << 11, 1 << 12), (1 << 31) - 1, np.int64)
+    got2 = fir_hip.fir2d_fixed(img, k2, 12, 100, fir_hip.OUT_I32)
+    # every output sees the 3 x 5 frame (all 255) under taps of one value: sum = 15 * 255 * h
+    s = 15 * 255 * ((1 << 31) - 1)
+    q = ((s + (1 << 11)) >> 12) & 0xFFFFFFFF
+    assert (got2 == (q - (1 << 32) if q >= (1 << 31) else q)).all()
 
 
 def test_table_cache_evicts_only_idle_tables():

@@ -18,9 +18,11 @@
 //  * fir1d_generic_kernel — every other configuration (any tap count up to FIR_MAX_TAPS,
 //    any channel count, any acc_bits / frac_bits, unaligned buffers, narrow rows, halo
 //    segments): a workgroup owns 1024 outputs and walks the taps (read from HBM) in chunks,
-//    staging each chunk's taps and window in LDS; exact 64-bit sums.
+//    staging each chunk's taps and window in LDS; exact 64-bit sums (128-bit when a no-wrap
+//    call's sum could reach 2^63).
 #include <algorithm>
 #include <string>
+#include <type_traits>
 
 #include "fir1d_reg_launch.h"
 #include "fir_common.h"
@@ -68,7 +70,9 @@ __device__ __forceinline__ int32_t seg_sample(const InT* __restrict__ x, int64_t
     return halo_r && gi < total + hre ? (int32_t)halo_r[gi - total] : 0;
 }
 
-template <typename InT, int STAGE>
+// WIDE: 128-bit sums (a no-wrap call whose sum may exceed 2^63: int16 samples with huge taps, or
+// more taps than 2^24), else 64-bit ones.
+template <typename InT, int STAGE, bool WIDE>
 __global__ __launch_bounds__(kBlock) void fir1d_generic_kernel(const InT* __restrict__ x,
                                                                typename OutTraits<STAGE>::T* __restrict__ y,
                                                                int64_t start, int64_t end, int64_t total,
@@ -82,7 +86,9 @@ __global__ __launch_bounds__(kBlock) void fir1d_generic_kernel(const InT* __rest
     const int c = L / 2;
     const int64_t HLE = (int64_t)(L - 1 - c) * ch, HRE = (int64_t)c * ch;
     const int64_t t0 = start + (int64_t)blockIdx.x * kGenTile;
-    uint64_t acc[kGenPer] = {};
+    using Acc = typename std::conditional<WIDE, unsigned __int128, uint64_t>::type;
+    using SAcc = typename std::conditional<WIDE, __int128, int64_t>::type;
+    Acc acc[kGenPer] = {};
     int64_t col[kGenPer];
 #pragma unroll
     for (int j = 0; j < kGenPer; ++j) col[j] = multi_row ? (t0 + threadIdx.x + j * kBlock) % rowlen : 0;
@@ -106,21 +112,26 @@ __global__ __launch_bounds__(kBlock) void fir1d_generic_kernel(const InT* __rest
                     const int64_t d = (int64_t)(c - k0 - k) * ch;
                     if (col[j] + d < 0 || col[j] + d >= rowlen) xv = 0;
                 }
-                acc[j] += (uint64_t)((int64_t)s_taps[k] * xv);
+                acc[j] += (Acc)(SAcc)((int64_t)s_taps[k] * xv);
             }
         }
     }
 #pragma unroll
     for (int j = 0; j < kGenPer; ++j) {
         const int64_t gi = t0 + threadIdx.x + j * kBlock;
-        if (gi < end) y[gi] = stage_out<STAGE>(round64((int64_t)acc[j], frac, acc_bits));
+        if (gi < end) {
+            if constexpr (WIDE)
+                y[gi] = stage_out128<STAGE>(round128((__int128)acc[j], frac, acc_bits));
+            else
+                y[gi] = stage_out<STAGE>(round64((int64_t)acc[j], frac, acc_bits));
+        }
     }
 }
 
 // Both edges of a single-row segment in one launch (multi-GPU step): output j < hle is the
 // left edge, j >= hle maps to the right edge total - hre + (j - hle).  Samples left of the
 // segment come from halo_l, right of it from halo_r (zeros when NULL).  Exact 64-bit sums.
-template <typename InT, int STAGE>
+template <typename InT, int STAGE, bool WIDE>
 __global__ __launch_bounds__(kBlock) void fir1d_edges_kernel(const InT* __restrict__ x,
                                                              typename OutTraits<STAGE>::T* __restrict__ y,
                                                              int64_t total, int64_t ch, const InT* __restrict__ halo_l,
@@ -130,15 +141,31 @@ __global__ __launch_bounds__(kBlock) void fir1d_edges_kernel(const InT* __restri
     const int c = L / 2;
     for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < hle + hre; j += (int64_t)gridDim.x * kBlock) {
         const int64_t gi = j < hle ? j : total - hre + (j - hle);
-        uint64_t acc = 0;
+        using Acc = typename std::conditional<WIDE, unsigned __int128, uint64_t>::type;
+        using SAcc = typename std::conditional<WIDE, __int128, int64_t>::type;
+        Acc acc = 0;
         for (int k = 0; k < L; ++k)
-            acc += (uint64_t)((int64_t)taps[k] * seg_sample(x, gi + (int64_t)(c - k) * ch, total, halo_l, hle, halo_r, hre));
-        y[gi] = stage_out<STAGE>(round64((int64_t)acc, frac, acc_bits));
+            acc += (Acc)(SAcc)((int64_t)taps[k] * seg_sample(x, gi + (int64_t)(c - k) * ch, total, halo_l, hle, halo_r, hre));
+        if constexpr (WIDE)
+            y[gi] = stage_out128<STAGE>(round128((__int128)acc, frac, acc_bits));
+        else
+            y[gi] = stage_out<STAGE>(round64((int64_t)acc, frac, acc_bits));
     }
 }
 
 // ---------------------------------------------------------------------------------------
 // Host-side launchers.
+
+// A no-wrap call (acc_bits >= 64) whose exact sum could reach 2^63: the 128-bit generic kernels
+// (the reference's sum is an unbounded Python int, fir_1d_fixed_ref.py:94-115).  A wrap to
+// acc_bits < 64 is exact mod 2^64, and |sum| < 2^63 is exact in 64 bits.
+static bool needs_wide(int in_dtype, const int32_t* hq, int L, int acc_bits) {
+    if (acc_bits < 64) return false;
+    unsigned __int128 habs = 0;
+    for (int k = 0; k < L; ++k) habs += (unsigned __int128)(hq[k] < 0 ? -(int64_t)hq[k] : (int64_t)hq[k]);
+    const unsigned __int128 xmax = in_dtype == FIR_IN_U8 ? 255 : 32768;
+    return habs * xmax >= ((unsigned __int128)1 << 63);
+}
 
 template <typename InT, int STAGE>
 static hipError_t launch_generic(const void* x, void* y, int64_t start, int64_t end, int64_t total,
@@ -152,9 +179,14 @@ static hipError_t launch_generic(const void* x, void* y, int64_t start, int64_t 
     TableHold hold(td, stream);
     const int64_t blocks = (end - start + kGenTile - 1) / kGenTile;
     if (blocks >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((fir1d_generic_kernel<InT, STAGE>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
-                       (const InT*)x, (OutT*)y, start, end, total, rowlen, multi_row ? 1 : 0, (int64_t)ch,
-                       (const InT*)hl, (const InT*)hr, td, L, gen_tap_chunk(L, ch), frac, acc_bits);
+    if (needs_wide(sizeof(InT) == 1 ? FIR_IN_U8 : FIR_IN_I16, hq, L, acc_bits))
+        hipLaunchKernelGGL((fir1d_generic_kernel<InT, STAGE, true>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
+                           (const InT*)x, (OutT*)y, start, end, total, rowlen, multi_row ? 1 : 0, (int64_t)ch,
+                           (const InT*)hl, (const InT*)hr, td, L, gen_tap_chunk(L, ch), frac, acc_bits);
+    else
+        hipLaunchKernelGGL((fir1d_generic_kernel<InT, STAGE, false>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
+                           (const InT*)x, (OutT*)y, start, end, total, rowlen, multi_row ? 1 : 0, (int64_t)ch,
+                           (const InT*)hl, (const InT*)hr, td, L, gen_tap_chunk(L, ch), frac, acc_bits);
     return hipGetLastError();
 }
 
@@ -178,12 +210,17 @@ static hipError_t dispatch_generic(int in_dtype, int stage, const void* x, void*
 
 template <typename InT, int STAGE>
 static hipError_t launch_edges(const void* x, void* y, int64_t total, int ch, const void* hl, const void* hr,
-                               const int32_t* td, int L, int64_t hle, int64_t hre, int frac, int acc_bits,
+                               const int32_t* td, int L, int64_t hle, int64_t hre, int frac, int acc_bits, bool wide,
                                hipStream_t stream) {
     const int64_t blocks = std::min<int64_t>((hle + hre + kBlock - 1) / kBlock, 1024);
-    hipLaunchKernelGGL((fir1d_edges_kernel<InT, STAGE>), dim3((unsigned)blocks), dim3(kBlock), 0, stream, (const InT*)x,
-                       (typename OutTraits<STAGE>::T*)y, total, (int64_t)ch, (const InT*)hl, (const InT*)hr, td, L,
-                       hle, hre, frac, acc_bits);
+    if (wide)
+        hipLaunchKernelGGL((fir1d_edges_kernel<InT, STAGE, true>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
+                           (const InT*)x, (typename OutTraits<STAGE>::T*)y, total, (int64_t)ch, (const InT*)hl,
+                           (const InT*)hr, td, L, hle, hre, frac, acc_bits);
+    else
+        hipLaunchKernelGGL((fir1d_edges_kernel<InT, STAGE, false>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
+                           (const InT*)x, (typename OutTraits<STAGE>::T*)y, total, (int64_t)ch, (const InT*)hl,
+                           (const InT*)hr, td, L, hle, hre, frac, acc_bits);
     return hipGetLastError();
 }
 
@@ -196,13 +233,6 @@ static int check_common(int in_dtype, int64_t rows, int64_t width, int ch, const
     if (!hq) return *err = "hq must not be NULL", FIR_EINVAL;
     if (L < 1 || L > FIR_MAX_TAPS) return *err = "taps must be in [1, " + std::to_string(FIR_MAX_TAPS) + "]", FIR_EINVAL;
     if (frac < 1 || acc_bits < 1) return *err = "frac_bits and acc_bits must be >= 1", FIR_EINVAL;
-    if (acc_bits >= 64) {  // no wrap: the 64-bit sum must be the exact one
-        int64_t habs = 0;
-        for (int k = 0; k < L; ++k) habs += hq[k] < 0 ? -(int64_t)hq[k] : hq[k];
-        const int64_t xmax = in_dtype == FIR_IN_U8 ? 255 : 32768;
-        if (habs > (INT64_MAX - 1) / xmax)
-            return *err = "acc_bits >= 64 with sum|hq| * max|x| >= 2^63: the sum exceeds 64 bits", FIR_EINVAL;
-    }
     return FIR_OK;
 }
 
@@ -351,14 +381,15 @@ int launch_fir1d_edges(const void* x, int in_dtype, int64_t n, int ch, const int
         const int32_t* td = (const int32_t*)device_table(hq, sizeof(int32_t) * (size_t)L, err);
         if (!td) return FIR_ENOMEM;
         TableHold hold(td, stream);
+        const bool wide = needs_wide(in_dtype, hq, L, acc_bits);
         if (in_dtype == FIR_IN_U8)
             e = stage == FIR_OUT_U8_SAT
-                    ? launch_edges<uint8_t, FIR_OUT_U8_SAT>(x, y, total, ch, hl, hr, td, L, hle, hre, frac, acc_bits, stream)
-                    : launch_edges<uint8_t, FIR_OUT_I32>(x, y, total, ch, hl, hr, td, L, hle, hre, frac, acc_bits, stream);
+                    ? launch_edges<uint8_t, FIR_OUT_U8_SAT>(x, y, total, ch, hl, hr, td, L, hle, hre, frac, acc_bits, wide, stream)
+                    : launch_edges<uint8_t, FIR_OUT_I32>(x, y, total, ch, hl, hr, td, L, hle, hre, frac, acc_bits, wide, stream);
         else
             e = stage == FIR_OUT_U8_SAT
-                    ? launch_edges<int16_t, FIR_OUT_U8_SAT>(x, y, total, ch, hl, hr, td, L, hle, hre, frac, acc_bits, stream)
-                    : launch_edges<int16_t, FIR_OUT_I32>(x, y, total, ch, hl, hr, td, L, hle, hre, frac, acc_bits, stream);
+                    ? launch_edges<int16_t, FIR_OUT_U8_SAT>(x, y, total, ch, hl, hr, td, L, hle, hre, frac, acc_bits, wide, stream)
+                    : launch_edges<int16_t, FIR_OUT_I32>(x, y, total, ch, hl, hr, td, L, hle, hre, frac, acc_bits, wide, stream);
     }
     if (e != hipSuccess) return *err = std::string("fir1d edge launch failed: ") + hipGetErrorString(e), FIR_EHIP;
     return FIR_OK;

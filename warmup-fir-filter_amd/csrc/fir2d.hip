@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 
 #include "fir2d_pk16.h"
 #include "fir2d_reg.h"
@@ -93,7 +94,7 @@ constexpr int pd_pk_gen() { return FIR2D_PKG_PD ? FIR2D_PKG_PD : (R * C >= 20 ? 
 
 // Generic: one output per thread, exact 64-bit sum (mod 2^64, see round64), global loads (L1/L2
 // absorb the reuse), taps of any count from HBM; rows grid-strided (any height).
-template <int STAGE>
+template <int STAGE, bool WIDE>  // WIDE: 128-bit sums (a no-wrap call whose sum could reach 2^63)
 __global__ __launch_bounds__(kBlock) void fir2d_generic_kernel(const uint8_t* __restrict__ x,
                                                                typename OutTraits<STAGE>::T* __restrict__ y,
                                                                int64_t H, int64_t W, const int32_t* __restrict__ taps,
@@ -104,17 +105,22 @@ __global__ __launch_bounds__(kBlock) void fir2d_generic_kernel(const uint8_t* __
     y += (int64_t)blockIdx.z * H * W;
     const int cr = R / 2, cc = C / 2;
     for (int64_t i = blockIdx.y; i < H; i += gridDim.y) {
-        uint64_t acc = 0;
+        using Acc = typename std::conditional<WIDE, unsigned __int128, uint64_t>::type;
+        using SAcc = typename std::conditional<WIDE, __int128, int64_t>::type;
+        Acc acc = 0;
         for (int m = 0; m < R; ++m) {
             const int64_t ii = i - m + cr;
             if (ii < 0 || ii >= H) continue;
             for (int n = 0; n < C; ++n) {
                 const int64_t jj = j - n + cc;
                 if (jj < 0 || jj >= W) continue;
-                acc += (uint64_t)((int64_t)taps[(int64_t)m * C + n] * (int64_t)x[ii * W + jj]);
+                acc += (Acc)(SAcc)((int64_t)taps[(int64_t)m * C + n] * (int64_t)x[ii * W + jj]);
             }
         }
-        y[i * W + j] = stage_out<STAGE>(round64((int64_t)acc, frac, acc_bits));
+        if constexpr (WIDE)
+            y[i * W + j] = stage_out128<STAGE>(round128((__int128)acc, frac, acc_bits));
+        else
+            y[i * W + j] = stage_out<STAGE>(round64((int64_t)acc, frac, acc_bits));
     }
 }
 
@@ -298,11 +304,11 @@ int launch_fir2d(const uint8_t* x, int64_t frames, int64_t H, int64_t W, const i
         return *err = "tap_rows*tap_cols must be in [1, " + std::to_string(FIR_MAX_TAPS) + "]", FIR_EINVAL;
     if (frac < 1 || acc_bits < 1) return *err = "frac_bits and acc_bits must be >= 1", FIR_EINVAL;
     const int64_t ntaps = (int64_t)R * C;
-    if (acc_bits >= 64) {  // no wrap: the 64-bit sum must be the exact one
-        int64_t habs = 0;
-        for (int64_t k = 0; k < ntaps; ++k) habs += hq[k] < 0 ? -(int64_t)hq[k] : hq[k];
-        if (habs > (INT64_MAX - 1) / 255)
-            return *err = "acc_bits >= 64 with sum|hq| * 255 >= 2^63: the sum exceeds 64 bits", FIR_EINVAL;
+    bool wide = false;  // a no-wrap call whose exact sum could reach 2^63: 128-bit sums
+    if (acc_bits >= 64) {
+        unsigned __int128 habs = 0;
+        for (int64_t k = 0; k < ntaps; ++k) habs += (unsigned __int128)(hq[k] < 0 ? -(int64_t)hq[k] : (int64_t)hq[k]);
+        wide = habs * 255 >= ((unsigned __int128)1 << 63);
     }
     if (H == 0 || W == 0 || frames == 0) return FIR_OK;
     if (!x || !y) return *err = "x and y must not be NULL", FIR_EINVAL;
@@ -332,12 +338,18 @@ int launch_fir2d(const uint8_t* x, int64_t frames, int64_t H, int64_t W, const i
         if (!td) return FIR_ENOMEM;
         TableHold hold(td, stream);
         dim3 grid((unsigned)((W + kBlock - 1) / kBlock), (unsigned)std::min<int64_t>(H, 65535), (unsigned)frames);
-        if (stage == FIR_OUT_U8_SAT)
-            hipLaunchKernelGGL((fir2d_generic_kernel<FIR_OUT_U8_SAT>), grid, dim3(kBlock), 0, stream, x, (uint8_t*)y, H,
-                               W, td, R, C, frac, acc_bits);
+        if (stage == FIR_OUT_U8_SAT && wide)
+            hipLaunchKernelGGL((fir2d_generic_kernel<FIR_OUT_U8_SAT, true>), grid, dim3(kBlock), 0, stream, x, (uint8_t*)y,
+                               H, W, td, R, C, frac, acc_bits);
+        else if (stage == FIR_OUT_U8_SAT)
+            hipLaunchKernelGGL((fir2d_generic_kernel<FIR_OUT_U8_SAT, false>), grid, dim3(kBlock), 0, stream, x, (uint8_t*)y,
+                               H, W, td, R, C, frac, acc_bits);
+        else if (wide)
+            hipLaunchKernelGGL((fir2d_generic_kernel<FIR_OUT_I32, true>), grid, dim3(kBlock), 0, stream, x, (int32_t*)y,
+                               H, W, td, R, C, frac, acc_bits);
         else
-            hipLaunchKernelGGL((fir2d_generic_kernel<FIR_OUT_I32>), grid, dim3(kBlock), 0, stream, x, (int32_t*)y, H,
-                               W, td, R, C, frac, acc_bits);
+            hipLaunchKernelGGL((fir2d_generic_kernel<FIR_OUT_I32, false>), grid, dim3(kBlock), 0, stream, x, (int32_t*)y,
+                               H, W, td, R, C, frac, acc_bits);
         e = hipGetLastError();
     }
     if (e != hipSuccess) return *err = std::string("fir2d launch failed: ") + hipGetErrorString(e), FIR_EHIP;

@@ -77,12 +77,34 @@ __device__ __forceinline__ int64_t round64(int64_t acc, int frac, int acc_bits) 
     return (acc >> frac) + ((acc >> (frac - 1)) & 1);
 }
 
+// 128-bit form for sums that may exceed 2^63 (no-wrap calls with huge taps x samples): `acc` is
+// the exact sum (|sum| < 2^127 for every legal input: FIR_MAX_TAPS x 2^31 x 2^15), wrapped to
+// acc_bits < 128 like the reference's mask-and-sign-restore, then rounded.
+__device__ __forceinline__ __int128 round128(__int128 acc, int frac, int acc_bits) {
+    if (acc_bits < 128) {
+        const int s = 128 - acc_bits;
+        acc = (__int128)((unsigned __int128)acc << s) >> s;
+    }
+    if (frac >= 128) return 0;
+    return (acc >> frac) + ((acc >> (frac - 1)) & 1);
+}
+
 template <int STAGE>
 __device__ __forceinline__ typename OutTraits<STAGE>::T stage_out(int64_t q) {
     if constexpr (STAGE == FIR_OUT_U8_SAT) {
         return (uint8_t)(q < 0 ? 0 : (q > 255 ? 255 : q));
     } else {
         return (int32_t)q;
+    }
+}
+
+// the stage of a 128-bit result: u8 saturation, or the low 32 bits (as stage_out's int32 cast)
+template <int STAGE>
+__device__ __forceinline__ typename OutTraits<STAGE>::T stage_out128(__int128 q) {
+    if constexpr (STAGE == FIR_OUT_U8_SAT) {
+        return (uint8_t)(q < 0 ? 0 : (q > 255 ? 255 : (int)q));
+    } else {
+        return (int32_t)(uint32_t)(unsigned __int128)q;
     }
 }
 

@@ -68,10 +68,10 @@ def quantize_fixed_taps(h, frac_bits: int = 12, acc_bits: int = 32, coeff_bits: 
 
 
 def device_bits(frac_bits: int, acc_bits: int) -> tuple[int, int]:
-    """Clamp the bit widths to what changes the result (u8 samples: the exact sum |acc| < 2^63
-    for any tap count up to FIR_MAX_TAPS): acc_bits >= 64 never wraps, frac_bits >= 64 always
-    rounds to 0."""
-    return min(int(frac_bits), 64), min(int(acc_bits), 64)
+    """Clamp the bit widths to what changes the result (the exact sum |acc| < 2^127 for any tap
+    count up to FIR_MAX_TAPS): acc_bits >= 128 never wraps, frac_bits >= 128 always rounds to 0;
+    the library sums in 64 bits while that is exact and in 128 bits otherwise."""
+    return min(int(frac_bits), 128), min(int(acc_bits), 128)
 
 
 def fir_1d_fixed_golden(

@@ -31,7 +31,7 @@ __all__ = [
 IN_U8, IN_I16 = 0, 1
 OUT_U8_SAT, OUT_I32 = 0, 1
 RESTORE_CLIP, RESTORE_NORMALIZE = 0, 1
-MAX_TAPS = 1 << 24  # FIR_MAX_TAPS: any practical length (the reference has no limit)
+MAX_TAPS = 1 << 30  # FIR_MAX_TAPS: any practical length (the reference has no limit)
 IPC_HANDLE_BYTES = 64
 ABI_VERSION = 4
 GATE_TIMEOUT = 1  # FIR_GATE_TIMEOUT
@@ -142,11 +142,12 @@ def _ptr(a: np.ndarray):
 
 
 def _taps_i32(hq) -> np.ndarray:
-    h = np.ascontiguousarray(np.asarray(hq, dtype=np.int64))
+    h = np.asarray(hq)
     if h.ndim != 1 or h.size == 0:
         raise FirHipError("hq must be a non-empty 1-D array")
-    if h.size > MAX_TAPS:
+    if h.size > MAX_TAPS:  # before any copy
         raise FirHipError(f"{h.size} taps exceed the library limit of {MAX_TAPS}")
+    h = np.ascontiguousarray(h, dtype=np.int64)
     if h.min() < -(1 << 31) or h.max() >= (1 << 31):
         raise FirHipError("quantized taps must fit in int32")
     return h.astype(np.int32)
