@@ -898,20 +898,26 @@ static hipError_t launch_mfma_long(const void* x, void* y, int64_t rl, int64_t t
 // no VGPRs held.  The bytes land unsigned; the B fragment is XORed with 0x80 after its LDS read
 // (xs = x - 128, as in every other kernel here).  The left halo P is rounded to 16 so a window
 // vector never straddles a row start.
-#ifndef FIR_MR_BLOCKS                // grid-stride blocks (4 waves, one per SIMD)
-#define FIR_MR_BLOCKS 256
-#endif
 #ifndef FIR_MR_TPS                   // tiles per run
-#define FIR_MR_TPS 4
+#define FIR_MR_TPS 2
 #endif
 #ifndef FIR_MR_C                     // k-steps per chunk
 #define FIR_MR_C 16
 #endif
-constexpr int kMrTps = FIR_MR_TPS, kMrC = FIR_MR_C;
+#ifndef FIR_MR_WAVES                 // waves per SIMD the registers must allow (LDS: (DEPTH+1) TPS 2 KiB per wave)
+#define FIR_MR_WAVES 2
+#endif
+#ifndef FIR_MR_DEPTH                 // iterations whose windows are in flight ahead of the one computed
+#define FIR_MR_DEPTH 2
+#endif
+#ifndef FIR_MR_BLOCKS                // grid-stride blocks (4 waves each): one resident round
+#define FIR_MR_BLOCKS (256 * FIR_MR_WAVES)
+#endif
+constexpr int kMrTps = FIR_MR_TPS, kMrC = FIR_MR_C, kMrDepth = FIR_MR_DEPTH;
 constexpr int kMrTileLds = 2048;     // LDS bytes per tile window (128 vectors of 16 samples)
 
 template <int STAGE, bool ACC32, bool FAST, bool MULTI>
-__global__ __launch_bounds__(kBlock, 1) void fir1d_mfma_run_kernel(const uint8_t* __restrict__ x,
+__global__ __launch_bounds__(kBlock, FIR_MR_WAVES) void fir1d_mfma_run_kernel(const uint8_t* __restrict__ x,
                                                                    typename OutTraits<STAGE>::T* __restrict__ y,
                                                                    int64_t rowlen, uint32_t tiles_per_row, uint32_t ntiles,
                                                                    const mf_i32x4* __restrict__ frag, int KS, int P,
@@ -923,13 +929,14 @@ __global__ __launch_bounds__(kBlock, 1) void fir1d_mfma_run_kernel(const uint8_t
     static_assert(NVT > kWave && NVT <= 2 * kWave && 16 * 2 * kWave <= kMrTileLds, "two DMAs per tile window");
     constexpr bool OLDS = STAGE == FIR_OUT_I32;
     constexpr int BUF = TPS * kMrTileLds;
+    constexpr int NBUF = kMrDepth + 1;          // LDS window buffers per wave (a ring)
     constexpr int NDMA = 2 * TPS;               // DMA instructions per iteration
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kMfWaves][2 * BUF + (OLDS ? 4608 : 16)];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kMfWaves][NBUF * BUF + (OLDS ? 4608 : 16)];
 
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r = lane & 31, hf = lane >> 5;
-    uint32_t* ob = reinterpret_cast<uint32_t*>(lds[wv] + 2 * BUF);
+    uint32_t* ob = reinterpret_cast<uint32_t*>(lds[wv] + NBUF * BUF);
     const int32_t sat_hi = FAST ? (int32_t)((256u << (frac & 31)) - 1u) : 0;
     const int nch = (KS + C - 1) / C;
     const uint32_t nruns = (ntiles + TPS - 1) / TPS;
@@ -969,18 +976,26 @@ __global__ __launch_bounds__(kBlock, 1) void fir1d_mfma_run_kernel(const uint8_t
 #pragma unroll
     for (int q = 0; q < TPS; ++q) acc_ll[q] = mf_i32x16{}, acc_mid[q] = mf_i32x16{};
     if constexpr (!MULTI) load_a(0);  // KS <= C: one chunk, fragments loaded once
+    // iterations (run, chunk) in order; `ahead` is the one whose windows are issued next, kMrDepth
+    // ahead of the one computed (past the last: runs past nruns, whose zero-size descriptors move
+    // nothing -- every iteration issues the same NDMA operations, so the counted wait is exact)
+    auto advance = [&](uint32_t& r, int& ch) __attribute__((always_inline)) {
+        if (++ch == nch) ch = 0, r += stride;
+    };
     int c = 0, buf = 0;
-    issue_win(rn, 0, 0);
+    uint32_t ar = rn;
+    int ac = 0;
+#pragma unroll
+    for (int d = 0; d < kMrDepth; ++d) {
+        issue_win(ar, ac, d);
+        advance(ar, ac);
+    }
     for (;;) {
-        // the next iteration: the next chunk of this run, or chunk 0 of the next run (past the
-        // last: a run past nruns, whose zero-size descriptors move nothing -- every path issues the
-        // same NDMA operations, so the counted wait below is exact)
-        int nc = c + 1;
-        uint32_t nr = rn;
-        if (nc == nch) nc = 0, nr = rn + stride;
         if constexpr (MULTI) load_a(c);  // issued before the next windows: its wait leaves them in flight
-        issue_win(nr, nc, buf ^ 1);
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");  // this iteration's windows (and A) landed
+        issue_win(ar, ac, buf == 0 ? NBUF - 1 : buf - 1);  // the buffer computed last iteration
+        advance(ar, ac);
+        // this iteration's windows (and A) landed; the kMrDepth younger iterations stay in flight
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kMrDepth * NDMA) : "memory");
         __builtin_amdgcn_wave_barrier();
         const uint8_t* pl = lds[wv] + buf * BUF;
         const int steps = min(C, KS - C * c);
@@ -1049,11 +1064,15 @@ __global__ __launch_bounds__(kBlock, 1) void fir1d_mfma_run_kernel(const uint8_t
                 }
             }
         }
+        uint32_t nr = rn;
+        int nc = c;
+        advance(nr, nc);
         if (nr >= nruns) break;
-        rn = nr, c = nc, buf ^= 1;
+        rn = nr, c = nc, buf = buf + 1 == NBUF ? 0 : buf + 1;
         __builtin_amdgcn_wave_barrier();  // this iteration's B reads are done before its buffer is refilled
         asm volatile("" ::: "memory");
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMAs past the end land before the wave exits
 }
 
 template <int STAGE>

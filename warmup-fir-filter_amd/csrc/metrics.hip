@@ -38,8 +38,8 @@ namespace fir {
 #define FIR_METRIC_BLOCKS 512  // of an 8192-block part; 2^28: 453 -> 430 us vs 2048, 4096 slower)
 #endif
 constexpr int kMetricBlocks = FIR_METRIC_BLOCKS;
-#ifndef FIR_METRIC_GLDS  // 1: the LDS-DMA double-buffered block pass (metrics_blocks_glds)
-#define FIR_METRIC_GLDS 1
+#ifndef FIR_METRIC_GLDS  // 1: the LDS-DMA double-buffered block pass (metrics_blocks_glds; A/B:
+#define FIR_METRIC_GLDS 0   // 446.6 vs 429.9 us for the register-staged pass, profiles/r04/metrics_glds_ab.txt)
 #endif
 constexpr bool kMetricGlds = FIR_METRIC_GLDS;
 #ifndef FIR_METRIC_MINB  // waves per SIMD the block kernel's registers must allow
