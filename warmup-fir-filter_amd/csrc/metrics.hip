@@ -42,6 +42,10 @@ constexpr int kMetricBlocks = FIR_METRIC_BLOCKS;
 #define FIR_METRIC_GLDS 0   // 446.6 vs 429.9 us for the register-staged pass, profiles/r04/metrics_glds_ab.txt)
 #endif
 constexpr bool kMetricGlds = FIR_METRIC_GLDS;
+#ifndef FIR_METRIC_LEAF  // 1: one lane per leaf (metrics_leaf_kernel)
+#define FIR_METRIC_LEAF 1
+#endif
+constexpr bool kMetricLeaf = FIR_METRIC_LEAF;
 #ifndef FIR_METRIC_MINB  // waves per SIMD the block kernel's registers must allow
 #define FIR_METRIC_MINB 4
 #endif
@@ -415,6 +419,143 @@ __global__ __launch_bounds__(kBlock, 2) void metrics_blocks_glds(const double* _
     block_counts(Cnt{mx, lo, hi, clip}, parts + wg);
 }
 
+// The block pass with one LANE per leaf (round 4): lane l owns leaf l (samples 128 l .. 128 l +
+// 127) of the wave's block and keeps all 8 of its accumulators r[0..7] in registers, so the leaf
+// combine ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) is 7 adds per 128 samples and only the block tree
+// over the 64 leaves crosses lanes (6 DPP / permlane levels per 8192 samples) -- against one
+// lane per accumulator above, whose 6-level tree ran every 1024 samples.  A round q (0..7) is the
+// 16-sample band [16 q, 16 q + 16) of every leaf: loaded as 8 coalesced 1 KiB instructions (8
+// lanes per leaf's 128-byte band row), staged in the wave's LDS as [leaf][16 doubles] rows of
+// 144 bytes (conflict-free ds_read_b128 of a lane's own row), the next round's band loaded into
+// registers while this one is reduced.  The block's 8 KiB of fixed bytes arrive with its first
+// band (coalesced, staged as [leaf][128 bytes] rows).  Counts without per-sample VALU adds: zeros
+// and 255s of four fixed bytes at once (byte tricks + v_bcnt), the ideal range test as two
+// compares whose lane masks are counted on the SALU.
+constexpr int kLfRow = 144;                       // LDS bytes per leaf row (128 + 16: conflict-free b128)
+constexpr int kLfWaveLds = 2 * kWave * kLfRow;    // ideal band + the block's fixed bytes
+static_assert(kBlock / kWave * kLfWaveLds >= kChainLds, "the chain's staging shares the wave buffers");
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mt_rsrc(const void* p, uint32_t bytes) {
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0, (int)bytes, 0x00020000);
+}
+__global__ __launch_bounds__(kBlock, 2) void metrics_leaf_kernel(const double* __restrict__ ideal,
+                                                                const uint8_t* __restrict__ fixed,
+                                                                double* __restrict__ bsum, int64_t nb, int64_t b_lo,
+                                                                int64_t b_hi, int64_t c_lo, int64_t c_hi,
+                                                                double* __restrict__ state, Cnt* __restrict__ parts) {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    typedef int i4 __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock / kWave * kLfWaveLds];
+    const bool chain = c_hi > c_lo;
+    if (chain && blockIdx.x == 0) {
+        chain_range(bsum, nb, c_lo, c_hi, state, smem);
+        return;
+    }
+    const int wg = blockIdx.x - (chain ? 1 : 0);
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x >> 6;
+    uint8_t* wl = smem + wv * kLfWaveLds;
+    uint8_t* fl = wl + kWave * kLfRow;  // fixed rows
+    const int64_t nwaves = (int64_t)(gridDim.x - (chain ? 1 : 0)) * (kBlock / kWave);
+    const int64_t b0 = b_lo + (int64_t)wg * (kBlock / kWave) + wv;
+    const int64_t nrounds = b0 < b_hi ? ((b_hi - 1 - b0) / nwaves + 1) * 8 : 0;
+    double mx = 0.0;
+    uint32_t nz_acc = 0, ff_acc = 0, ndw = 0;  // v_bcnt sums (28 + count per dword) and dwords seen
+    uint64_t clip = 0;                          // wave-uniform (SALU)
+    // band q of a block: load i, lane p -> leaf 8 i + p / 8, doubles 2 (p % 8) .. of its band row:
+    // byte offset 1024 (8 i + p / 8) + 128 q + 16 (p % 8) from the block (soffset: the uniform part)
+    const uint32_t voff = 1024u * (uint32_t)(lane >> 3) + 16u * (uint32_t)(lane & 7);
+    const int lrow = lane >> 3, lcol = lane & 7;
+    d2 nx[8];
+    u4 fx[8];
+    auto load_band = [&](int64_t t, bool with_fixed) __attribute__((always_inline)) {
+        const int64_t blk = b0 + (t >> 3) * nwaves;
+        const __amdgpu_buffer_rsrc_t ri = mt_rsrc(ideal + blk * kPwBlock, kPwBlock * 8);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const i4 v = __builtin_amdgcn_raw_buffer_load_b128(ri, voff, 8192 * i + 128 * (int)(t & 7), 2);
+            nx[i] = __builtin_bit_cast(d2, v);
+        }
+        if (with_fixed) {
+            const __amdgpu_buffer_rsrc_t rf = mt_rsrc(fixed + blk * kPwBlock, kPwBlock);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) fx[i] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rf, 16u * lane, 1024 * i, 0));
+        }
+    };
+    if (nrounds) load_band(0, true);
+    Term r[8];
+    // one band of this lane's leaf: 16 terms into r[s % 8] (FIRST: the leaf's first band, whose
+    // first 8 terms start the accumulators, as pairwise_sum's r[j] = a[j])
+    auto band = [&](auto first, const double (&idv)[16], const uint32_t (&fw)[4]) __attribute__((always_inline)) {
+        constexpr bool FIRST = decltype(first)::value;
+        uint32_t clip_band = 0;  // <= 1024 per band: 32-bit SALU adds, one 64-bit add per band
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            const double id = idv[s];
+            const uint32_t f = (fw[s / 4] >> (8 * (s % 4))) & 0xFFu;
+            const double d = __dsub_rn((double)f, id);
+            const double ad = fabs(d);
+            mx = fmax(mx, ad);
+            // (id < 0) and (id > 255) exclude each other: two lane masks counted on the SALU
+            clip_band += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(id < 0.0)) +
+                         (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(id > 255.0));
+            const Term tt{ad, __dmul_rn(d, d), d};
+            if (FIRST && s < 8) r[s] = tt;
+            else tadd(r[s & 7], tt);
+        }
+        clip += clip_band;
+    };
+#pragma unroll 1
+    for (int64_t t = 0; t < nrounds; ++t) {
+        const int q = (int)(t & 7);
+        __builtin_amdgcn_wave_barrier();  // the previous round's LDS reads are done
+#pragma unroll
+        for (int i = 0; i < 8; ++i) *reinterpret_cast<d2*>(wl + (8 * i + lrow) * kLfRow + 16 * lcol) = nx[i];
+        if (q == 0) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) *reinterpret_cast<u4*>(fl + (8 * i + lrow) * kLfRow + 16 * lcol) = fx[i];
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (t + 1 < nrounds) load_band(t + 1, q == 7);  // the next band (+ the next block's fixed bytes)
+        // this lane's leaf: 16 doubles and 16 fixed bytes of band q
+        double idv[16];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const d2 v = *reinterpret_cast<const d2*>(wl + lane * kLfRow + 16 * k);
+            idv[2 * k] = v.x, idv[2 * k + 1] = v.y;
+        }
+        const u4 fr = *reinterpret_cast<const u4*>(fl + lane * kLfRow + 16 * q);
+        const uint32_t fw[4] = {fr.x, fr.y, fr.z, fr.w};
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {  // zeros / 255s of 4 bytes: high bit of each byte = "nonzero" / "== 255"
+            const uint32_t lo7 = fw[w] & 0x7F7F7F7Fu;
+            nz_acc += (uint32_t)__builtin_popcount((lo7 + 0x7F7F7F7Fu) | fw[w] | 0x7F7F7F7Fu);
+            ff_acc += (uint32_t)__builtin_popcount(((lo7 + 0x01010101u) & fw[w]) | 0x7F7F7F7Fu);
+        }
+        ndw += 4;
+        if (q == 0)
+            band(std::true_type{}, idv, fw);
+        else
+            band(std::false_type{}, idv, fw);
+        if (q == 7) {  // the leaf is complete: its pairwise combine, then the block's tree over lanes
+            Term lf = tadd2(tadd2(tadd2(r[0], r[1]), tadd2(r[2], r[3])), tadd2(tadd2(r[4], r[5]), tadd2(r[6], r[7])));
+            lf = tadd2(lf, tshift<1>(lf));
+            lf = tadd2(lf, tshift<2>(lf));
+            lf = tadd2(lf, tshift<4>(lf));
+            lf = tadd2(lf, tshift<8>(lf));
+            lf = tadd2(lf, tshift<16>(lf));
+            lf = tadd2(lf, tshift<32>(lf));
+            if (lane == 0) {
+                const int64_t b = b0 + (t >> 3) * nwaves;
+                bsum[b] = lf.a, bsum[nb + b] = lf.q, bsum[2 * nb + b] = lf.d;
+            }
+        }
+    }
+    const uint32_t lo = 4 * ndw - (nz_acc - 28 * ndw), hi = ff_acc - 28 * ndw;
+    block_counts(Cnt{mx, lo, hi, lane == 0 ? clip : 0ull}, parts + wg);
+}
+
 // Fixed arrays of any other dtype (int8..int64, uint16..uint64, float16/32/64: the reference's
 // astype(np.float64) accepts them all): the same blocks, rounds, leaves and trees, each lane
 // reading its accumulator's 16 samples (stride 8) straight from memory.  Not a bandwidth path.
@@ -610,7 +751,10 @@ int launch_metrics_t(const double* ideal, const FT* fixed, int64_t n, double* ou
         const int g = (int)(want > kMetricBlocks ? kMetricBlocks : want);
         const unsigned grid = (unsigned)g + (prev_hi > prev_lo ? 1u : 0u);
         if constexpr (std::is_same_v<FT, uint8_t>) {
-            if (vec && kMetricGlds)
+            if (vec && kMetricLeaf)
+                hipLaunchKernelGGL(metrics_leaf_kernel, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, lo,
+                                   hi, prev_lo, prev_hi, state, parts + slot);
+            else if (vec && kMetricGlds)
                 hipLaunchKernelGGL(metrics_blocks_glds, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, lo,
                                    hi, prev_lo, prev_hi, state, parts + slot);
             else if (vec)
