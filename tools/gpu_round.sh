@@ -84,6 +84,8 @@ for s in $STEPS; do
         ltab) run long_taps_ab 400 python tools/long_taps_ab.py 66,128,257,450,500,1000,4099 \
                  warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_mr_v1.so abrun/libfir_hip_mr_d1.so \
                  abrun/libfir_hip_mr_d3.so abrun/libfir_hip_mr_t4w1d2.so abrun/libfir_hip_mr_old.so; fatal $? ;;
+        metab2) run metab2 300 python tools/metrics_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_mleaf0.so \
+                 abrun/libfir_hip_mleaf1024.so abrun/libfir_hip_mleaf256.so; fatal $? ;;
         asan) run asan 600 make -C warmup-fir-filter_amd/csrc asan-check; fatal $? ;;
         micro) run micro 300 tools/microbench/fir_micro 28 20; fatal $? ;;
         micro2d) run micro2d 300 tools/microbench/fir2d_micro 15; fatal $? ;;
