@@ -180,13 +180,11 @@ def test_acc64_wide_sums_are_exact():
             assert [int(got[i]) for i in idx] == want, (frac, acc, stage)
     # a shard's edge outputs through the same 128-bit sums (fir1d_fixed_edges_dev)
     m = 4096
-    xs = x[:m].copy()
     hl_n, hr_n = fo.halo_sizes(L)
-    hlv = x[m:m + hl_n].copy()
-    hrv = x[m + hl_n:m + hl_n + hr_n].copy()
+    full = np.where(np.arange(hl_n + m + hr_n) % 2 == 0, 32767, -32768).astype(np.int16)
+    hlv, xs, hrv = full[:hl_n].copy(), full[hl_n:hl_n + m].copy(), full[hl_n + m:].copy()
     y = torch_ops.fir1d_fixed_segment_dev(torch.from_numpy(xs).to(DEV), hq, torch.from_numpy(hlv).to(DEV),
                                           torch.from_numpy(hrv).to(DEV), 12, 80, fir_hip.OUT_U8_SAT)
-    full = np.concatenate([hlv, xs, hrv])
     eidx = list(range(0, 32)) + list(range(m - 32, m))
     want = _exact_out(full, hq, [hl_n + i for i in eidx], 12, 80, fo.OUT_U8_SAT)
     got = y.cpu().numpy()

@@ -86,6 +86,16 @@ for s in $STEPS; do
                  abrun/libfir_hip_mr_d3.so abrun/libfir_hip_mr_t4w1d2.so abrun/libfir_hip_mr_old.so; fatal $? ;;
         metab2) run metab2 300 python tools/metrics_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_mleaf0.so \
                  abrun/libfir_hip_mleaf1024.so abrun/libfir_hip_mleaf256.so; fatal $? ;;
+        ktrace_*) wl=${s#ktrace_}
+             run "ktrace_$wl" 150 rocprofv3 --kernel-trace -d "$OUT/ktrace_$wl" -o run --output-format csv -- \
+                 python bench.py --workload "$wl" --steps 20 --warmup 10 --cpu-seconds 0 --no-parity \
+                 --roofline-launches 20 --roofline-ramp 10; fatal $? ;;
+        sqlt) run sq_lt257 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+                 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_VALU --kernel-trace -d "$OUT/sq_lt257" \
+                 -o run --output-format csv -- python tools/long_taps_one.py 257 u8 6; fatal $?
+              run sq_lt257b 150 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_LDS \
+                 SQ_INSTS_MFMA --kernel-trace -d "$OUT/sq_lt257b" -o run --output-format csv -- \
+                 python tools/long_taps_one.py 257 u8 6; fatal $? ;;
         asan) run asan 600 make -C warmup-fir-filter_amd/csrc asan-check; fatal $? ;;
         micro) run micro 300 tools/microbench/fir_micro 28 20; fatal $? ;;
         micro2d) run micro2d 300 tools/microbench/fir2d_micro 15; fatal $? ;;
