@@ -86,12 +86,32 @@ for s in $STEPS; do
                  abrun/libfir_hip_mr_d3.so abrun/libfir_hip_mr_t4w1d2.so abrun/libfir_hip_mr_old.so; fatal $? ;;
         metab2) run metab2 300 python tools/metrics_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_mleaf0.so \
                  abrun/libfir_hip_mleaf1024.so abrun/libfir_hip_mleaf256.so; fatal $? ;;
+        ltab2) run long_taps_ab2 400 python tools/long_taps_ab.py 66,128,257,450,500,1000,4099 \
+                 warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_prev.so; fatal $? ;;
+        metab3) run metab3 300 python tools/metrics_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_prev.so \
+                 abrun/libfir_hip_met_ng1.so abrun/libfir_hip_met_b256.so abrun/libfir_hip_met_b256t4k.so \
+                 abrun/libfir_hip_met_t1k.so; fatal $? ;;
+        ltexp) run long_taps_exp 400 python tools/long_taps_ab.py 66,257,1000,4099 \
+                 warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_lt_e2.so --no-check; fatal $? ;;
+        ltx) run long_taps_x 400 python tools/long_taps_ab.py 66,128,257,450,1000,4099 \
+                 warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_lt_x4.so abrun/libfir_hip_lt_x99.so \
+                 abrun/libfir_hip_lt_bpd2.so abrun/libfir_hip_prev.so; fatal $? ;;
+        metp) run metp 300 python tools/metrics_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so \
+                 abrun/libfir_hip_met_p256.so abrun/libfir_hip_met_p1024.so abrun/libfir_hip_met_np.so \
+                 abrun/libfir_hip_met_npb256t4k.so; fatal $? ;;
+        metp2) run metp2 300 python tools/metrics_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so \
+                 abrun/libfir_hip_met_ng2.so abrun/libfir_hip_met_p128.so abrun/libfir_hip_met_npb256t4k.so; fatal $?
+              run metp3 300 python tools/metrics_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so \
+                 abrun/libfir_hip_met_e4.so --no-check; fatal $? ;;
+        metexp) run metexp 300 python tools/metrics_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so \
+                 abrun/libfir_hip_met_e1.so abrun/libfir_hip_met_e2.so abrun/libfir_hip_met_e3.so \
+                 abrun/libfir_hip_met_b256t4k.so --no-check; fatal $? ;;
         ktrace_*) wl=${s#ktrace_}
              run "ktrace_$wl" 150 rocprofv3 --kernel-trace -d "$OUT/ktrace_$wl" -o run --output-format csv -- \
                  python bench.py --workload "$wl" --steps 20 --warmup 10 --cpu-seconds 0 --no-parity \
                  --roofline-launches 20 --roofline-ramp 10; fatal $? ;;
         sqlt) run sq_lt257 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
-                 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_VALU --kernel-trace -d "$OUT/sq_lt257" \
+                 SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_VALU --kernel-trace -d "$OUT/sq_lt257" \
                  -o run --output-format csv -- python tools/long_taps_one.py 257 u8 6; fatal $?
               run sq_lt257b 150 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_LDS \
                  SQ_INSTS_MFMA --kernel-trace -d "$OUT/sq_lt257b" -o run --output-format csv -- \

@@ -15,6 +15,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--batch", type=int, default=20)
     ap.add_argument("--log2n", type=int, default=28)
+    ap.add_argument("--no-check", action="store_true", help="experiment builds with knowingly wrong sums: time only")
     a = ap.parse_args()
     libs = [ctypes.CDLL(p) for p in a.libs]
     dev = torch.device("cuda", 0)
@@ -41,7 +42,7 @@ def main():
         run(i, 30)
     torch.cuda.synchronize()
     ref = outs[0].cpu().numpy()
-    for i in range(1, len(libs)):
+    for i in range(1, len(libs) if not a.no_check else 1):
         got = outs[i].cpu().numpy()
         assert np.array_equal(got.view(np.uint64), ref.view(np.uint64)), (a.libs[i], got, ref)
     times = [[] for _ in libs]

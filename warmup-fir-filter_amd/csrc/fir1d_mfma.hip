@@ -910,20 +910,43 @@ static hipError_t launch_mfma_long(const void* x, void* y, int64_t rl, int64_t t
 #ifndef FIR_MR_DEPTH                 // iterations whose windows are in flight ahead of the one computed
 #define FIR_MR_DEPTH 2
 #endif
+#ifndef FIR_MR_EXP                   // timing experiments (wrong results): 1 no MFMAs, 2 no window DMAs
+#define FIR_MR_EXP 0
+#endif
 #ifndef FIR_MR_BLOCKS                // grid-stride blocks (4 waves each): one resident round
 #define FIR_MR_BLOCKS (256 * FIR_MR_WAVES)
 #endif
-constexpr int kMrTps = FIR_MR_TPS, kMrC = FIR_MR_C, kMrDepth = FIR_MR_DEPTH;
+#ifndef FIR_MR_XLDS_FROM             // chunk lengths whose windows are re-biased in LDS
+#define FIR_MR_XLDS_FROM 8
+#endif
+#ifndef FIR_MR_BPD                   // k-steps whose B fragments are read ahead of the MFMAs
+#define FIR_MR_BPD 3
+#endif
+constexpr int kMrTps = FIR_MR_TPS, kMrC = FIR_MR_C, kMrDepth = FIR_MR_DEPTH, kMrBpd = FIR_MR_BPD;
+// f(integral_constant<I>) for I in [B, E), unrolled at compile time
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
 constexpr int kMrTileLds = 2048;     // LDS bytes per tile window (128 vectors of 16 samples)
 
-template <int STAGE, bool ACC32, bool FAST, bool MULTI>
+// NS: k-steps per chunk, a compile-time count (the fragment table is zero-padded to whole chunks;
+// the launcher picks NS so the padding is at most one k-step below 9 and small above): the
+// chunk's MFMAs are one straight line.  (A runtime count, as a skip per slot or a jump into the
+// sequence, made the compiler copy every accumulator at each join: 600-800 v_mov per iteration,
+// VALU-bound at 257 taps, profiles/r04/sq_run_kernel_257.csv.)  mode: 0 FAST (no wrap, no int32
+// overflow), 1 acc_bits == 32, 2 acc_bits < 32 -- an epilogue branch, uniform per launch.
+template <int STAGE, int NS, bool MULTI>
 __global__ __launch_bounds__(kBlock, FIR_MR_WAVES) void fir1d_mfma_run_kernel(const uint8_t* __restrict__ x,
                                                                    typename OutTraits<STAGE>::T* __restrict__ y,
                                                                    int64_t rowlen, uint32_t tiles_per_row, uint32_t ntiles,
                                                                    const mf_i32x4* __restrict__ frag, int KS, int P,
-                                                                   uint32_t bias, int shl, int frac) {
+                                                                   uint32_t bias, int mode, int shl, int frac) {
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-    constexpr int TPS = kMrTps, C = kMrC;
+    constexpr int TPS = kMrTps, C = NS;
     constexpr int WT = kMfTile + 32 * C - 32;  // window samples per tile and chunk
     constexpr int NVT = (WT + 15) / 16;         // 16-sample vectors per tile window
     static_assert(NVT > kWave && NVT <= 2 * kWave && 16 * 2 * kWave <= kMrTileLds, "two DMAs per tile window");
@@ -931,14 +954,17 @@ __global__ __launch_bounds__(kBlock, FIR_MR_WAVES) void fir1d_mfma_run_kernel(co
     constexpr int BUF = TPS * kMrTileLds;
     constexpr int NBUF = kMrDepth + 1;          // LDS window buffers per wave (a ring)
     constexpr int NDMA = 2 * TPS;               // DMA instructions per iteration
+    constexpr int NST = TPS * (OLDS ? 4 : 1);   // store instructions per completed run
+    // the x - 128 of the B operand: in LDS once per window (long chunks) or per fragment read
+    constexpr bool XLDS = C >= FIR_MR_XLDS_FROM;
     __shared__ __attribute__((aligned(16))) uint8_t lds[kMfWaves][NBUF * BUF + (OLDS ? 4608 : 16)];
 
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r = lane & 31, hf = lane >> 5;
     uint32_t* ob = reinterpret_cast<uint32_t*>(lds[wv] + NBUF * BUF);
-    const int32_t sat_hi = FAST ? (int32_t)((256u << (frac & 31)) - 1u) : 0;
-    const int nch = (KS + C - 1) / C;
+    const int32_t sat_hi = (int32_t)((256u << (frac & 31)) - 1u);  // (mode 0)
+    const int nch = KS / C;  // KS: a multiple of C
     const uint32_t nruns = (ntiles + TPS - 1) / TPS;
     const uint32_t stride = gridDim.x * kMfWaves;
     uint32_t rn = blockIdx.x * kMfWaves + wv;
@@ -953,6 +979,7 @@ __global__ __launch_bounds__(kBlock, FIR_MR_WAVES) void fir1d_mfma_run_kernel(co
     // the run's TPS tile windows of chunk c into LDS buffer `buf`: per tile two 1 KiB DMAs
     // (vectors lane and lane + 64; the second past the window's NVT vectors reads zeros)
     auto issue_win = [&](uint32_t run, int c, int buf) __attribute__((always_inline)) {
+        if constexpr (FIR_MR_EXP == 2) return;
 #pragma unroll
         for (int q = 0; q < TPS; ++q) {
             const uint32_t t = run < nruns ? run * TPS + q : ntiles;
@@ -975,6 +1002,9 @@ __global__ __launch_bounds__(kBlock, FIR_MR_WAVES) void fir1d_mfma_run_kernel(co
     mf_i32x16 acc_ll[TPS], acc_mid[TPS];
 #pragma unroll
     for (int q = 0; q < TPS; ++q) acc_ll[q] = mf_i32x16{}, acc_mid[q] = mf_i32x16{};
+    mf_i32x16 biasv;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) biasv[i] = (int)bias;
     if constexpr (!MULTI) load_a(0);  // KS <= C: one chunk, fragments loaded once
     // iterations (run, chunk) in order; `ahead` is the one whose windows are issued next, kMrDepth
     // ahead of the one computed (past the last: runs past nruns, whose zero-size descriptors move
@@ -989,28 +1019,64 @@ __global__ __launch_bounds__(kBlock, FIR_MR_WAVES) void fir1d_mfma_run_kernel(co
     for (int d = 0; d < kMrDepth; ++d) {
         issue_win(ar, ac, d);
         advance(ar, ac);
+        if constexpr (!MULTI) {  // stand-ins for the stores of the iterations before the first (a
+            const __amdgpu_buffer_rsrc_t none = mf_rsrc(y, 0u);  // zero-size range: nothing written),
+#pragma unroll                                                   // so the counted wait below is exact
+            for (int k = 0; k < NST; ++k) __builtin_amdgcn_raw_buffer_store_b32(0, none, 0, 0, 0);
+        }
     }
     for (;;) {
         if constexpr (MULTI) load_a(c);  // issued before the next windows: its wait leaves them in flight
         issue_win(ar, ac, buf == 0 ? NBUF - 1 : buf - 1);  // the buffer computed last iteration
         advance(ar, ac);
-        // this iteration's windows (and A) landed; the kMrDepth younger iterations stay in flight
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kMrDepth * NDMA) : "memory");
+        // this iteration's windows (and A) landed; the kMrDepth younger iterations stay in flight.
+        // vmcnt also counts stores, in order with the loads: without fragment loads (one chunk)
+        // every iteration ends with its NST stores, so kMrDepth iterations of DMAs + stores may
+        // stay outstanding (counting only the DMAs drained the next iteration's windows too)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MULTI ? kMrDepth * NDMA : kMrDepth * (NDMA + NST)) : "memory");
         __builtin_amdgcn_wave_barrier();
-        const uint8_t* pl = lds[wv] + buf * BUF;
-        const int steps = min(C, KS - C * c);
+        uint8_t* pl = lds[wv] + buf * BUF;
+        if constexpr (XLDS) {  // xs = x - 128 once per window byte (each is read by ~C fragments)
 #pragma unroll
-        for (int s = 0; s < C; ++s) {
-            if (s < steps) {
+            for (int q = 0; q < TPS; ++q)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    mf_i32x4* v = reinterpret_cast<mf_i32x4*>(&pl[q * kMrTileLds + 1024 * i + 16 * lane]);
+                    *v = *v ^ (int)0x80808080;
+                }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+        }
+        // B fragments read kMrBpd k-steps ahead of their MFMAs (the sched barriers keep the reads
+        // there: left to itself the scheduler put each read right before its use, exposing the LDS
+        // latency every 2 MFMAs)
+        mf_i32x4 bq[C][TPS];
+        auto rd_b = [&](auto slc) __attribute__((always_inline)) {
+            constexpr int sl = decltype(slc)::value;
+#pragma unroll
+            for (int q = 0; q < TPS; ++q)
+                bq[sl][q] = *reinterpret_cast<const mf_i32x4*>(&pl[q * kMrTileLds + 32 * r + 32 * sl + 16 * hf]);
+        };
+        static_for<0, (kMrBpd < C ? kMrBpd : C)>([&](auto slc) { rd_b(slc); });
+        static_for<0, C>([&](auto slc) {
+            constexpr int sl = decltype(slc)::value;
+            if constexpr (sl + kMrBpd < C) rd_b(std::integral_constant<int, sl + kMrBpd>{});
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (FIR_MR_EXP != 1) {  // (FIR_MR_EXP: timing experiments only)
 #pragma unroll
                 for (int q = 0; q < TPS; ++q) {
-                    const mf_i32x4 bu = *reinterpret_cast<const mf_i32x4*>(&pl[q * kMrTileLds + 32 * r + 32 * s + 16 * hf]);
-                    const mf_i32x4 b = bu ^ (int)0x80808080;
-                    acc_ll[q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_lo[s], b, acc_ll[q], 0, 0, 0);
-                    acc_mid[q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_hi[s], b, acc_mid[q], 0, 0, 0);
+                    const mf_i32x4 b = XLDS ? bq[sl][q] : bq[sl][q] ^ (int)0x80808080;
+                    if constexpr (!MULTI && sl == 0) {  // a run's first k-step: the bias, and zero
+                        acc_ll[q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_lo[sl], b, biasv, 0, 0, 0);
+                        acc_mid[q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_hi[sl], b, mf_i32x16{}, 0, 0, 0);
+                    } else {
+                        acc_ll[q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_lo[sl], b, acc_ll[q], 0, 0, 0);
+                        acc_mid[q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_hi[sl], b, acc_mid[q], 0, 0, 0);
+                    }
                 }
             }
-        }
+            __builtin_amdgcn_sched_barrier(0);
+        });
         if (c == nch - 1) {  // the run's tiles are complete: combine, round, stage, store
 #pragma unroll
             for (int q = 0; q < TPS; ++q) {
@@ -1018,20 +1084,27 @@ __global__ __launch_bounds__(kBlock, FIR_MR_WAVES) void fir1d_mfma_run_kernel(co
                 const MfTile tl = mf_tile(t < ntiles ? t : ntiles - 1, rowlen, tiles_per_row);
                 const int m = t < ntiles ? (int)min((int64_t)kMfTile, tl.re - tl.ts) : 0;
                 int32_t o[16];
+                uint32_t a[16];
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const uint32_t a = (((uint32_t)acc_mid[q][i] << 8) + (uint32_t)acc_ll[q][i]) + bias;
-                    if constexpr (FAST)
-                        o[i] = STAGE == FIR_OUT_U8_SAT ? (int32_t)mf_med3_0(a, sat_hi) : (int32_t)a >> frac;
-                    else
-                        o[i] = round_acc<ACC32>(a, shl, frac);
+                for (int i = 0; i < 16; ++i)  // (one chunk: the bias started acc_ll)
+                    a[i] = ((uint32_t)acc_mid[q][i] << 8) + (uint32_t)acc_ll[q][i] + (MULTI ? bias : 0u);
+                if (mode == 0) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        o[i] = STAGE == FIR_OUT_U8_SAT ? (int32_t)mf_med3_0(a[i], sat_hi) : (int32_t)a[i] >> frac;
+                } else if (mode == 1) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) o[i] = round_acc<true>(a[i], 0, frac);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) o[i] = round_acc<false>(a[i], shl, frac);
                 }
-                acc_ll[q] = mf_i32x16{}, acc_mid[q] = mf_i32x16{};
+                if constexpr (MULTI) acc_ll[q] = mf_i32x16{}, acc_mid[q] = mf_i32x16{};
                 if constexpr (STAGE == FIR_OUT_U8_SAT) {
                     uint32_t w[4];
 #pragma unroll
                     for (int g4 = 0; g4 < 4; ++g4) {
-                        if constexpr (FAST)
+                        if (mode == 0)
                             w[g4] = mf_shr_byte<3>(mf_shr_byte<2>(mf_shr_byte<1>((uint32_t)o[4 * g4] >> frac, (uint32_t)o[4 * g4 + 1], frac),
                                                                   (uint32_t)o[4 * g4 + 2], frac),
                                                    (uint32_t)o[4 * g4 + 3], frac);
@@ -1075,12 +1148,27 @@ __global__ __launch_bounds__(kBlock, FIR_MR_WAVES) void fir1d_mfma_run_kernel(co
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMAs past the end land before the wave exits
 }
 
+// k-steps per chunk for KS k-steps: one chunk of exactly KS (rounded up to an even count past 10)
+// when KS <= kMrC; past it the chunk size among 8..kMrC (even) with the least zero padding, the
+// larger on a tie (fewer fragment reloads)
+static int mfma_run_ns(int KS) {
+    if (KS <= 10) return KS < 4 ? 4 : KS;
+    if (KS <= kMrC) return (KS + 1) & ~1;
+    int best = kMrC, pad = (KS + kMrC - 1) / kMrC * kMrC;
+    for (int ns = kMrC - 2; ns >= 8; ns -= 2) {
+        const int p = (KS + ns - 1) / ns * ns;
+        if (p < pad) best = ns, pad = p;
+    }
+    return best;
+}
+
 template <int STAGE>
 static hipError_t launch_mfma_run(const void* x, void* y, int64_t rl, int64_t tpr, int64_t ntiles, const int32_t* hq,
                                   int L, int P, int KS, uint32_t bias, bool fast, int frac, int acc_bits, hipStream_t s) {
     using OutT = typename OutTraits<STAGE>::T;
     std::string err;
-    const int ksp = (KS + kMrC - 1) / kMrC * kMrC;  // the table padded to whole chunks (zero fragments)
+    const int ns = mfma_run_ns(KS);
+    const int ksp = (KS + ns - 1) / ns * ns;  // the table padded to whole chunks (zero fragments)
     const mf_i32x4* fr = mfma_frag_table(hq, L, P, ksp, &err);
     if (!fr) return hipErrorOutOfMemory;
     TableHold hold(fr, s);
@@ -1088,22 +1176,30 @@ static hipError_t launch_mfma_run(const void* x, void* y, int64_t rl, int64_t tp
     const int64_t want = (nruns + kMfWaves - 1) / kMfWaves;
     const unsigned blocks = (unsigned)(want < FIR_MR_BLOCKS ? want : FIR_MR_BLOCKS);
     const uint32_t tp = (uint32_t)tpr, nt = (uint32_t)ntiles;
-    auto go = [&](auto multi) {
+    const int mode = fast ? 0 : acc_bits == 32 ? 1 : 2;
+    const int shl = mode == 2 ? 32 - acc_bits : 0;
+    auto go = [&](auto nsc, auto multi) {
+        constexpr int NS = decltype(nsc)::value;
         constexpr bool M = decltype(multi)::value;
-        if (fast)
-            hipLaunchKernelGGL((fir1d_mfma_run_kernel<STAGE, true, true, M>), dim3(blocks), dim3(kBlock), 0, s,
-                               (const uint8_t*)x, (OutT*)y, rl, tp, nt, fr, KS, P, bias, 0, frac);
-        else if (acc_bits == 32)
-            hipLaunchKernelGGL((fir1d_mfma_run_kernel<STAGE, true, false, M>), dim3(blocks), dim3(kBlock), 0, s,
-                               (const uint8_t*)x, (OutT*)y, rl, tp, nt, fr, KS, P, bias, 0, frac);
-        else
-            hipLaunchKernelGGL((fir1d_mfma_run_kernel<STAGE, false, false, M>), dim3(blocks), dim3(kBlock), 0, s,
-                               (const uint8_t*)x, (OutT*)y, rl, tp, nt, fr, KS, P, bias, 32 - acc_bits, frac);
+        hipLaunchKernelGGL((fir1d_mfma_run_kernel<STAGE, NS, M>), dim3(blocks), dim3(kBlock), 0, s, (const uint8_t*)x,
+                           (OutT*)y, rl, tp, nt, fr, ksp, P, bias, mode, shl, frac);
     };
-    if (KS > kMrC)
-        go(std::true_type{});
-    else
-        go(std::false_type{});
+    using std::integral_constant;
+    const bool multi = ksp > ns;
+#define FIR_MR_NS(n)                                                                       \
+    case n:                                                                                \
+        if (multi) {                                                                       \
+            if constexpr (n >= 8 && n % 2 == 0) go(integral_constant<int, n>{}, std::true_type{}); \
+        } else {                                                                           \
+            go(integral_constant<int, n>{}, std::false_type{});                            \
+        }                                                                                  \
+        break;
+    switch (ns) {
+        FIR_MR_NS(4) FIR_MR_NS(5) FIR_MR_NS(6) FIR_MR_NS(7) FIR_MR_NS(8) FIR_MR_NS(9) FIR_MR_NS(10) FIR_MR_NS(12)
+        FIR_MR_NS(14) FIR_MR_NS(16)
+        default: return hipErrorInvalidValue;
+    }
+#undef FIR_MR_NS
     return hipGetLastError();
 }
 

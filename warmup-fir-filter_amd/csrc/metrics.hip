@@ -46,6 +46,9 @@ constexpr bool kMetricGlds = FIR_METRIC_GLDS;
 #define FIR_METRIC_LEAF 1
 #endif
 constexpr bool kMetricLeaf = FIR_METRIC_LEAF;
+#ifndef FIR_METRIC_EXP  // timing experiments (wrong sums): 1 no chain in the part launches,
+#define FIR_METRIC_EXP 0  // 2 no count reduction in metrics_final, 3 no chain in metrics_final,
+#endif                    // 4 no chain in the publishing launch, 5 = 4 with plain block-sum stores
 #ifndef FIR_METRIC_MINB  // waves per SIMD the block kernel's registers must allow
 #define FIR_METRIC_MINB 4
 #endif
@@ -159,48 +162,200 @@ __device__ void block_counts(Cnt c, Cnt* dst) {
 }
 
 // The running sums state[0..2] += block sums [lo, hi) of |d|, d^2, d, in order (from 0.0 when
-// lo == 0).  Waves 0-2 take one array each: kChainDepth coalesced loads of 64 block sums in
-// flight, each group staged in the wave's LDS and read back in order by every lane at the same
-// address (a broadcast), so the dependent chain is one float64 add with a VGPR operand per 8192
-// samples (2.7 ns; fed by v_readlane instead: 8.7 ns, tools/microbench/chain_micro.hip).
-// `lds` holds 3 x kChainDepth x 64 doubles; no workgroup barrier inside.
+// lo == 0).  Waves 0-2 take one array each: groups of kChainDepth x 64 block sums, loaded
+// coalesced kChainGroups groups ahead (the loaded latency of one group, ~3 us beside a streaming
+// launch, exceeds the 1.4 us its adds take), each staged in the wave's LDS and read back in order
+// by every lane at the same address (a broadcast), so the dependent chain is one float64 add with
+// a VGPR operand per 8192 samples (2.7 ns; fed by v_readlane instead: 8.7 ns,
+// tools/microbench/chain_micro.hip).  `lds` holds 3 x kChainDepth x 64 doubles; no workgroup
+// barrier inside.
 constexpr int kChainDepth = 8;
+#ifndef FIR_METRIC_CHAIN_NG  // groups of block sums chain_follow checks and takes per batch
+#define FIR_METRIC_CHAIN_NG 1
+#endif
+constexpr int kChainGroups = FIR_METRIC_CHAIN_NG;
 constexpr int kChainLds = 3 * kChainDepth * kWave * (int)sizeof(double);
-__device__ void chain_range(const double* __restrict__ bsum, int64_t nb, int64_t lo, int64_t hi, double* state,
+constexpr int kChainGS = kChainDepth * kWave;  // block sums per group
+// s += sh[0], sh[1], ..., sh[len - 1] in order (sh: a staged group in the wave's LDS)
+__device__ __forceinline__ void add_group(double& s, const double* sh, int len) {
+    constexpr int GS = kChainGS;
+    int e = 0;
+    if (len == GS) {  // a full group: 16-element batches, the next batch's reads in flight
+        typedef double d2 __attribute__((ext_vector_type(2)));
+        d2 va[8], vb[8];
+        auto ld = [&](d2 (&v)[8], int e0) __attribute__((always_inline)) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const d2*>(&sh[e0 + 2 * j]);
+        };
+        auto add = [&](const d2 (&v)[8]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s = __dadd_rn(__dadd_rn(s, v[j].x), v[j].y);
+        };
+        ld(va, 0);
+#pragma unroll 1
+        for (int e0 = 0; e0 < GS; e0 += 32) {  // (sched barriers: keep each batch's reads
+            ld(vb, e0 + 16);                      // ahead of the previous batch's adds)
+            __builtin_amdgcn_sched_barrier(0);
+            add(va);
+            ld(va, (e0 + 32) & (GS - 1));  // (the last one re-reads batch 0, unused)
+            __builtin_amdgcn_sched_barrier(0);
+            add(vb);
+        }
+        e = GS;
+    }
+    for (; e + 16 <= len; e += 16) {
+        double v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = sh[e + j];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) s = __dadd_rn(s, v[j]);
+    }
+    for (; e < len; ++e) s = __dadd_rn(s, sh[e]);
+}
+__device__ __forceinline__ void chain_range(const double* __restrict__ bsum, int64_t nb, int64_t lo, int64_t hi, double* state,
                             uint8_t* lds, double* out = nullptr) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
     if (wv >= 3) return;
     const double* src = bsum + (int64_t)wv * nb;
     double* sh = reinterpret_cast<double*>(lds) + wv * kChainDepth * kWave;
     double s = lo == 0 ? 0.0 : state[wv];
-    constexpr int D = kChainDepth;
-    auto fetch = [&](int64_t c0, double (&q)[D]) {
+    constexpr int D = kChainDepth, NG = 2, GS = kChainGS;  // (deeper: no faster, more registers)
+    auto fetch = [&](int64_t c0, double (&q)[D]) __attribute__((always_inline)) {
 #pragma unroll
         for (int d = 0; d < D; ++d) q[d] = c0 + d * kWave + lane < hi ? src[c0 + d * kWave + lane] : 0.0;
     };
-    double q[D];
-    fetch(lo, q);
-    for (int64_t g0 = lo; g0 < hi; g0 += D * kWave) {
-        __builtin_amdgcn_wave_barrier();  // the previous group's reads are done (one wave: in order)
+    double q[NG][D];
 #pragma unroll
-        for (int d = 0; d < D; ++d) sh[d * kWave + lane] = q[d];
-        __builtin_amdgcn_wave_barrier();
-        fetch(g0 + D * kWave, q);  // the next group's loads, in flight during the adds
-        const int len = hi - g0 < D * kWave ? (int)(hi - g0) : D * kWave;
-        int e = 0;
-        for (; e + 16 <= len; e += 16) {
-            double v[16];
+    for (int k = 0; k < NG; ++k) fetch(lo + (int64_t)k * GS, q[k]);
+    for (int64_t g0 = lo; g0 < hi;) {
 #pragma unroll
-            for (int j = 0; j < 16; ++j) v[j] = sh[e + j];
+        for (int k = 0; k < NG; ++k) {  // group g0 is in q[k]
+            if (g0 < hi) {
+                __builtin_amdgcn_wave_barrier();  // the previous group's reads are done (one wave: in order)
 #pragma unroll
-            for (int j = 0; j < 16; ++j) s = __dadd_rn(s, v[j]);
+                for (int d = 0; d < D; ++d) sh[d * kWave + lane] = q[k][d];
+                __builtin_amdgcn_wave_barrier();
+                fetch(g0 + (int64_t)NG * GS, q[k]);  // NG groups ahead, in flight during the adds
+                add_group(s, sh, hi - g0 < GS ? (int)(hi - g0) : GS);
+                g0 += GS;
+            }
         }
-        for (; e < len; ++e) s = __dadd_rn(s, sh[e]);
     }
     if (lane == 0) {
         state[wv] = s;
         if (out) out[1 + wv] = s;
     }
+}
+
+// The chain inside the launch that produces the block sums (metrics_leaf_kernel<true>).  Streaming
+// wave w takes blocks w, w + nw, w + 2 nw, ... (nw waves) and publishes them in that order: the
+// three sums of a block by write-through (sc1) stores, then -- one round later, once the wave's
+// next band has landed, which drains those stores (vmcnt retires in order) -- its progress word
+// prog[w] = blocks done, by an sc1 store (no read-modify-write: 2048 waves adding to shared
+// counters serialised in the memory-side atomic unit, +114 us at 2^28, profiles/r04/metrics_publish_ab.txt).
+// Waves 0-2 of this workgroup follow: a group of kChainGS blocks is ready when every block's wave
+// has passed it; ONE wave-wide check of the next group's progress words (s_sleep
+// between polls, bounded), every further group already ready taken with it (up to kChainGroups),
+// then the sums, every read of a handed-off word by a returning atomic (coherent_read below).
+// Blocks [nbf, nb) (the ragged
+// block) were written by an earlier launch.  The chain's waves run at raised priority (a
+// dependent float64 add per block, sharing a SIMD with streaming waves).  A wait past the spin
+// bound (no correct run reaches it: the producers never wait) makes the sums NaN.
+constexpr uint32_t kChainSpinCap = 1u << 24;  // x (s_sleep 2 + a poll): ~1 s
+typedef __attribute__((address_space(1))) uint64_t gu64;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+// A read of a word another XCD wrote in this launch (or the memset before it) that no cache of the
+// reading XCD can answer: a returning agent-scope atomic (performed past the XCD's L2).  Loads --
+// plain, sc1, or behind an agent acquire -- are served by the reading XCD's L2, which can hold the
+// line from an earlier call: in a graph replay the chain then saw the previous replay's progress
+// words and sums (tests/test_gpu_graphs.py, all 9 full blocks of seed 1 in seed 2's sums).
+// (The zero operand is opaque: with a literal 0 the compiler turns the idempotent RMW into a load.)
+__device__ __forceinline__ uint32_t opaque_zero() {
+    uint32_t z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return z;
+}
+__device__ __forceinline__ uint32_t coherent_read(const uint32_t* p) {
+    return __hip_atomic_fetch_add((gu32*)p, opaque_zero(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double coherent_read(const double* p) {
+    return __builtin_bit_cast(double, __hip_atomic_fetch_or((gu64*)p, (uint64_t)opaque_zero(), __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void chain_follow(const double* __restrict__ bsum, int64_t nb, int64_t nbf, uint32_t* prog,
+                                             int64_t nw, double* state, uint8_t* lds) {
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
+    if (wv >= 3) return;
+    __builtin_amdgcn_s_setprio(3);
+    const double* src = bsum + (int64_t)wv * nb;
+    double* sh = reinterpret_cast<double*>(lds) + wv * kChainDepth * kWave;
+    constexpr int D = kChainDepth, NG = kChainGroups, GS = kChainGS;
+    double s = 0.0;
+    bool ok = true;
+    const int64_t ngr = (nbf + GS - 1) / GS;
+    auto need = [&](int64_t g) { return (int)(nbf - g * GS < GS ? nbf - g * GS : GS); };
+    const uint32_t nw32 = (uint32_t)nw;  // (block indices < 2^32: n < 2^40)
+    // how many of groups g, g + 1, ..., g + NG - 1 are complete, counting from g (one round trip:
+    // every progress word of the NG groups in flight at once; wave-uniform)
+    auto ready_prefix = [&](int64_t g) {
+        uint32_t v[NG][D], lay[NG][D];
+#pragma unroll
+        for (int i = 0; i < NG; ++i) {
+            const uint32_t c0 = (uint32_t)((g + i) * GS), l0 = c0 / nw32, r0 = c0 - l0 * nw32;
+#pragma unroll
+            for (int d = 0; d < D; ++d) {  // block c0 + 64 d + lane = layer nw + w: wave w's (layer + 1)-th
+                const uint32_t r = r0 + d * kWave + lane, w = r % nw32;
+                lay[i][d] = l0 + r / nw32;
+                v[i][d] = coherent_read(prog + w);
+            }
+        }
+        int k = 0;
+#pragma unroll
+        for (int i = 0; i < NG; ++i) {
+            bool mine = true;
+#pragma unroll
+            for (int d = 0; d < D; ++d) mine &= (g + i) * GS + d * kWave + lane >= nbf || v[i][d] >= lay[i][d] + 1;
+            const bool all = __builtin_amdgcn_ballot_w64(!mine) == 0;
+            if (k == i && all && g + i < ngr) k = i + 1;
+        }
+        return k;
+    };
+    for (int64_t g = 0; g < ngr && ok;) {
+        int k = 0;
+        for (uint32_t spins = 0; (k = ready_prefix(g)) == 0;) {
+            if (++spins > kChainSpinCap) {
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!ok) break;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the reads below the polls)
+        double q[NG][D];
+#pragma unroll
+        for (int i = 0; i < NG; ++i) {
+            const int64_t c0 = (g + i) * GS;
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const int64_t b = c0 + d * kWave + lane;
+                q[i][d] = i < k && b < nbf ? coherent_read(src + b) : 0.0;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NG; ++i) {
+            if (i < k) {
+                __builtin_amdgcn_wave_barrier();  // the previous group's reads are done
+#pragma unroll
+                for (int d = 0; d < D; ++d) sh[d * kWave + lane] = q[i][d];
+                __builtin_amdgcn_wave_barrier();
+                add_group(s, sh, need(g + i));
+            }
+        }
+        g += k;
+    }
+    for (int64_t b = nbf; b < nb; ++b) s = __dadd_rn(s, coherent_read(src + b));
+    if (lane == 0) state[wv] = ok ? s : __builtin_nan("");
+    __builtin_amdgcn_s_setprio(0);
 }
 
 // A round's 64 lane sums (lane (leaf k, accumulator j)) -> lane 0: each leaf's
@@ -439,18 +594,26 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mt_rsrc(const void* p, uint32_
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
     return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0, (int)bytes, 0x00020000);
 }
+// PUB: one launch over every full block, publishing each block's sums to the chain workgroup
+// (chain_follow; c_lo/c_hi unused) instead of chaining the previous launch's part.
+template <bool PUB>
 __global__ __launch_bounds__(kBlock, 2) void metrics_leaf_kernel(const double* __restrict__ ideal,
                                                                 const uint8_t* __restrict__ fixed,
                                                                 double* __restrict__ bsum, int64_t nb, int64_t b_lo,
                                                                 int64_t b_hi, int64_t c_lo, int64_t c_hi,
-                                                                double* __restrict__ state, Cnt* __restrict__ parts) {
+                                                                double* __restrict__ state, Cnt* __restrict__ parts,
+                                                                uint32_t* __restrict__ cnt) {
     typedef double d2 __attribute__((ext_vector_type(2)));
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     typedef int i4 __attribute__((ext_vector_type(4)));
     __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock / kWave * kLfWaveLds];
-    const bool chain = c_hi > c_lo;
+    const bool chain = PUB || c_hi > c_lo;
     if (chain && blockIdx.x == 0) {
-        chain_range(bsum, nb, c_lo, c_hi, state, smem);
+        if constexpr (PUB) {
+            if (FIR_METRIC_EXP != 4 && FIR_METRIC_EXP != 5) chain_follow(bsum, nb, b_hi, cnt, (int64_t)(gridDim.x - 1) * (kBlock / kWave), state, smem);
+        }
+        else if (FIR_METRIC_EXP != 1)  // (EXP: timing experiments)
+            chain_range(bsum, nb, c_lo, c_hi, state, smem);
         return;
     }
     const int wg = blockIdx.x - (chain ? 1 : 0);
@@ -458,7 +621,8 @@ __global__ __launch_bounds__(kBlock, 2) void metrics_leaf_kernel(const double* _
     uint8_t* wl = smem + wv * kLfWaveLds;
     uint8_t* fl = wl + kWave * kLfRow;  // fixed rows
     const int64_t nwaves = (int64_t)(gridDim.x - (chain ? 1 : 0)) * (kBlock / kWave);
-    const int64_t b0 = b_lo + (int64_t)wg * (kBlock / kWave) + wv;
+    const int64_t sw = (int64_t)wg * (kBlock / kWave) + wv;  // streaming wave index
+    const int64_t b0 = b_lo + sw;
     const int64_t nrounds = b0 < b_hi ? ((b_hi - 1 - b0) / nwaves + 1) * 8 : 0;
     double mx = 0.0;
     uint32_t nz_acc = 0, ff_acc = 0, ndw = 0;  // v_bcnt sums (28 + count per dword) and dwords seen
@@ -517,6 +681,14 @@ __global__ __launch_bounds__(kBlock, 2) void metrics_leaf_kernel(const double* _
             for (int i = 0; i < 8; ++i) *reinterpret_cast<u4*>(fl + (8 * i + lrow) * kLfRow + 16 * lcol) = fx[i];
         }
         __builtin_amdgcn_wave_barrier();
+        if constexpr (PUB && FIR_METRIC_EXP != 5) {
+            if (q == 1 && t > 8) {  // the previous block's sums: stored two rounds ago, before the loads of
+                                    // the band just staged, so this (already satisfied) wait drains them
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0)
+                    __hip_atomic_store((gu32*)(cnt + sw), (uint32_t)(t >> 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
         if (t + 1 < nrounds) load_band(t + 1, q == 7);  // the next band (+ the next block's fixed bytes)
         // this lane's leaf: 16 doubles and 16 fixed bytes of band q
         double idv[16];
@@ -548,8 +720,24 @@ __global__ __launch_bounds__(kBlock, 2) void metrics_leaf_kernel(const double* _
             lf = tadd2(lf, tshift<32>(lf));
             if (lane == 0) {
                 const int64_t b = b0 + (t >> 3) * nwaves;
-                bsum[b] = lf.a, bsum[nb + b] = lf.q, bsum[2 * nb + b] = lf.d;
+                if constexpr (PUB && FIR_METRIC_EXP != 5) {  // write-through; progress published later
+                    __hip_atomic_store((gu64*)(bsum + b), __builtin_bit_cast(uint64_t, lf.a), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store((gu64*)(bsum + nb + b), __builtin_bit_cast(uint64_t, lf.q), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store((gu64*)(bsum + 2 * nb + b), __builtin_bit_cast(uint64_t, lf.d), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    bsum[b] = lf.a, bsum[nb + b] = lf.q, bsum[2 * nb + b] = lf.d;
+                }
             }
+        }
+    }
+    if constexpr (PUB && FIR_METRIC_EXP != 5) {  // the wave's last block
+        if (nrounds) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0)
+                __hip_atomic_store((gu32*)(cnt + sw), (uint32_t)(nrounds >> 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     const uint32_t lo = 4 * ndw - (nz_acc - 28 * ndw), hi = ff_acc - 28 * ndw;
@@ -601,7 +789,13 @@ __global__ __launch_bounds__(kBlock) void metrics_blocks_any(const double* __res
 template <typename FT>
 __global__ __launch_bounds__(kBlock) void metrics_ragged(const double* __restrict__ ideal, const FT* __restrict__ fixed,
                                                          int64_t n, double* __restrict__ bsum, int64_t nb,
-                                                         Cnt* __restrict__ part) {
+                                                         Cnt* __restrict__ part, uint32_t* __restrict__ prog, int nprog) {
+    // prog / nprog: the publishing launch's progress words, zeroed here -- by a kernel ahead of it in
+    // the stream, not a memset node: replayed in a graph behind other kernels, a captured
+    // hipMemsetAsync left the previous replay's words in place (tests/test_gpu_graphs.py); with no
+    // ragged block only the zeroing runs
+    for (int i = threadIdx.x; i < nprog; i += kBlock) prog[i] = 0u;
+    if (n % kPwBlock == 0) return;
     __shared__ int leaf_off[kPwMaxLeaves], leaf_len[kPwMaxLeaves];
     __shared__ Term lsum[kPwMaxLeaves];
     __shared__ int nleaves;
@@ -669,12 +863,12 @@ __global__ __launch_bounds__(kBlock) void metrics_final(const double* __restrict
     __shared__ __attribute__((aligned(16))) uint8_t smem[kChainLds];
     const int t = threadIdx.x;
     Cnt c{0.0, 0, 0, 0};
-    for (int i = t; i < nparts; i += kBlock) {
+    for (int i = t; i < nparts && FIR_METRIC_EXP != 2; i += kBlock) {
         const Cnt& q = parts[i];
         c.mx = fmax(c.mx, q.mx), c.lo += q.lo, c.hi += q.hi, c.clip += q.clip;
     }
     red[t] = c;
-    if (c_lo < nb) chain_range(bsum, nb, c_lo, nb, state, smem, out);  // out[1..3]
+    if (c_lo < nb && FIR_METRIC_EXP != 3) chain_range(bsum, nb, c_lo, nb, state, smem, out);  // out[1..3]
     if (c_lo >= nb && t < 3) out[1 + t] = nb > 0 ? state[t] : 0.0;  // (no last part: n == 0)
     __syncthreads();
     for (int w = kBlock / 2; w > 0; w >>= 1) {
@@ -712,8 +906,23 @@ constexpr int64_t kTailPart = FIR_METRIC_TAIL, kBodyPart = FIR_METRIC_BODY;
 constexpr int kMaxParts = 16;
 constexpr int64_t kCntSlots = (int64_t)kMaxParts * kMetricBlocks + 1;
 
+#ifndef FIR_METRIC_PERSIST  // 1: u8 (aligned) in ONE launch whose chain workgroup follows the
+#define FIR_METRIC_PERSIST 1   // published block sums (metrics_leaf_kernel<true>)
+#endif
+#ifndef FIR_METRIC_PBLOCKS   // streaming workgroups of that launch
+#define FIR_METRIC_PBLOCKS 256
+#endif
+constexpr int kMetricPBlocks = FIR_METRIC_PBLOCKS;
+static_assert(kMetricPBlocks + 1 <= kCntSlots, "count slots");
+// the progress words of the publishing launch's streaming waves (zeroed every call by the kernel
+// ahead of it), at the start of the work buffer
+static size_t metrics_cnt_bytes(int64_t) { return (size_t)4 * kMetricPBlocks * (kBlock / kWave); }
+
+// Work buffer: the publish counters, Cnt per workgroup of every launch (+ the ragged block's), the
+// 3 running sums, then the block sums [3][nb].
 size_t metrics_work_bytes(int64_t n) {
-    return sizeof(Cnt) * kCntSlots + 64 + 3 * sizeof(double) * (size_t)metrics_nblocks(n < 0 ? 0 : n);
+    if (n < 0) n = 0;
+    return metrics_cnt_bytes(n) + sizeof(Cnt) * kCntSlots + 64 + 3 * sizeof(double) * (size_t)metrics_nblocks(n);
 }
 
 namespace {
@@ -722,10 +931,29 @@ template <typename FT>
 int launch_metrics_t(const double* ideal, const FT* fixed, int64_t n, double* out, void* work, hipStream_t stream,
                      std::string* err) {
     const int64_t nb = metrics_nblocks(n), nbf = n / kPwBlock;
-    Cnt* parts = (Cnt*)work;
-    double* state = (double*)((char*)work + sizeof(Cnt) * kCntSlots);
+    const size_t cb = metrics_cnt_bytes(n);
+    uint32_t* cnt = (uint32_t*)work;
+    Cnt* parts = (Cnt*)((char*)work + cb);
+    double* state = (double*)((char*)parts + sizeof(Cnt) * kCntSlots);
     double* bsum = state + 8;
     const bool vec = (uintptr_t)ideal % 16 == 0 && (uintptr_t)fixed % 16 == 0;
+    if constexpr (std::is_same_v<FT, uint8_t>) {
+        if (vec && kMetricLeaf && FIR_METRIC_PERSIST && nbf > 0) {  // one streaming launch
+            // the progress words zeroed and the ragged block (if any) summed first: the chain adds it last
+            const int slot = nb > nbf ? 1 : 0;
+            hipLaunchKernelGGL(metrics_ragged<FT>, dim3(1), dim3(kBlock), 0, stream, ideal, fixed, n, bsum, nb, parts, cnt,
+                               (int)(cb / 4));
+            const int64_t want = (nbf + kBlock / kWave - 1) / (kBlock / kWave);
+            const int g = (int)(want > kMetricPBlocks ? kMetricPBlocks : want);
+            hipLaunchKernelGGL(metrics_leaf_kernel<true>, dim3(g + 1), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb,
+                               (int64_t)0, nbf, (int64_t)0, (int64_t)0, state, parts + slot, cnt);
+            hipLaunchKernelGGL(metrics_final, dim3(1), dim3(kBlock), 0, stream, (const double*)bsum, nb, nb, state,
+                               (const Cnt*)parts, slot + g, n, out);
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return *err = std::string("metrics launch failed: ") + hipGetErrorString(e), FIR_EHIP;
+            return FIR_OK;
+        }
+    }
     // parts from the end: kTailPart blocks last, kBodyPart before it, the first part the rest; the
     // chain of a part (2.7 ns per block) hides under the next part's streaming (~14 ns per block),
     // only the last part's chain is exposed (A/B, profiles/r03/metrics_exact_ab.txt: equal parts
@@ -752,8 +980,8 @@ int launch_metrics_t(const double* ideal, const FT* fixed, int64_t n, double* ou
         const unsigned grid = (unsigned)g + (prev_hi > prev_lo ? 1u : 0u);
         if constexpr (std::is_same_v<FT, uint8_t>) {
             if (vec && kMetricLeaf)
-                hipLaunchKernelGGL(metrics_leaf_kernel, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, lo,
-                                   hi, prev_lo, prev_hi, state, parts + slot);
+                hipLaunchKernelGGL(metrics_leaf_kernel<false>, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb,
+                                   lo, hi, prev_lo, prev_hi, state, parts + slot, (uint32_t*)nullptr);
             else if (vec && kMetricGlds)
                 hipLaunchKernelGGL(metrics_blocks_glds, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, lo,
                                    hi, prev_lo, prev_hi, state, parts + slot);
@@ -772,7 +1000,8 @@ int launch_metrics_t(const double* ideal, const FT* fixed, int64_t n, double* ou
         prev_lo = lo, prev_hi = hi;
     }
     if (nb > nbf) {  // the ragged last block (its sum is the last in order)
-        hipLaunchKernelGGL(metrics_ragged<FT>, dim3(1), dim3(kBlock), 0, stream, ideal, fixed, n, bsum, nb, parts + slot);
+        hipLaunchKernelGGL(metrics_ragged<FT>, dim3(1), dim3(kBlock), 0, stream, ideal, fixed, n, bsum, nb, parts + slot,
+                           (uint32_t*)nullptr, 0);
         ++slot;
     }
     hipLaunchKernelGGL(metrics_final, dim3(1), dim3(kBlock), 0, stream, (const double*)bsum, nb, prev_lo, state,

@@ -91,6 +91,32 @@ _lib = None
 _lock = threading.Lock()
 
 
+def _share_torch_hip_runtime() -> None:
+    """Make this library and PyTorch use ONE HIP runtime in a process that has both.
+
+    PyTorch-ROCm ships its own libamdhip64 / libhsa-runtime64 with the same sonames as
+    /opt/rocm's.  Loaded after torch, libfir_hip binds to torch's copies (the soname is already
+    loaded); loaded first, it pulls in /opt/rocm's, torch later loads its own by path, and the
+    second HSA runtime in the process finds no device ("No HIP GPUs are available").  So when
+    torch is installed, its runtime is loaded first, whichever of the two is imported first.
+    FIR_HIP_OWN_RUNTIME=1 keeps /opt/rocm's (a process without torch uses it anyway)."""
+    if os.environ.get("FIR_HIP_OWN_RUNTIME") == "1":
+        return
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return
+    tlib = Path(spec.origin).parent / "lib"
+    for name in ("libhsa-runtime64.so", "libamdhip64.so"):
+        p = tlib / name
+        if p.exists():
+            try:
+                ctypes.CDLL(str(p), mode=ctypes.RTLD_GLOBAL)
+            except OSError:
+                return
+
+
 def lib() -> ctypes.CDLL:
     """Load libfir_hip.so once; raise FirHipError if it is missing or mismatched."""
     global _lib
@@ -104,6 +130,7 @@ def lib() -> ctypes.CDLL:
             raise FirHipError(
                 f"{path} is not built: run `make -C warmup-fir-filter_amd/csrc` or "
                 "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
+        _share_torch_hip_runtime()
         try:
             handle = ctypes.CDLL(str(path))
         except OSError as exc:
