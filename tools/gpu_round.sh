@@ -93,9 +93,8 @@ for s in $STEPS; do
                  abrun/libfir_hip_met_t1k.so; fatal $? ;;
         ltexp) run long_taps_exp 400 python tools/long_taps_ab.py 66,257,1000,4099 \
                  warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_lt_e2.so --no-check; fatal $? ;;
-        ltx) run long_taps_x 400 python tools/long_taps_ab.py 66,128,257,450,1000,4099 \
-                 warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_lt_x4.so abrun/libfir_hip_lt_x99.so \
-                 abrun/libfir_hip_lt_bpd2.so abrun/libfir_hip_prev.so; fatal $? ;;
+        lth) run long_taps_head 400 python tools/long_taps_ab.py 66,128,257,450,500,1000,2048,4099 \
+                 warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_head.so; fatal $? ;;
         metp) run metp 300 python tools/metrics_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so \
                  abrun/libfir_hip_met_p256.so abrun/libfir_hip_met_p1024.so abrun/libfir_hip_met_np.so \
                  abrun/libfir_hip_met_npb256t4k.so; fatal $? ;;

@@ -939,14 +939,31 @@ constexpr int kMrTileLds = 2048;     // LDS bytes per tile window (128 vectors o
 // sequence, made the compiler copy every accumulator at each join: 600-800 v_mov per iteration,
 // VALU-bound at 257 taps, profiles/r04/sq_run_kernel_257.csv.)  mode: 0 FAST (no wrap, no int32
 // overflow), 1 acc_bits == 32, 2 acc_bits < 32 -- an epilogue branch, uniform per launch.
-template <int STAGE, int NS, bool MULTI>
-__global__ __launch_bounds__(kBlock, FIR_MR_WAVES) void fir1d_mfma_run_kernel(const uint8_t* __restrict__ x,
+// TPS tiles per run: 2 (FIR_MR_TPS) at 2 waves per SIMD; 1 at 3 waves per SIMD (and windows one
+// iteration deeper) for one-chunk filters up to 10 k-steps, whose registers fit a third wave
+// (A/B at 66 / 128 / 257 taps: 109 / 119 / 151 us vs 127 / 131 / 170, profiles/r04/long_taps_run_v3_ab.txt)
+// Several chunks: FIR_MR_MWAVES waves per SIMD.  FIR_MR_ADBL 1 loads the next chunk's fragments
+// during this one's MFMAs into a second register set (A/B, profiles/r04/long_taps_run_v3_ab.txt:
+// with chunks of 6-8 at 2 waves 4099 taps 2415 us, of up to 16 at 1 wave 3166, vs 2205 for one set
+// loaded at the top of each iteration at 2 waves -- the per-iteration costs and the waves, not
+// the fragment latency, bound this loop)
+#ifndef FIR_MR_MWAVES
+#define FIR_MR_MWAVES 2
+#endif
+#ifndef FIR_MR_ADBL
+#define FIR_MR_ADBL 0
+#endif
+template <int TPS_, bool MULTI>
+constexpr int mr_waves() { return MULTI ? FIR_MR_MWAVES : TPS_ == 1 ? 3 : FIR_MR_WAVES; }
+template <int STAGE, int NS, bool MULTI, int TPS_>
+__global__ __launch_bounds__(kBlock, (mr_waves<TPS_, MULTI>())) void fir1d_mfma_run_kernel(const uint8_t* __restrict__ x,
                                                                    typename OutTraits<STAGE>::T* __restrict__ y,
                                                                    int64_t rowlen, uint32_t tiles_per_row, uint32_t ntiles,
                                                                    const mf_i32x4* __restrict__ frag, int KS, int P,
                                                                    uint32_t bias, int mode, int shl, int frac) {
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-    constexpr int TPS = kMrTps, C = NS;
+    constexpr int TPS = TPS_, C = NS;
+    constexpr int kMrDepth = TPS == 1 ? 3 : ::fir::kMrDepth;
     constexpr int WT = kMfTile + 32 * C - 32;  // window samples per tile and chunk
     constexpr int NVT = (WT + 15) / 16;         // 16-sample vectors per tile window
     static_assert(NVT > kWave && NVT <= 2 * kWave && 16 * 2 * kWave <= kMrTileLds, "two DMAs per tile window");
@@ -970,11 +987,15 @@ __global__ __launch_bounds__(kBlock, FIR_MR_WAVES) void fir1d_mfma_run_kernel(co
     uint32_t rn = blockIdx.x * kMfWaves + wv;
     if (rn >= nruns) return;  // wave-uniform: nothing issued yet
 
-    mf_i32x4 a_lo[C], a_hi[C];
-    auto load_a = [&](int c) __attribute__((always_inline)) {
+    // tap fragments: one set (one chunk: loaded once), or two (several chunks: the next iteration's
+    // chunk loaded while this one's MFMAs run -- loaded at the top of each iteration instead, the
+    // L2 latency of 2 C loads was exposed every iteration, 4099 taps 2087 us)
+    constexpr bool ADBL = MULTI && FIR_MR_ADBL;
+    mf_i32x4 a0_lo[C], a0_hi[C], a1_lo[ADBL ? C : 1], a1_hi[ADBL ? C : 1];
+    auto load_a = [&](mf_i32x4 (&lo)[C], mf_i32x4 (&hi)[C], int c) __attribute__((always_inline)) {
         const mf_i32x4* f = frag + (int64_t)c * C * 2 * kWave + lane;
 #pragma unroll
-        for (int s = 0; s < C; ++s) a_lo[s] = f[(2 * s) * kWave], a_hi[s] = f[(2 * s + 1) * kWave];
+        for (int s = 0; s < C; ++s) lo[s] = f[(2 * s) * kWave], hi[s] = f[(2 * s + 1) * kWave];
     };
     // the run's TPS tile windows of chunk c into LDS buffer `buf`: per tile two 1 KiB DMAs
     // (vectors lane and lane + 64; the second past the window's NVT vectors reads zeros)
@@ -1005,7 +1026,7 @@ __global__ __launch_bounds__(kBlock, FIR_MR_WAVES) void fir1d_mfma_run_kernel(co
     mf_i32x16 biasv;
 #pragma unroll
     for (int i = 0; i < 16; ++i) biasv[i] = (int)bias;
-    if constexpr (!MULTI) load_a(0);  // KS <= C: one chunk, fragments loaded once
+    if constexpr (!MULTI) load_a(a0_lo, a0_hi, 0);  // KS <= C: one chunk, fragments loaded once
     // iterations (run, chunk) in order; `ahead` is the one whose windows are issued next, kMrDepth
     // ahead of the one computed (past the last: runs past nruns, whose zero-size descriptors move
     // nothing -- every iteration issues the same NDMA operations, so the counted wait is exact)
@@ -1025,15 +1046,38 @@ __global__ __launch_bounds__(kBlock, FIR_MR_WAVES) void fir1d_mfma_run_kernel(co
             for (int k = 0; k < NST; ++k) __builtin_amdgcn_raw_buffer_store_b32(0, none, 0, 0, 0);
         }
     }
-    for (;;) {
-        if constexpr (MULTI) load_a(c);  // issued before the next windows: its wait leaves them in flight
+    if constexpr (ADBL) load_a(a0_lo, a0_hi, 0);  // behind the first windows (the first wait below)
+    bool first = true, stored = false;
+    // one iteration (run rn, chunk c) on fragments acur, loading anext for the next one; false at the end
+    auto body = [&](mf_i32x4 (&a_lo)[C], mf_i32x4 (&a_hi)[C], mf_i32x4 (&an_lo)[C], mf_i32x4 (&an_hi)[C])
+                    __attribute__((always_inline)) -> bool {
+        uint32_t nr = rn;
+        int nc = c;
+        advance(nr, nc);
+        if constexpr (ADBL) load_a(an_lo, an_hi, nc);  // (past the last run: a valid chunk, unused)
+        else if constexpr (MULTI) load_a(a_lo, a_hi, c);  // issued before the next windows: its wait leaves them in flight
         issue_win(ar, ac, buf == 0 ? NBUF - 1 : buf - 1);  // the buffer computed last iteration
         advance(ar, ac);
-        // this iteration's windows (and A) landed; the kMrDepth younger iterations stay in flight.
-        // vmcnt also counts stores, in order with the loads: without fragment loads (one chunk)
-        // every iteration ends with its NST stores, so kMrDepth iterations of DMAs + stores may
-        // stay outstanding (counting only the DMAs drained the next iteration's windows too)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MULTI ? kMrDepth * NDMA : kMrDepth * (NDMA + NST)) : "memory");
+        // this iteration's windows (and A) landed; the younger operations stay in flight.  vmcnt
+        // also counts stores, in order with the loads.  One chunk: every iteration ends with its
+        // NST stores, so kMrDepth iterations of DMAs + stores may stay outstanding (counting only
+        // the DMAs drained the next iteration's windows too).  Several: A(i) was issued at the top
+        // of the previous iteration, after this iteration's windows, so what may stay outstanding
+        // is everything issued after A(i): the previous iteration's DMAs and stores (if it ended a
+        // run) and this iteration's A(i + 1) and DMAs.
+        if constexpr (MULTI && !ADBL) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kMrDepth * NDMA) : "memory");
+        } else if constexpr (MULTI) {
+            if (first)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * C + NDMA) : "memory");
+            else if (stored)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * C + 2 * NDMA + NST) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * C + 2 * NDMA) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kMrDepth * (NDMA + NST)) : "memory");
+        }
+        first = false;
         __builtin_amdgcn_wave_barrier();
         uint8_t* pl = lds[wv] + buf * BUF;
         if constexpr (XLDS) {  // xs = x - 128 once per window byte (each is read by ~C fragments)
@@ -1137,20 +1181,27 @@ __global__ __launch_bounds__(kBlock, FIR_MR_WAVES) void fir1d_mfma_run_kernel(co
                 }
             }
         }
-        uint32_t nr = rn;
-        int nc = c;
-        advance(nr, nc);
-        if (nr >= nruns) break;
+        stored = c == nch - 1;
+        if (nr >= nruns) return false;
         rn = nr, c = nc, buf = buf + 1 == NBUF ? 0 : buf + 1;
         __builtin_amdgcn_wave_barrier();  // this iteration's B reads are done before its buffer is refilled
         asm volatile("" ::: "memory");
+        return true;
+    };
+    if constexpr (ADBL) {
+        for (;;) {  // the two fragment sets alternate (unrolled: registers are not indexable)
+            if (!body(a0_lo, a0_hi, a1_lo, a1_hi)) break;
+            if (!body(a1_lo, a1_hi, a0_lo, a0_hi)) break;
+        }
+    } else {
+        while (body(a0_lo, a0_hi, a0_lo, a0_hi)) {}
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMAs past the end land before the wave exits
 }
 
 // k-steps per chunk for KS k-steps: one chunk of exactly KS (rounded up to an even count past 10)
 // when KS <= kMrC; past it the chunk size among 8..kMrC (even) with the least zero padding, the
-// larger on a tie (fewer fragment reloads)
+// larger on a tie (fewer iterations)
 static int mfma_run_ns(int KS) {
     if (KS <= 10) return KS < 4 ? 4 : KS;
     if (KS <= kMrC) return (KS + 1) & ~1;
@@ -1172,20 +1223,26 @@ static hipError_t launch_mfma_run(const void* x, void* y, int64_t rl, int64_t tp
     const mf_i32x4* fr = mfma_frag_table(hq, L, P, ksp, &err);
     if (!fr) return hipErrorOutOfMemory;
     TableHold hold(fr, s);
-    const int64_t nruns = (ntiles + kMrTps - 1) / kMrTps;
+    const bool multi = ksp > ns;
+    const int tps = !multi && ns <= 10 ? 1 : kMrTps;
+    const int64_t nruns = (ntiles + tps - 1) / tps;
     const int64_t want = (nruns + kMfWaves - 1) / kMfWaves;
-    const unsigned blocks = (unsigned)(want < FIR_MR_BLOCKS ? want : FIR_MR_BLOCKS);
+    const int64_t cap = (int64_t)256 * (multi ? FIR_MR_MWAVES : tps == 1 ? 3 : FIR_MR_WAVES);  // one resident round
+    const unsigned blocks = (unsigned)(want < cap ? want : cap);
     const uint32_t tp = (uint32_t)tpr, nt = (uint32_t)ntiles;
     const int mode = fast ? 0 : acc_bits == 32 ? 1 : 2;
     const int shl = mode == 2 ? 32 - acc_bits : 0;
-    auto go = [&](auto nsc, auto multi) {
+    auto go = [&](auto nsc, auto mc) {
         constexpr int NS = decltype(nsc)::value;
-        constexpr bool M = decltype(multi)::value;
-        hipLaunchKernelGGL((fir1d_mfma_run_kernel<STAGE, NS, M>), dim3(blocks), dim3(kBlock), 0, s, (const uint8_t*)x,
-                           (OutT*)y, rl, tp, nt, fr, ksp, P, bias, mode, shl, frac);
+        constexpr bool M = decltype(mc)::value;
+        if constexpr (!M && NS <= 10)
+            hipLaunchKernelGGL((fir1d_mfma_run_kernel<STAGE, NS, M, 1>), dim3(blocks), dim3(kBlock), 0, s,
+                               (const uint8_t*)x, (OutT*)y, rl, tp, nt, fr, ksp, P, bias, mode, shl, frac);
+        else
+            hipLaunchKernelGGL((fir1d_mfma_run_kernel<STAGE, NS, M, kMrTps>), dim3(blocks), dim3(kBlock), 0, s,
+                               (const uint8_t*)x, (OutT*)y, rl, tp, nt, fr, ksp, P, bias, mode, shl, frac);
     };
     using std::integral_constant;
-    const bool multi = ksp > ns;
 #define FIR_MR_NS(n)                                                                       \
     case n:                                                                                \
         if (multi) {                                                                       \
