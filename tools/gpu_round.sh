@@ -99,7 +99,7 @@ for s in $STEPS; do
                  abrun/libfir_hip_met_p256.so abrun/libfir_hip_met_p1024.so abrun/libfir_hip_met_np.so \
                  abrun/libfir_hip_met_npb256t4k.so; fatal $? ;;
         metp2) run metp2 300 python tools/metrics_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so \
-                 abrun/libfir_hip_met_ng2.so abrun/libfir_hip_met_p128.so abrun/libfir_hip_met_npb256t4k.so; fatal $?
+                 abrun/libfir_hip_met_d16.so abrun/libfir_hip_met_d16ng2.so; fatal $?
               run metp3 300 python tools/metrics_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so \
                  abrun/libfir_hip_met_e4.so --no-check; fatal $? ;;
         metexp) run metexp 300 python tools/metrics_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so \

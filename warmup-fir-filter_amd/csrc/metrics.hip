@@ -169,7 +169,10 @@ __device__ void block_counts(Cnt c, Cnt* dst) {
 // a VGPR operand per 8192 samples (2.7 ns; fed by v_readlane instead: 8.7 ns,
 // tools/microbench/chain_micro.hip).  `lds` holds 3 x kChainDepth x 64 doubles; no workgroup
 // barrier inside.
-constexpr int kChainDepth = 8;
+#ifndef FIR_METRIC_CHAIN_D  // block sums per lane of a chain group (a group = 64 x this)
+#define FIR_METRIC_CHAIN_D 8
+#endif
+constexpr int kChainDepth = FIR_METRIC_CHAIN_D;
 #ifndef FIR_METRIC_CHAIN_NG  // groups of block sums chain_follow checks and takes per batch
 #define FIR_METRIC_CHAIN_NG 1
 #endif
