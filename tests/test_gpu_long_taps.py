@@ -249,12 +249,15 @@ def test_table_cache_evicts_only_idle_tables():
             fir_hip.fir1d_fixed_rows(xs, hq, 12, 32, fir_hip.OUT_U8_SAT)
 
 
-@pytest.mark.parametrize("L", [65, 66, 100, 129, 257, 449, 450, 500, 1000, 2048, 4099])
+# every instantiation of fir1d_mfma_run_kernel: one chunk of 4, 5, 6, 7, 8, 9, 10 k-steps (one
+# tile per run), 12, 14, 16 (two tiles); several chunks of 8, 10, 12, 14, 16
+@pytest.mark.parametrize("L", [65, 66, 100, 129, 130, 162, 194, 257, 258, 290, 354, 449, 450, 500, 930, 1000, 2048,
+                               2658, 4099])
 def test_u8_long_filter_run_kernel_vs_oracle(L):
-    """u8 filters past 64 taps (fir1d_mfma_run_kernel: runs of 4 tiles, k-step chunks of 16,
-    LDS-DMA windows): single-chunk and multi-chunk tap counts on both sides of KS = 16, rows
-    whose runs cross row ends (tiles per row not a multiple of 4), one long row, both stages,
-    the no-wrap fast form, 24-bit wrap and 32-bit taps near the int16 byte-split limit."""
+    """u8 filters past 64 taps (fir1d_mfma_run_kernel: runs of 1-2 tiles sharing each chunk of
+    tap fragments, LDS-DMA windows): every chunk length and one- or several-chunk form, rows
+    whose runs cross row ends, one long row, both stages, the no-wrap fast form, 24-bit wrap and
+    32-bit taps near the int16 byte-split limit."""
     rng = np.random.default_rng(L)
     co = c_oracle()
     shapes = [(16, 4096), (5, 5 * 1024 + 8), (1, (1 << 18) + 64)]

@@ -913,6 +913,9 @@ static hipError_t launch_mfma_long(const void* x, void* y, int64_t rl, int64_t t
 #ifndef FIR_MR_EXP                   // timing experiments (wrong results): 1 no MFMAs, 2 no window DMAs
 #define FIR_MR_EXP 0
 #endif
+#ifndef FIR_MR_DEPTH1                // window iterations in flight with one tile per run (u8 out; 12 waves
+#define FIR_MR_DEPTH1 3               // per CU: (DEPTH1 + 1) x 2 KiB of LDS each)
+#endif
 #ifndef FIR_MR_BLOCKS                // grid-stride blocks (4 waves each): one resident round
 #define FIR_MR_BLOCKS (256 * FIR_MR_WAVES)
 #endif
@@ -963,11 +966,11 @@ __global__ __launch_bounds__(kBlock, (mr_waves<TPS_, MULTI>())) void fir1d_mfma_
                                                                    uint32_t bias, int mode, int shl, int frac) {
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     constexpr int TPS = TPS_, C = NS;
-    constexpr int kMrDepth = TPS == 1 ? 3 : ::fir::kMrDepth;
+    constexpr bool OLDS = STAGE == FIR_OUT_I32;
+    constexpr int kMrDepth = TPS == 1 ? (OLDS ? 3 : FIR_MR_DEPTH1) : ::fir::kMrDepth;
     constexpr int WT = kMfTile + 32 * C - 32;  // window samples per tile and chunk
     constexpr int NVT = (WT + 15) / 16;         // 16-sample vectors per tile window
     static_assert(NVT > kWave && NVT <= 2 * kWave && 16 * 2 * kWave <= kMrTileLds, "two DMAs per tile window");
-    constexpr bool OLDS = STAGE == FIR_OUT_I32;
     constexpr int BUF = TPS * kMrTileLds;
     constexpr int NBUF = kMrDepth + 1;          // LDS window buffers per wave (a ring)
     constexpr int NDMA = 2 * TPS;               // DMA instructions per iteration
