@@ -169,6 +169,9 @@ __device__ void block_counts(Cnt c, Cnt* dst) {
 // a VGPR operand per 8192 samples (2.7 ns; fed by v_readlane instead: 8.7 ns,
 // tools/microbench/chain_micro.hip).  `lds` holds 3 x kChainDepth x 64 doubles; no workgroup
 // barrier inside.
+#ifndef FIR_METRIC_ONEPOLL
+#define FIR_METRIC_ONEPOLL 1
+#endif
 #ifndef FIR_METRIC_CHAIN_D  // block sums per lane of a chain group (a group = 64 x this)
 #define FIR_METRIC_CHAIN_D 8
 #endif
@@ -323,9 +326,24 @@ __device__ __forceinline__ void chain_follow(const double* __restrict__ bsum, in
         }
         return k;
     };
+    // FIR_METRIC_ONEPOLL: only wave 0 polls the progress words and posts how many groups are
+    // complete in an LDS word that waves 1-2 watch (one third of the polling atomics)
+    int* posted = reinterpret_cast<int*>(lds + kChainLds);  // (past the three staging areas)
+    if (FIR_METRIC_ONEPOLL && wv == 0 && lane == 0) __hip_atomic_store(posted, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __builtin_amdgcn_s_barrier();  // (waves 0-2 only reach here; wave 3 returned: s_barrier counts waves alive)
     for (int64_t g = 0; g < ngr && ok;) {
         int k = 0;
-        for (uint32_t spins = 0; (k = ready_prefix(g)) == 0;) {
+        for (uint32_t spins = 0;;) {
+            if (!FIR_METRIC_ONEPOLL || wv == 0) {
+                k = ready_prefix(g);
+                if (FIR_METRIC_ONEPOLL && k > 0 && lane == 0)
+                    __hip_atomic_store(posted, (int)(g + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+                const int p = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                k = p > g ? (int)min<int64_t>(p - g, NG) : 0;
+            }
+            if (k > 0) break;
             if (++spins > kChainSpinCap) {
                 ok = false;
                 break;
