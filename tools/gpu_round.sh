@@ -77,6 +77,8 @@ for s in $STEPS; do
                  --warmup 2 --cpu-seconds 0 --no-parity --roofline-launches 5 --roofline-ramp 0; fatal $? ;;
         dist2prof_serial|dist2prof_overlap) m=${s#dist2prof_}
              run "dist2prof_$m" 300 tools/dist2_prof.sh "$OUT/dist2prof_$m" "$m"; fatal $? ;;
+        banknc) run banknc 200 python tools/lib_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so \
+                     abrun/libfir_hip_sk0.so 10 bank; fatal $? ;;
         bankab) for v in u2 xcd persist u2xcd; do
                  run "bankab_$v" 200 python tools/lib_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so \
                      abrun/libfir_hip_bank_$v.so 10 bank; fatal $? || exit

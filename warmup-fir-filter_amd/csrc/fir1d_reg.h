@@ -90,7 +90,26 @@ struct TapsN {
     uint32_t hb[F][L];
     uint32_t pkbias[F], pkshift[F], pkmax;
     uint32_t pkmode[F];  // 0: v_dot2 form, 1: packed-16 unsigned V, 2: packed-16 signed V
+    // v_dot2 form, u8 stage: 1 when 2^(frac-1) + sum h x lies in [0, 256 * 2^frac) for every u8
+    // x, so the stage is the shift alone (the moving average of the report's bank: no v_med3)
+    uint32_t noclamp[F];
 };
+
+#ifndef FIR_REG_SKIP0  // 1: packed-16 filters skip their zero taps (A/B builds: make abreg)
+#define FIR_REG_SKIP0 1
+#endif
+#ifndef FIR_REG_NOCLAMP  // 0: always clamp (A/B builds: make abreg)
+#define FIR_REG_NOCLAMP 1
+#endif
+// noclamp[] for the u8 stage of the no-wrap v_dot2 form (host)
+template <int L, int F>
+inline void plan_u8_noclamp(TapsN<L, F>& t, int frac) {
+    for (int f = 0; f < F; ++f) {
+        int64_t vmin = frac >= 1 && frac <= 22 ? (int64_t)1 << (frac - 1) : -1, vmax = vmin;
+        for (int k = 0; k < L; ++k) (t.h[f][k] > 0 ? vmax : vmin) += 255 * (int64_t)t.h[f][k];
+        t.noclamp[f] = FIR_REG_NOCLAMP && vmin >= 0 && vmax < ((int64_t)256 << frac) ? 1u : 0u;
+    }
+}
 
 // Packed-16 planning for the u8 stage (host).  Per filter: s = the largest power of two
 // common to its taps (s <= frac - 1, frac - s <= 15), h' = h / 2^s, and the range of
@@ -361,8 +380,9 @@ __device__ __forceinline__ void u8_pk16_vec(const uint32_t* P, const uint32_t* h
     for (int q = 0; q < VEC / 2; ++q) a[q] = pk_mad16(P[2 * q], hb[0], bias);
 #pragma unroll
     for (int i = 1; i < L; ++i)
+        if (!FIR_REG_SKIP0 || hb[i] != 0u)  // wave-uniform: a zero tap (the bank's edge filter) costs nothing
 #pragma unroll
-        for (int q = 0; q < VEC / 2; ++q) a[q] = pk_mad16(P[2 * q + i], hb[i], a[q]);
+            for (int q = 0; q < VEC / 2; ++q) a[q] = pk_mad16(P[2 * q + i], hb[i], a[q]);
 #pragma unroll
     for (int d = 0; d < VEC / 4; ++d) {
         if constexpr ((FLAGS & kU8PkHi8) != 0) {
@@ -379,14 +399,18 @@ __device__ __forceinline__ void u8_pk16_vec(const uint32_t* P, const uint32_t* h
 
 // No-wrap u8 form: every chain starts at the rounding bias (a VGPR), the u8 stage is
 // v_med3 clamp then shift (sat_u8_pixel), the int32 stage one arithmetic shift.
-template <int NDL, int NW, int L, int J, int VEC, int STAGE>
+// NC: the filter's u8 stage needs no clamp (TapsN::noclamp): the shift alone.
+template <int NDL, int NW, int L, int J, int VEC, int STAGE, bool NC = false>
 struct U8Dot2Vec {
     __device__ static __forceinline__ void run(const uint32_t* Wd, const uint32_t* pk, uint32_t bias, int frac,
                                                int32_t sat_hi, int32_t* q) {
         if constexpr (J < VEC) {
             const uint32_t acc = U8Dot2Row<NDL, NW, L, J, 0>::run(Wd, pk, bias);
-            q[J] = STAGE == FIR_OUT_U8_SAT ? (int32_t)sat_u8_pixel<true>(acc, 0, frac, sat_hi) : (int32_t)acc >> frac;
-            U8Dot2Vec<NDL, NW, L, J + 1, VEC, STAGE>::run(Wd, pk, bias, frac, sat_hi, q);
+            if constexpr (NC)
+                q[J] = (int32_t)(acc >> frac);  // acc in [0, 256 << frac)
+            else
+                q[J] = STAGE == FIR_OUT_U8_SAT ? (int32_t)sat_u8_pixel<true>(acc, 0, frac, sat_hi) : (int32_t)acc >> frac;
+            U8Dot2Vec<NDL, NW, L, J + 1, VEC, STAGE, NC>::run(Wd, pk, bias, frac, sat_hi, q);
         }
     }
 };
@@ -576,7 +600,10 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
                         if constexpr (DOT2) {
                             Dot2Vec<NDL, NW, L, 0, VEC, ACC32>::run(Wd, taps.pk[f], shl, frac, q);
                         } else if constexpr (U8DOT2) {
-                            U8Dot2Vec<NDL, NW, L, 0, VEC, STAGE>::run(Wd, taps.pk[f], bias, frac, sat_hi, q);
+                            if (STAGE == FIR_OUT_U8_SAT && taps.noclamp[f])  // wave-uniform
+                                U8Dot2Vec<NDL, NW, L, 0, VEC, STAGE, true>::run(Wd, taps.pk[f], bias, frac, sat_hi, q);
+                            else
+                                U8Dot2Vec<NDL, NW, L, 0, VEC, STAGE>::run(Wd, taps.pk[f], bias, frac, sat_hi, q);
                         } else {
                             fir_vector_interior<InT, L, CH, ACC32>(w, taps.h[f], shl, frac, q);
                         }

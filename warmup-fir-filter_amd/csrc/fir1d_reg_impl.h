@@ -49,6 +49,7 @@ static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t
     for (int f = 0; f < F; ++f)
         for (int k = 0; k < L; ++k) t.h[f][k] = hq[f * L + k];
     pack_taps(t);
+    plan_u8_noclamp(t, frac);
     if constexpr ((FL & kU8Pk16) != 0)
         if (!(plan_u8_pk16(t, frac) & kU8Pk16)) return hipErrorInvalidValue;  // caller checked
     int64_t ntiles = 0, blocks = 0;
