@@ -913,6 +913,15 @@ static hipError_t launch_mfma_long(const void* x, void* y, int64_t rl, int64_t t
 #ifndef FIR_MR_EXP                   // timing experiments (wrong results): 1 no MFMAs, 2 no window DMAs
 #define FIR_MR_EXP 0
 #endif
+#ifndef FIR_MR_W4_NS                 // one-tile runs of up to this many k-steps: 4 waves per SIMD
+#define FIR_MR_W4_NS 6
+#endif
+#ifndef FIR_MR_BIASV                 // 1: bias folded into the first MFMA (below 4 waves per SIMD)
+#define FIR_MR_BIASV 1
+#endif
+#ifndef FIR_MR_CURSOR                // 1: incremental tile geometry for one-tile one-chunk runs
+#define FIR_MR_CURSOR 1
+#endif
 #ifndef FIR_MR_DEPTH1                // window iterations in flight with one tile per run (u8 out; 12 waves
 #define FIR_MR_DEPTH1 3               // per CU: (DEPTH1 + 1) x 2 KiB of LDS each)
 #endif
@@ -956,10 +965,12 @@ constexpr int kMrTileLds = 2048;     // LDS bytes per tile window (128 vectors o
 #ifndef FIR_MR_ADBL
 #define FIR_MR_ADBL 0
 #endif
-template <int TPS_, bool MULTI>
-constexpr int mr_waves() { return MULTI ? FIR_MR_MWAVES : TPS_ == 1 ? 3 : FIR_MR_WAVES; }
+template <int STAGE, int TPS_, bool MULTI, int NS>
+constexpr int mr_waves() {
+    return MULTI ? FIR_MR_MWAVES : TPS_ == 1 ? (NS <= FIR_MR_W4_NS && STAGE == FIR_OUT_U8_SAT ? 4 : 3) : FIR_MR_WAVES;
+}
 template <int STAGE, int NS, bool MULTI, int TPS_>
-__global__ __launch_bounds__(kBlock, (mr_waves<TPS_, MULTI>())) void fir1d_mfma_run_kernel(const uint8_t* __restrict__ x,
+__global__ __launch_bounds__(kBlock, (mr_waves<STAGE, TPS_, MULTI, NS>())) void fir1d_mfma_run_kernel(const uint8_t* __restrict__ x,
                                                                    typename OutTraits<STAGE>::T* __restrict__ y,
                                                                    int64_t rowlen, uint32_t tiles_per_row, uint32_t ntiles,
                                                                    const mf_i32x4* __restrict__ frag, int KS, int P,
@@ -1000,6 +1011,42 @@ __global__ __launch_bounds__(kBlock, (mr_waves<TPS_, MULTI>())) void fir1d_mfma_
 #pragma unroll
         for (int s = 0; s < C; ++s) lo[s] = f[(2 * s) * kWave], hi[s] = f[(2 * s + 1) * kWave];
     };
+    // One tile per run and one chunk (the wave's tiles t, t + S, t + 2S, ...): the tile's row and
+    // column advance by constant steps (one division at the start instead of one per tile and use,
+    // ~40 of the loop's ~114 SALU per tile).  Past the last tile the cursor runs on; those tiles'
+    // descriptors have size 0.
+    constexpr bool CUR = TPS == 1 && !MULTI && FIR_MR_CURSOR;
+    // the bias as the first MFMA's accumulator input (16 VGPRs) or one add per output
+    constexpr bool BIASV = FIR_MR_BIASV && mr_waves<STAGE, TPS_, MULTI, NS>() < 4;
+    constexpr int BPD = mr_waves<STAGE, TPS_, MULTI, NS>() < 4 ? kMrBpd : 2;  // B reads ahead (registers)
+    struct Cursor {
+        uint32_t row, col;
+        int64_t rs;
+    };
+    const uint32_t tpr = tiles_per_row, dr = stride / tpr, dc = stride - dr * tpr;
+    const int64_t drs = (int64_t)dr * rowlen;
+    auto cur_at = [&](uint32_t t) __attribute__((always_inline)) {
+        Cursor k;
+        k.row = __builtin_amdgcn_readfirstlane(t / tpr);
+        k.col = __builtin_amdgcn_readfirstlane(t - k.row * tpr);
+        k.rs = (int64_t)k.row * rowlen;
+        return k;
+    };
+    auto cur_step = [&](Cursor& k) __attribute__((always_inline)) {
+        k.col += dc, k.row += dr, k.rs += drs;
+        if (k.col >= tpr) k.col -= tpr, ++k.row, k.rs += rowlen;
+    };
+    auto tile_of = [&](uint32_t t, const Cursor& k) __attribute__((always_inline)) {
+        if constexpr (CUR) {
+            MfTile tl;
+            tl.rs = k.rs, tl.re = k.rs + rowlen, tl.ts = k.rs + (int64_t)k.col * kMfTile;
+            return tl;
+        } else {
+            return mf_tile(t < ntiles ? t : ntiles - 1, rowlen, tiles_per_row);
+        }
+    };
+    Cursor acur{}, rcur{};
+    if constexpr (CUR) acur = cur_at(rn), rcur = acur;
     // the run's TPS tile windows of chunk c into LDS buffer `buf`: per tile two 1 KiB DMAs
     // (vectors lane and lane + 64; the second past the window's NVT vectors reads zeros)
     auto issue_win = [&](uint32_t run, int c, int buf) __attribute__((always_inline)) {
@@ -1007,7 +1054,7 @@ __global__ __launch_bounds__(kBlock, (mr_waves<TPS_, MULTI>())) void fir1d_mfma_
 #pragma unroll
         for (int q = 0; q < TPS; ++q) {
             const uint32_t t = run < nruns ? run * TPS + q : ntiles;
-            const MfTile tl = mf_tile(t < ntiles ? t : ntiles - 1, rowlen, tiles_per_row);
+            const MfTile tl = tile_of(t, acur);
             const int64_t w0 = tl.ts - P + 32 * (int64_t)C * c;
             const int64_t base = w0 > tl.rs ? w0 : tl.rs, end = tl.re < w0 + WT ? tl.re : w0 + WT;
             const __amdgpu_buffer_rsrc_t rd = mf_rsrc(x + base, (uint32_t)(end > base && t < ntiles ? end - base : 0));
@@ -1039,10 +1086,14 @@ __global__ __launch_bounds__(kBlock, (mr_waves<TPS_, MULTI>())) void fir1d_mfma_
     int c = 0, buf = 0;
     uint32_t ar = rn;
     int ac = 0;
+    auto advance_ahead = [&]() __attribute__((always_inline)) {
+        advance(ar, ac);
+        if constexpr (CUR) cur_step(acur);
+    };
 #pragma unroll
     for (int d = 0; d < kMrDepth; ++d) {
         issue_win(ar, ac, d);
-        advance(ar, ac);
+        advance_ahead();
         if constexpr (!MULTI) {  // stand-ins for the stores of the iterations before the first (a
             const __amdgpu_buffer_rsrc_t none = mf_rsrc(y, 0u);  // zero-size range: nothing written),
 #pragma unroll                                                   // so the counted wait below is exact
@@ -1060,7 +1111,7 @@ __global__ __launch_bounds__(kBlock, (mr_waves<TPS_, MULTI>())) void fir1d_mfma_
         if constexpr (ADBL) load_a(an_lo, an_hi, nc);  // (past the last run: a valid chunk, unused)
         else if constexpr (MULTI) load_a(a_lo, a_hi, c);  // issued before the next windows: its wait leaves them in flight
         issue_win(ar, ac, buf == 0 ? NBUF - 1 : buf - 1);  // the buffer computed last iteration
-        advance(ar, ac);
+        advance_ahead();
         // this iteration's windows (and A) landed; the younger operations stay in flight.  vmcnt
         // also counts stores, in order with the loads.  One chunk: every iteration ends with its
         // NST stores, so kMrDepth iterations of DMAs + stores may stay outstanding (counting only
@@ -1104,17 +1155,17 @@ __global__ __launch_bounds__(kBlock, (mr_waves<TPS_, MULTI>())) void fir1d_mfma_
             for (int q = 0; q < TPS; ++q)
                 bq[sl][q] = *reinterpret_cast<const mf_i32x4*>(&pl[q * kMrTileLds + 32 * r + 32 * sl + 16 * hf]);
         };
-        static_for<0, (kMrBpd < C ? kMrBpd : C)>([&](auto slc) { rd_b(slc); });
+        static_for<0, (BPD < C ? BPD : C)>([&](auto slc) { rd_b(slc); });
         static_for<0, C>([&](auto slc) {
             constexpr int sl = decltype(slc)::value;
-            if constexpr (sl + kMrBpd < C) rd_b(std::integral_constant<int, sl + kMrBpd>{});
+            if constexpr (sl + BPD < C) rd_b(std::integral_constant<int, sl + BPD>{});
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (FIR_MR_EXP != 1) {  // (FIR_MR_EXP: timing experiments only)
 #pragma unroll
                 for (int q = 0; q < TPS; ++q) {
                     const mf_i32x4 b = XLDS ? bq[sl][q] : bq[sl][q] ^ (int)0x80808080;
                     if constexpr (!MULTI && sl == 0) {  // a run's first k-step: the bias, and zero
-                        acc_ll[q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_lo[sl], b, biasv, 0, 0, 0);
+                        acc_ll[q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_lo[sl], b, BIASV ? biasv : mf_i32x16{}, 0, 0, 0);
                         acc_mid[q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_hi[sl], b, mf_i32x16{}, 0, 0, 0);
                     } else {
                         acc_ll[q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_lo[sl], b, acc_ll[q], 0, 0, 0);
@@ -1128,13 +1179,13 @@ __global__ __launch_bounds__(kBlock, (mr_waves<TPS_, MULTI>())) void fir1d_mfma_
 #pragma unroll
             for (int q = 0; q < TPS; ++q) {
                 const uint32_t t = rn * TPS + q;
-                const MfTile tl = mf_tile(t < ntiles ? t : ntiles - 1, rowlen, tiles_per_row);
+                const MfTile tl = tile_of(t, rcur);
                 const int m = t < ntiles ? (int)min((int64_t)kMfTile, tl.re - tl.ts) : 0;
                 int32_t o[16];
                 uint32_t a[16];
 #pragma unroll
                 for (int i = 0; i < 16; ++i)  // (one chunk: the bias started acc_ll)
-                    a[i] = ((uint32_t)acc_mid[q][i] << 8) + (uint32_t)acc_ll[q][i] + (MULTI ? bias : 0u);
+                    a[i] = ((uint32_t)acc_mid[q][i] << 8) + (uint32_t)acc_ll[q][i] + (MULTI || !BIASV ? bias : 0u);
                 if (mode == 0) {
 #pragma unroll
                     for (int i = 0; i < 16; ++i)
@@ -1187,6 +1238,7 @@ __global__ __launch_bounds__(kBlock, (mr_waves<TPS_, MULTI>())) void fir1d_mfma_
         stored = c == nch - 1;
         if (nr >= nruns) return false;
         rn = nr, c = nc, buf = buf + 1 == NBUF ? 0 : buf + 1;
+        if constexpr (CUR) cur_step(rcur);
         __builtin_amdgcn_wave_barrier();  // this iteration's B reads are done before its buffer is refilled
         asm volatile("" ::: "memory");
         return true;
@@ -1230,7 +1282,8 @@ static hipError_t launch_mfma_run(const void* x, void* y, int64_t rl, int64_t tp
     const int tps = !multi && ns <= 10 ? 1 : kMrTps;
     const int64_t nruns = (ntiles + tps - 1) / tps;
     const int64_t want = (nruns + kMfWaves - 1) / kMfWaves;
-    const int64_t cap = (int64_t)256 * (multi ? FIR_MR_MWAVES : tps == 1 ? 3 : FIR_MR_WAVES);  // one resident round
+    const int64_t cap =
+        (int64_t)256 * (multi ? FIR_MR_MWAVES : tps == 1 ? (ns <= FIR_MR_W4_NS && STAGE == FIR_OUT_U8_SAT ? 4 : 3) : FIR_MR_WAVES);
     const unsigned blocks = (unsigned)(want < cap ? want : cap);
     const uint32_t tp = (uint32_t)tpr, nt = (uint32_t)ntiles;
     const int mode = fast ? 0 : acc_bits == 32 ? 1 : 2;
