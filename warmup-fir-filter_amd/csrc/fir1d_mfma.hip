@@ -919,6 +919,15 @@ static hipError_t launch_mfma_long(const void* x, void* y, int64_t rl, int64_t t
 #ifndef FIR_MR_BIASV                 // 1: bias folded into the first MFMA (below 4 waves per SIMD)
 #define FIR_MR_BIASV 1
 #endif
+#ifndef FIR_MR_MTPS                  // tiles per run with several chunks (u8 stage)
+#define FIR_MR_MTPS 4
+#endif
+#ifndef FIR_MR_MNS_MIN               // shortest chunk considered with 4-tile runs
+#define FIR_MR_MNS_MIN 6
+#endif
+#ifndef FIR_MR_MDEPTH                // window iterations in flight with 4-tile runs (LDS: 2 WGs per CU)
+#define FIR_MR_MDEPTH 1
+#endif
 #ifndef FIR_MR_CURSOR                // 1: incremental tile geometry for one-tile one-chunk runs
 #define FIR_MR_CURSOR 1
 #endif
@@ -978,7 +987,7 @@ __global__ __launch_bounds__(kBlock, (mr_waves<STAGE, TPS_, MULTI, NS>())) void 
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     constexpr int TPS = TPS_, C = NS;
     constexpr bool OLDS = STAGE == FIR_OUT_I32;
-    constexpr int kMrDepth = TPS == 1 ? (OLDS ? 3 : FIR_MR_DEPTH1) : ::fir::kMrDepth;
+    constexpr int kMrDepth = TPS == 1 ? (OLDS ? 3 : FIR_MR_DEPTH1) : TPS == 4 ? FIR_MR_MDEPTH : ::fir::kMrDepth;
     constexpr int WT = kMfTile + 32 * C - 32;  // window samples per tile and chunk
     constexpr int NVT = (WT + 15) / 16;         // 16-sample vectors per tile window
     static_assert(NVT > kWave && NVT <= 2 * kWave && 16 * 2 * kWave <= kMrTileLds, "two DMAs per tile window");
@@ -1018,7 +1027,7 @@ __global__ __launch_bounds__(kBlock, (mr_waves<STAGE, TPS_, MULTI, NS>())) void 
     constexpr bool CUR = TPS == 1 && !MULTI && FIR_MR_CURSOR;
     // the bias as the first MFMA's accumulator input (16 VGPRs) or one add per output
     constexpr bool BIASV = FIR_MR_BIASV && mr_waves<STAGE, TPS_, MULTI, NS>() < 4;
-    constexpr int BPD = mr_waves<STAGE, TPS_, MULTI, NS>() < 4 ? kMrBpd : 2;  // B reads ahead (registers)
+    constexpr int BPD = TPS == 4 ? 1 : mr_waves<STAGE, TPS_, MULTI, NS>() < 4 ? kMrBpd : 2;  // B reads ahead (registers)
     struct Cursor {
         uint32_t row, col;
         int64_t rs;
@@ -1257,11 +1266,11 @@ __global__ __launch_bounds__(kBlock, (mr_waves<STAGE, TPS_, MULTI, NS>())) void 
 // k-steps per chunk for KS k-steps: one chunk of exactly KS (rounded up to an even count past 10)
 // when KS <= kMrC; past it the chunk size among 8..kMrC (even) with the least zero padding, the
 // larger on a tie (fewer iterations)
-static int mfma_run_ns(int KS) {
+static int mfma_run_ns(int KS, int multi_max) {
     if (KS <= 10) return KS < 4 ? 4 : KS;
     if (KS <= kMrC) return (KS + 1) & ~1;
-    int best = kMrC, pad = (KS + kMrC - 1) / kMrC * kMrC;
-    for (int ns = kMrC - 2; ns >= 8; ns -= 2) {
+    int best = multi_max, pad = (KS + multi_max - 1) / multi_max * multi_max;
+    for (int ns = multi_max - 2; ns >= (multi_max <= 8 ? FIR_MR_MNS_MIN : 8); ns -= 2) {
         const int p = (KS + ns - 1) / ns * ns;
         if (p < pad) best = ns, pad = p;
     }
@@ -1273,13 +1282,17 @@ static hipError_t launch_mfma_run(const void* x, void* y, int64_t rl, int64_t tp
                                   int L, int P, int KS, uint32_t bias, bool fast, int frac, int acc_bits, hipStream_t s) {
     using OutT = typename OutTraits<STAGE>::T;
     std::string err;
-    const int ns = mfma_run_ns(KS);
+    // several chunks, u8 stage: runs of FIR_MR_MTPS tiles (4: each chunk's fragments, loaded once
+    // per iteration from L2, feed 4 tiles, so their latency is paid per 4 tiles), chunks of <= 8
+    // k-steps (the accumulators of 4 tiles and one fragment set fit two waves per SIMD)
+    constexpr int MTPS = STAGE == FIR_OUT_U8_SAT ? FIR_MR_MTPS : kMrTps;
+    const int ns = mfma_run_ns(KS, MTPS == 4 ? 8 : kMrC);
     const int ksp = (KS + ns - 1) / ns * ns;  // the table padded to whole chunks (zero fragments)
     const mf_i32x4* fr = mfma_frag_table(hq, L, P, ksp, &err);
     if (!fr) return hipErrorOutOfMemory;
     TableHold hold(fr, s);
     const bool multi = ksp > ns;
-    const int tps = !multi && ns <= 10 ? 1 : kMrTps;
+    const int tps = !multi && ns <= 10 ? 1 : multi ? MTPS : kMrTps;
     const int64_t nruns = (ntiles + tps - 1) / tps;
     const int64_t want = (nruns + kMfWaves - 1) / kMfWaves;
     const int64_t cap =
@@ -1294,6 +1307,9 @@ static hipError_t launch_mfma_run(const void* x, void* y, int64_t rl, int64_t tp
         if constexpr (!M && NS <= 10)
             hipLaunchKernelGGL((fir1d_mfma_run_kernel<STAGE, NS, M, 1>), dim3(blocks), dim3(kBlock), 0, s,
                                (const uint8_t*)x, (OutT*)y, rl, tp, nt, fr, ksp, P, bias, mode, shl, frac);
+        else if constexpr (M && MTPS == 4)
+            hipLaunchKernelGGL((fir1d_mfma_run_kernel<STAGE, NS, M, 4>), dim3(blocks), dim3(kBlock), 0, s,
+                               (const uint8_t*)x, (OutT*)y, rl, tp, nt, fr, ksp, P, bias, mode, shl, frac);
         else
             hipLaunchKernelGGL((fir1d_mfma_run_kernel<STAGE, NS, M, kMrTps>), dim3(blocks), dim3(kBlock), 0, s,
                                (const uint8_t*)x, (OutT*)y, rl, tp, nt, fr, ksp, P, bias, mode, shl, frac);
@@ -1302,7 +1318,8 @@ static hipError_t launch_mfma_run(const void* x, void* y, int64_t rl, int64_t tp
 #define FIR_MR_NS(n)                                                                       \
     case n:                                                                                \
         if (multi) {                                                                       \
-            if constexpr (n >= 8 && n % 2 == 0) go(integral_constant<int, n>{}, std::true_type{}); \
+            if constexpr (MTPS == 4 ? (n == 6 || n == 8) : n >= 8 && n % 2 == 0)                  \
+                go(integral_constant<int, n>{}, std::true_type{});                         \
         } else {                                                                           \
             go(integral_constant<int, n>{}, std::false_type{});                            \
         }                                                                                  \
