@@ -98,7 +98,7 @@ for s in $STEPS; do
         lth) run long_taps_head 400 python tools/long_taps_ab.py 66,128,257,450,500,1000,2048,4099 \
                  warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_head.so; fatal $? ;;
         ltd) run long_taps_d 400 python tools/long_taps_ab.py 257,450,500,700,1000,2048,4099 \
-                 warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_lt_ns8.so abrun/libfir_hip_lt_mt2.so; fatal $? ;;
+                 warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_lt_roll0.so abrun/libfir_hip_lt_mt2.so; fatal $? ;;
         metp) run metp 300 python tools/metrics_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so \
                  abrun/libfir_hip_met_p256.so abrun/libfir_hip_met_p1024.so abrun/libfir_hip_met_np.so \
                  abrun/libfir_hip_met_npb256t4k.so; fatal $? ;;

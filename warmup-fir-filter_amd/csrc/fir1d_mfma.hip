@@ -922,6 +922,10 @@ static hipError_t launch_mfma_long(const void* x, void* y, int64_t rl, int64_t t
 #ifndef FIR_MR_MTPS                  // tiles per run with several chunks (u8 stage)
 #define FIR_MR_MTPS 4
 #endif
+#ifndef FIR_MR_ROLL                  // 1: next chunk's fragments loaded step by step behind the MFMAs
+                                     // (A/B: 4099 taps 2091 vs 2020 us, profiles/r04/long_taps_run_v3_ab.txt)
+#define FIR_MR_ROLL 0
+#endif
 #ifndef FIR_MR_MNS_MIN               // shortest chunk considered with 4-tile runs
 #define FIR_MR_MNS_MIN 6
 #endif
@@ -1109,7 +1113,11 @@ __global__ __launch_bounds__(kBlock, (mr_waves<STAGE, TPS_, MULTI, NS>())) void 
             for (int k = 0; k < NST; ++k) __builtin_amdgcn_raw_buffer_store_b32(0, none, 0, 0, 0);
         }
     }
-    if constexpr (ADBL) load_a(a0_lo, a0_hi, 0);  // behind the first windows (the first wait below)
+    // ROLL (several chunks, one fragment set): each k-step's fragments for the NEXT iteration are
+    // loaded right after that step's MFMAs issue, so they land during this iteration's remaining
+    // MFMAs instead of being waited for at the top of the next one
+    constexpr bool ROLL = MULTI && !ADBL && FIR_MR_ROLL;
+    if constexpr (ADBL || ROLL) load_a(a0_lo, a0_hi, 0);  // behind the first windows (the first wait below)
     bool first = true, stored = false;
     // one iteration (run rn, chunk c) on fragments acur, loading anext for the next one; false at the end
     auto body = [&](mf_i32x4 (&a_lo)[C], mf_i32x4 (&a_hi)[C], mf_i32x4 (&an_lo)[C], mf_i32x4 (&an_hi)[C])
@@ -1118,7 +1126,7 @@ __global__ __launch_bounds__(kBlock, (mr_waves<STAGE, TPS_, MULTI, NS>())) void 
         int nc = c;
         advance(nr, nc);
         if constexpr (ADBL) load_a(an_lo, an_hi, nc);  // (past the last run: a valid chunk, unused)
-        else if constexpr (MULTI) load_a(a_lo, a_hi, c);  // issued before the next windows: its wait leaves them in flight
+        else if constexpr (MULTI && !ROLL) load_a(a_lo, a_hi, c);  // issued before the next windows: its wait leaves them in flight
         issue_win(ar, ac, buf == 0 ? NBUF - 1 : buf - 1);  // the buffer computed last iteration
         advance_ahead();
         // this iteration's windows (and A) landed; the younger operations stay in flight.  vmcnt
@@ -1181,6 +1189,10 @@ __global__ __launch_bounds__(kBlock, (mr_waves<STAGE, TPS_, MULTI, NS>())) void 
                         acc_mid[q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_hi[sl], b, acc_mid[q], 0, 0, 0);
                     }
                 }
+            }
+            if constexpr (ROLL) {  // step sl's fragments of the next iteration's chunk (nc)
+                const mf_i32x4* fn = frag + (int64_t)nc * C * 2 * kWave + lane;
+                a_lo[sl] = fn[(2 * sl) * kWave], a_hi[sl] = fn[(2 * sl + 1) * kWave];
             }
             __builtin_amdgcn_sched_barrier(0);
         });
