@@ -494,3 +494,19 @@ def test_host_entry_chunked_overlap(shape, dtype, channels, taps):
         buf = x.copy()
         fir_hip.fir1d_fixed_rows(buf, hq, channels=channels, out=buf)
         assert np.array_equal(buf, ref)
+
+
+@pytest.mark.parametrize("c", [1365, 1366, 1370, 1371, 4095])
+def test_bank_noclamp_stage_boundary(c):
+    """A v_dot2-form filter whose biased sum provably stays in [0, 256 * 2^frac) runs its u8 stage
+    as a shift alone (fir1d_reg.h plan_u8_noclamp): moving averages c * [1, 1, 1] on both sides of
+    that bound (3 * 255 * c + 2048 < 2^20 holds up to c = 1368), on all-zero, all-255 and random
+    u8 rows, beside packed-16 filters in one bank, against the C oracle bit for bit."""
+    co = c_oracle()
+    rng = np.random.default_rng(c)
+    hq = np.array([[c] * 3, [1024, 2048, 1024], [-4096, 0, 4096], [-512, 5120, -512]])
+    for x in (np.zeros((8, 4096), np.uint8), np.full((8, 4096), 255, np.uint8),
+              rng.integers(0, 256, (8, 4096), dtype=np.uint8), rng.integers(250, 256, (8, 4096), dtype=np.uint8)):
+        ys = fir_hip.fir1d_fixed_rows_multi(x, hq, 12, 32, fir_hip.OUT_U8_SAT)
+        for f in range(4):
+            assert np.array_equal(ys[f], co.fir1d_rows(x, hq[f], 12, 32, fir_hip.OUT_U8_SAT)), (c, f)
