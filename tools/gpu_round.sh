@@ -97,8 +97,8 @@ for s in $STEPS; do
                  warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_lt_e2.so --no-check; fatal $? ;;
         lth) run long_taps_head 400 python tools/long_taps_ab.py 66,128,257,450,500,1000,2048,4099 \
                  warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_head.so; fatal $? ;;
-        ltd) run long_taps_d 400 python tools/long_taps_ab.py 257,450,500,700,1000,2048,4099 \
-                 warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_lt_roll0.so abrun/libfir_hip_lt_mt2.so; fatal $? ;;
+        ltd) run long_taps_d 400 python tools/long_taps_ab.py 66,128,162,200,257,500,1000,4099 \
+                 warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_lt_x6.so abrun/libfir_hip_lt_x4.so; fatal $? ;;
         metp) run metp 300 python tools/metrics_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so \
                  abrun/libfir_hip_met_p256.so abrun/libfir_hip_met_p1024.so abrun/libfir_hip_met_np.so \
                  abrun/libfir_hip_met_npb256t4k.so; fatal $? ;;
