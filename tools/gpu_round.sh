@@ -103,7 +103,7 @@ for s in $STEPS; do
                  abrun/libfir_hip_met_p256.so abrun/libfir_hip_met_p1024.so abrun/libfir_hip_met_np.so \
                  abrun/libfir_hip_met_npb256t4k.so; fatal $? ;;
         metp2) run metp2 300 python tools/metrics_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so \
-                 abrun/libfir_hip_met_op0.so; fatal $? ;;
+                 abrun/libfir_hip_prevmet.so; fatal $? ;;
         metexp) run metexp 300 python tools/metrics_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so \
                  abrun/libfir_hip_met_e1.so abrun/libfir_hip_met_e2.so abrun/libfir_hip_met_e3.so \
                  abrun/libfir_hip_met_b256t4k.so --no-check; fatal $? ;;

@@ -291,8 +291,6 @@ __device__ __forceinline__ double coherent_read(const double* p) {
 __device__ __forceinline__ void chain_follow(const double* __restrict__ bsum, int64_t nb, int64_t nbf, uint32_t* prog,
                                              int64_t nw, double* state, uint8_t* lds) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
-    if (wv >= 3) return;
-    __builtin_amdgcn_s_setprio(3);
     const double* src = bsum + (int64_t)wv * nb;
     double* sh = reinterpret_cast<double*>(lds) + wv * kChainDepth * kWave;
     constexpr int D = kChainDepth, NG = kChainGroups, GS = kChainGS;
@@ -330,7 +328,9 @@ __device__ __forceinline__ void chain_follow(const double* __restrict__ bsum, in
     // complete in an LDS word that waves 1-2 watch (one third of the polling atomics)
     int* posted = reinterpret_cast<int*>(lds + kChainLds);  // (past the three staging areas)
     if (FIR_METRIC_ONEPOLL && wv == 0 && lane == 0) __hip_atomic_store(posted, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __builtin_amdgcn_s_barrier();  // (waves 0-2 only reach here; wave 3 returned: s_barrier counts waves alive)
+    __builtin_amdgcn_s_barrier();  // (every wave of the workgroup: the word is zero before anyone reads it)
+    if (wv >= 3) return;
+    __builtin_amdgcn_s_setprio(3);
     for (int64_t g = 0; g < ngr && ok;) {
         int k = 0;
         for (uint32_t spins = 0;;) {
@@ -375,7 +375,10 @@ __device__ __forceinline__ void chain_follow(const double* __restrict__ bsum, in
         g += k;
     }
     for (int64_t b = nbf; b < nb; ++b) s = __dadd_rn(s, coherent_read(src + b));
-    if (lane == 0) state[wv] = ok ? s : __builtin_nan("");
+    if (lane == 0) {
+        state[wv] = ok ? s : __builtin_nan("");
+        reinterpret_cast<double*>(lds + kChainLds + 16)[wv] = ok ? s : __builtin_nan("");  // (for final_in_launch)
+    }
     __builtin_amdgcn_s_setprio(0);
 }
 
@@ -615,6 +618,79 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mt_rsrc(const void* p, uint32_
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
     return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0, (int)bytes, 0x00020000);
 }
+// block_counts for the publishing launch: the workgroup's counts stored write-through, drained,
+// then one agent-scope add to the done counter the chain workgroup waits on.
+__device__ void block_counts_pub(Cnt c, Cnt* dst, uint32_t* done) {
+    __shared__ Cnt red[kBlock / kWave];
+#pragma unroll
+    for (int m = 1; m < kWave; m <<= 1) {
+        c.mx = fmax(c.mx, __shfl_xor(c.mx, m));
+        c.lo += __shfl_xor(c.lo, m);
+        c.hi += __shfl_xor(c.hi, m);
+        c.clip += __shfl_xor(c.clip, m);
+    }
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        Cnt a = red[0];
+        for (int w = 1; w < kBlock / kWave; ++w)
+            a.mx = fmax(a.mx, red[w].mx), a.lo += red[w].lo, a.hi += red[w].hi, a.clip += red[w].clip;
+        uint64_t* d = reinterpret_cast<uint64_t*>(dst);
+        __hip_atomic_store((gu64*)(d + 0), __builtin_bit_cast(uint64_t, a.mx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((gu64*)(d + 1), (uint64_t)a.lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((gu64*)(d + 2), (uint64_t)a.hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((gu64*)(d + 3), (uint64_t)a.clip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add((gu32*)done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// metrics_final's work inside the publishing launch (its chain workgroup, after the chain): wait
+// until every streaming workgroup has added to `done`, reduce the nparts workgroup counts (read by
+// returning atomics, like every handed-off word) and the chain's sums, write out[0..8].  A wait past
+// the spin bound writes NaN sums.
+__device__ void final_in_launch(const Cnt* parts, int nparts, uint32_t* done, uint32_t ndone, int64_t n, double* out,
+                                uint8_t* lds) {
+    const int t = threadIdx.x;
+    double* sums = reinterpret_cast<double*>(lds + kChainLds + 16);  // the chain's three sums
+    int* flag = reinterpret_cast<int*>(lds + kChainLds + 48);
+    Cnt* red = reinterpret_cast<Cnt*>(lds + kChainLds + 64);
+    __syncthreads();  // the chain's sums are in LDS
+    if (t == 0) {
+        uint32_t spins = 0;
+        while (coherent_read(done) < ndone && ++spins <= kChainSpinCap) __builtin_amdgcn_s_sleep(2);
+        *flag = spins <= kChainSpinCap;
+    }
+    __syncthreads();
+    const bool ok = *flag != 0;
+    Cnt c{0.0, 0, 0, 0};
+    for (int i = t; i < nparts && ok; i += kBlock) {
+        const double* q = reinterpret_cast<const double*>(parts + i);
+        c.mx = fmax(c.mx, coherent_read(q));
+        c.lo += __builtin_bit_cast(uint64_t, coherent_read(q + 1));
+        c.hi += __builtin_bit_cast(uint64_t, coherent_read(q + 2));
+        c.clip += __builtin_bit_cast(uint64_t, coherent_read(q + 3));
+    }
+    red[t] = c;
+    __syncthreads();
+    for (int w = kBlock / 2; w > 0; w >>= 1) {
+        if (t < w) {
+            Cnt& a = red[t];
+            const Cnt& b = red[t + w];
+            a.mx = fmax(a.mx, b.mx), a.lo += b.lo, a.hi += b.hi, a.clip += b.clip;
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        const double nan = __builtin_nan("");
+        const double s0 = ok ? sums[0] : nan;
+        out[1] = s0, out[2] = ok ? sums[1] : nan, out[3] = ok ? sums[2] : nan;
+        out[0] = s0 != s0 ? s0 : red[0].mx;  // NumPy's NaN max (metrics_final)
+        out[4] = (double)red[0].lo, out[5] = (double)red[0].hi, out[6] = (double)red[0].clip;
+        out[7] = (double)n, out[8] = 0.0;
+    }
+}
+
 // PUB: one launch over every full block, publishing each block's sums to the chain workgroup
 // (chain_follow; c_lo/c_hi unused) instead of chaining the previous launch's part.
 template <bool PUB>
@@ -623,7 +699,8 @@ __global__ __launch_bounds__(kBlock, 2) void metrics_leaf_kernel(const double* _
                                                                 double* __restrict__ bsum, int64_t nb, int64_t b_lo,
                                                                 int64_t b_hi, int64_t c_lo, int64_t c_hi,
                                                                 double* __restrict__ state, Cnt* __restrict__ parts,
-                                                                uint32_t* __restrict__ cnt) {
+                                                                uint32_t* __restrict__ cnt, const Cnt* parts_all,
+                                                                int nparts_all, int64_t n, double* __restrict__ out) {
     typedef double d2 __attribute__((ext_vector_type(2)));
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     typedef int i4 __attribute__((ext_vector_type(4)));
@@ -631,7 +708,9 @@ __global__ __launch_bounds__(kBlock, 2) void metrics_leaf_kernel(const double* _
     const bool chain = PUB || c_hi > c_lo;
     if (chain && blockIdx.x == 0) {
         if constexpr (PUB) {
-            if (FIR_METRIC_EXP != 4 && FIR_METRIC_EXP != 5) chain_follow(bsum, nb, b_hi, cnt, (int64_t)(gridDim.x - 1) * (kBlock / kWave), state, smem);
+            const int64_t nw = (int64_t)(gridDim.x - 1) * (kBlock / kWave);
+            if (FIR_METRIC_EXP != 4 && FIR_METRIC_EXP != 5) chain_follow(bsum, nb, b_hi, cnt, nw, state, smem);
+            final_in_launch(parts_all, nparts_all, cnt + nw, gridDim.x - 1, n, out, smem);
         }
         else if (FIR_METRIC_EXP != 1)  // (EXP: timing experiments)
             chain_range(bsum, nb, c_lo, c_hi, state, smem);
@@ -762,7 +841,10 @@ __global__ __launch_bounds__(kBlock, 2) void metrics_leaf_kernel(const double* _
         }
     }
     const uint32_t lo = 4 * ndw - (nz_acc - 28 * ndw), hi = ff_acc - 28 * ndw;
-    block_counts(Cnt{mx, lo, hi, lane == 0 ? clip : 0ull}, parts + wg);
+    if constexpr (PUB)
+        block_counts_pub(Cnt{mx, lo, hi, lane == 0 ? clip : 0ull}, parts + wg, cnt + nwaves);
+    else
+        block_counts(Cnt{mx, lo, hi, lane == 0 ? clip : 0ull}, parts + wg);
 }
 
 // Fixed arrays of any other dtype (int8..int64, uint16..uint64, float16/32/64: the reference's
@@ -937,7 +1019,7 @@ constexpr int kMetricPBlocks = FIR_METRIC_PBLOCKS;
 static_assert(kMetricPBlocks + 1 <= kCntSlots, "count slots");
 // the progress words of the publishing launch's streaming waves (zeroed every call by the kernel
 // ahead of it), at the start of the work buffer
-static size_t metrics_cnt_bytes(int64_t) { return (size_t)4 * kMetricPBlocks * (kBlock / kWave); }
+static size_t metrics_cnt_bytes(int64_t) { return (size_t)4 * kMetricPBlocks * (kBlock / kWave) + 16; }  // + done
 
 // Work buffer: the publish counters, Cnt per workgroup of every launch (+ the ragged block's), the
 // 3 running sums, then the block sums [3][nb].
@@ -967,9 +1049,8 @@ int launch_metrics_t(const double* ideal, const FT* fixed, int64_t n, double* ou
             const int64_t want = (nbf + kBlock / kWave - 1) / (kBlock / kWave);
             const int g = (int)(want > kMetricPBlocks ? kMetricPBlocks : want);
             hipLaunchKernelGGL(metrics_leaf_kernel<true>, dim3(g + 1), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb,
-                               (int64_t)0, nbf, (int64_t)0, (int64_t)0, state, parts + slot, cnt);
-            hipLaunchKernelGGL(metrics_final, dim3(1), dim3(kBlock), 0, stream, (const double*)bsum, nb, nb, state,
-                               (const Cnt*)parts, slot + g, n, out);
+                               (int64_t)0, nbf, (int64_t)0, (int64_t)0, state, parts + slot, cnt, (const Cnt*)parts,
+                               slot + g, n, out);
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return *err = std::string("metrics launch failed: ") + hipGetErrorString(e), FIR_EHIP;
             return FIR_OK;
@@ -1002,7 +1083,8 @@ int launch_metrics_t(const double* ideal, const FT* fixed, int64_t n, double* ou
         if constexpr (std::is_same_v<FT, uint8_t>) {
             if (vec && kMetricLeaf)
                 hipLaunchKernelGGL(metrics_leaf_kernel<false>, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb,
-                                   lo, hi, prev_lo, prev_hi, state, parts + slot, (uint32_t*)nullptr);
+                                   lo, hi, prev_lo, prev_hi, state, parts + slot, (uint32_t*)nullptr, (const Cnt*)nullptr, 0,
+                                   (int64_t)0, (double*)nullptr);
             else if (vec && kMetricGlds)
                 hipLaunchKernelGGL(metrics_blocks_glds, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, lo,
                                    hi, prev_lo, prev_hi, state, parts + slot);
