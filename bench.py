@@ -87,7 +87,8 @@ HALO_PREF = os.environ.get("FIR_HALO", "xgmi")
 GATE_MODE = os.environ.get("FIR_GATE_MODE", "serial")
 KERNELS = {"fir1d_i16": "fir1d_reg_kernel", "cplx_i16": "fir1d_reg_kernel", "fir2d_u8": "fir2d_pk16_strip_kernel",
            "fir1d_u8": "fir1d_reg_kernel", "ideal_u8": "fir1d_ideal_kernel", "bank_u8": "fir1d_reg_kernel",
-           "restore_u8": "restore_map_kernel", "metrics_u8": "metrics_blocks+chain"}
+           "restore_u8": "restore_map_kernel",
+           "metrics_u8": "metrics_leaf_kernel<true> (+ progress-word reset; chain and final in the launch)"}
 NUMPY_ONLY = ("restore_u8", "metrics_u8")  # no C oracle leg: the NumPy restatement is the CPU baseline
 ROOF_RAMP, ROOF_LAUNCHES = 100, 200  # roofline loop: untimed ramp, then timed launches of the dominant kernel
 
