@@ -246,3 +246,17 @@ def test_stage_clis_end_to_end(tmp_path, images, capsys):
     # second restore without --overwrite: everything skipped, nothing rewritten
     assert restore_images.main(["--vector-output-dir", str(out), "--output-img-dir", str(img), "--tap", "3"]) == 0
     assert "generated=0 skipped=16" in capsys.readouterr().out
+
+
+def test_report_compute_metrics_keeps_fixed_dtype():
+    """The report's per-case metrics (fir_1d/sim/vector/gen_compare_report.compute_metrics) take the
+    fixed array as np.load returns it, as the reference's _compute_metrics does
+    (gen_3tap_compare_report.py:84-86, :303-304): int16 / int32 / float / bool fixed arrays are not
+    narrowed to uint8 (256 -> 0, -1 -> 255 would change every metric); equal to the reference's own
+    outputs (tests/golden/metrics_dtypes.*)."""
+    from conftest import load_metrics_dtypes, same_metrics
+    from fir_1d.sim.vector.gen_compare_report import compute_metrics
+
+    for name, yi, yf, want in load_metrics_dtypes():
+        got = compute_metrics(yi, yf)
+        assert not same_metrics(got, want), (name, {k: (got[k], want[k]) for k in same_metrics(got, want)})

@@ -55,11 +55,11 @@ def _collect(directory: Path, pattern: re.Pattern):
 
 
 def compute_metrics(y_ideal: np.ndarray, y_fixed: np.ndarray) -> dict[str, float | int]:
-    """Per-case metrics (reference :67-112) on the GPU."""
+    """Per-case metrics (reference gen_3tap_compare_report.py:67-112) on the GPU, for the fixed
+    array as loaded: any integer / bool / float dtype, as the reference's astype(np.float64) (:85)
+    takes it (no cast to uint8: int16 / int32 / float outputs keep their values)."""
     if y_ideal.shape != y_fixed.shape:
         raise ValueError(f"Shape mismatch: ideal={y_ideal.shape}, fixed={y_fixed.shape}")
-    if y_fixed.dtype != np.uint8:
-        y_fixed = y_fixed.astype(np.uint8)
     return fir_hip.compare_metrics(y_ideal, y_fixed)
 
 
