@@ -164,12 +164,14 @@ int fir1d_ideal_rows_dev(const uint8_t* x_dev, int64_t rows, int64_t width, cons
  * One pass over `n` samples of ideal (float64) and fixed outputs of `fixed_dtype` (the
  * reference takes any dtype: y_fixed.astype(np.float64), gen_3tap_compare_report.py:84-86;
  * its fixed stage writes uint8, FIR_DT_U8 is the bandwidth path).  out[9] =
- * {max|d|, sum|d|, sum d^2, sum d, #(fixed==0), #(fixed==255), #(ideal<0 or >255), n, 0}
+ * {max|d|, sum|d|, sum d^2, sum d, #(fixed==0), #(fixed==255), #(ideal<0 or >255), n, status}
  * with d = float64(fixed) - ideal; the report ratios are these over n.  The float64 sums are
  * added in NumPy's order (8192-sample blocks summed pairwise, block sums in order), so they equal
  * the reference's np.mean values bit for bit; counts are exact; max|d| is NaN when any |d| is
  * (np.max propagates NaN).  `work_dev` of the _dev form holds at least fir_metrics_work_bytes(n)
- * bytes.  ABI 4: the fixed dtype argument. */
+ * bytes.  status (out[8]) is 0; 1 means the one-launch pass's in-kernel hand-off gave up waiting
+ * (about 1 s; no correct run reaches it): the sums are then NaN, and fir_compare_metrics returns
+ * FIR_EHIP.  ABI 4: the fixed dtype argument. */
 typedef enum {
     FIR_DT_U8 = 0, FIR_DT_I8 = 1, FIR_DT_U16 = 2, FIR_DT_I16 = 3, FIR_DT_U32 = 4, FIR_DT_I32 = 5,
     FIR_DT_U64 = 6, FIR_DT_I64 = 7, FIR_DT_F16 = 8, FIR_DT_F32 = 9, FIR_DT_F64 = 10

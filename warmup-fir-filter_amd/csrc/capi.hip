@@ -677,6 +677,7 @@ int fir_compare_metrics(const double* ideal, const void* fixed, int fixed_dtype,
         }
         HIP_TRY(hipMemcpyAsync(out, dout, 9 * sizeof(double), hipMemcpyDeviceToHost, st->stream));
         HIP_TRY(hipStreamSynchronize(st->stream));
+        if (out[8] != 0.0) return fail(FIR_EHIP, "metrics: the in-kernel hand-off timed out");
         return FIR_OK;
     } catch (...) {
         return fail(FIR_EHIP, "internal error");

@@ -327,7 +327,11 @@ __device__ __forceinline__ void chain_follow(const double* __restrict__ bsum, in
     // FIR_METRIC_ONEPOLL: only wave 0 polls the progress words and posts how many groups are
     // complete in an LDS word that waves 1-2 watch (one third of the polling atomics)
     int* posted = reinterpret_cast<int*>(lds + kChainLds);  // (past the three staging areas)
-    if (FIR_METRIC_ONEPOLL && wv == 0 && lane == 0) __hip_atomic_store(posted, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    int* failed = reinterpret_cast<int*>(lds + kChainLds + 52);  // a chain wave gave up waiting
+    if (wv == 0 && lane == 0) {
+        __hip_atomic_store(posted, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(failed, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     __builtin_amdgcn_s_barrier();  // (every wave of the workgroup: the word is zero before anyone reads it)
     if (wv >= 3) return;
     __builtin_amdgcn_s_setprio(3);
@@ -378,6 +382,7 @@ __device__ __forceinline__ void chain_follow(const double* __restrict__ bsum, in
     if (lane == 0) {
         state[wv] = ok ? s : __builtin_nan("");
         reinterpret_cast<double*>(lds + kChainLds + 16)[wv] = ok ? s : __builtin_nan("");  // (for final_in_launch)
+        if (!ok) __hip_atomic_store(failed, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     __builtin_amdgcn_s_setprio(0);
 }
@@ -663,6 +668,7 @@ __device__ void final_in_launch(const Cnt* parts, int nparts, uint32_t* done, ui
     }
     __syncthreads();
     const bool ok = *flag != 0;
+    const bool chain_ok = reinterpret_cast<const int*>(lds + kChainLds + 52)[0] == 0;
     Cnt c{0.0, 0, 0, 0};
     for (int i = t; i < nparts && ok; i += kBlock) {
         const double* q = reinterpret_cast<const double*>(parts + i);
@@ -687,7 +693,7 @@ __device__ void final_in_launch(const Cnt* parts, int nparts, uint32_t* done, ui
         out[1] = s0, out[2] = ok ? sums[1] : nan, out[3] = ok ? sums[2] : nan;
         out[0] = s0 != s0 ? s0 : red[0].mx;  // NumPy's NaN max (metrics_final)
         out[4] = (double)red[0].lo, out[5] = (double)red[0].hi, out[6] = (double)red[0].clip;
-        out[7] = (double)n, out[8] = 0.0;
+        out[7] = (double)n, out[8] = ok && chain_ok ? 0.0 : 1.0;  // 1: a hand-off wait timed out
     }
 }
 

@@ -401,7 +401,10 @@ def fir1d_ideal_rows(x_u8: np.ndarray, h, device: int = 0, devices=None) -> np.n
 
 
 def metrics_from_sums(s, n: int) -> dict:
-    """The report's metric dict (gen_3tap_compare_report.py:102-112) from the 9 sums."""
+    """The report's metric dict (gen_3tap_compare_report.py:102-112) from the 9 sums (s[8]: the
+    kernel's status, non-zero when its in-kernel hand-off timed out)."""
+    if len(s) > 8 and float(s[8]) != 0.0:
+        raise FirHipError("metrics: the in-kernel hand-off timed out (status in out[8])")
     if n == 0:
         return {"num_samples": 0, "max_abs_err": 0.0, "mae": 0.0, "rmse": 0.0, "mean_err": 0.0,
                 "sat_low_ratio": 0.0, "sat_high_ratio": 0.0, "sat_ratio": 0.0, "clip_needed_ratio": 0.0}
