@@ -938,6 +938,9 @@ static hipError_t launch_mfma_long(const void* x, void* y, int64_t rl, int64_t t
 #ifndef FIR_MR_DEPTH1                // window iterations in flight with one tile per run (u8 out; 12 waves
 #define FIR_MR_DEPTH1 3               // per CU: (DEPTH1 + 1) x 2 KiB of LDS each)
 #endif
+#ifndef FIR_MR_T1_NS                 // one-chunk filters up to this many k-steps: one tile per run (A/B
+#define FIR_MR_T1_NS 16               // vs 10, 2-tile runs past it: 290 / 322 / 450 taps 165 / 173 / 212 us
+#endif                               // vs 196 / 189 / 221, profiles/r04/long_taps_t1ns_ab.txt)
 #ifndef FIR_MR_BLOCKS                // grid-stride blocks (4 waves each): one resident round
 #define FIR_MR_BLOCKS (256 * FIR_MR_WAVES)
 #endif
@@ -978,9 +981,19 @@ constexpr int kMrTileLds = 2048;     // LDS bytes per tile window (128 vectors o
 #ifndef FIR_MR_ADBL
 #define FIR_MR_ADBL 0
 #endif
+#ifndef FIR_MR_W3_NS                 // one-tile runs of up to this many k-steps: 3 waves per SIMD (2 past it)
+#define FIR_MR_W3_NS 12
+#endif
+constexpr int mr_waves_of(int stage, int tps, bool multi, int ns) {
+    return multi ? FIR_MR_MWAVES
+                 : tps == 1 ? (ns <= FIR_MR_W4_NS && stage == FIR_OUT_U8_SAT ? 4
+                               : ns <= (stage == FIR_OUT_U8_SAT ? FIR_MR_W3_NS : 11) ? 3  // (int32 out: 12 spilled)
+                                                                                      : 2)
+                            : FIR_MR_WAVES;
+}
 template <int STAGE, int TPS_, bool MULTI, int NS>
 constexpr int mr_waves() {
-    return MULTI ? FIR_MR_MWAVES : TPS_ == 1 ? (NS <= FIR_MR_W4_NS && STAGE == FIR_OUT_U8_SAT ? 4 : 3) : FIR_MR_WAVES;
+    return mr_waves_of(STAGE, TPS_, MULTI, NS);
 }
 template <int STAGE, int NS, bool MULTI, int TPS_>
 __global__ __launch_bounds__(kBlock, (mr_waves<STAGE, TPS_, MULTI, NS>())) void fir1d_mfma_run_kernel(const uint8_t* __restrict__ x,
@@ -1275,11 +1288,11 @@ __global__ __launch_bounds__(kBlock, (mr_waves<STAGE, TPS_, MULTI, NS>())) void 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMAs past the end land before the wave exits
 }
 
-// k-steps per chunk for KS k-steps: one chunk of exactly KS (rounded up to an even count past 10)
+// k-steps per chunk for KS k-steps: one chunk of exactly KS (rounded up to an even count past 12)
 // when KS <= kMrC; past it the chunk size among 8..kMrC (even) with the least zero padding, the
 // larger on a tie (fewer iterations)
 static int mfma_run_ns(int KS, int multi_max) {
-    if (KS <= 10) return KS < 4 ? 4 : KS;
+    if (KS <= FIR_MR_T1_NS) return KS < 4 ? 4 : KS <= 12 ? KS : (KS + 1) & ~1;
     if (KS <= kMrC) return (KS + 1) & ~1;
     int best = multi_max, pad = (KS + multi_max - 1) / multi_max * multi_max;
     for (int ns = multi_max - 2; ns >= (multi_max <= 8 ? FIR_MR_MNS_MIN : 8); ns -= 2) {
@@ -1304,11 +1317,10 @@ static hipError_t launch_mfma_run(const void* x, void* y, int64_t rl, int64_t tp
     if (!fr) return hipErrorOutOfMemory;
     TableHold hold(fr, s);
     const bool multi = ksp > ns;
-    const int tps = !multi && ns <= 10 ? 1 : multi ? MTPS : kMrTps;
+    const int tps = !multi && ns <= FIR_MR_T1_NS ? 1 : multi ? MTPS : kMrTps;
     const int64_t nruns = (ntiles + tps - 1) / tps;
     const int64_t want = (nruns + kMfWaves - 1) / kMfWaves;
-    const int64_t cap =
-        (int64_t)256 * (multi ? FIR_MR_MWAVES : tps == 1 ? (ns <= FIR_MR_W4_NS && STAGE == FIR_OUT_U8_SAT ? 4 : 3) : FIR_MR_WAVES);
+    const int64_t cap = (int64_t)256 * mr_waves_of(STAGE, tps, multi, ns);
     const unsigned blocks = (unsigned)(want < cap ? want : cap);
     const uint32_t tp = (uint32_t)tpr, nt = (uint32_t)ntiles;
     const int mode = fast ? 0 : acc_bits == 32 ? 1 : 2;
@@ -1316,7 +1328,7 @@ static hipError_t launch_mfma_run(const void* x, void* y, int64_t rl, int64_t tp
     auto go = [&](auto nsc, auto mc) {
         constexpr int NS = decltype(nsc)::value;
         constexpr bool M = decltype(mc)::value;
-        if constexpr (!M && NS <= 10)
+        if constexpr (!M && NS <= FIR_MR_T1_NS)
             hipLaunchKernelGGL((fir1d_mfma_run_kernel<STAGE, NS, M, 1>), dim3(blocks), dim3(kBlock), 0, s,
                                (const uint8_t*)x, (OutT*)y, rl, tp, nt, fr, ksp, P, bias, mode, shl, frac);
         else if constexpr (M && MTPS == 4)
@@ -1337,7 +1349,7 @@ static hipError_t launch_mfma_run(const void* x, void* y, int64_t rl, int64_t tp
         }                                                                                  \
         break;
     switch (ns) {
-        FIR_MR_NS(4) FIR_MR_NS(5) FIR_MR_NS(6) FIR_MR_NS(7) FIR_MR_NS(8) FIR_MR_NS(9) FIR_MR_NS(10) FIR_MR_NS(12)
+        FIR_MR_NS(4) FIR_MR_NS(5) FIR_MR_NS(6) FIR_MR_NS(7) FIR_MR_NS(8) FIR_MR_NS(9) FIR_MR_NS(10) FIR_MR_NS(11) FIR_MR_NS(12)
         FIR_MR_NS(14) FIR_MR_NS(16)
         default: return hipErrorInvalidValue;
     }
