@@ -250,8 +250,10 @@ def test_table_cache_evicts_only_idle_tables():
 
 
 # every instantiation of fir1d_mfma_run_kernel: one chunk of 4 .. 12 k-steps (one tile per run,
-# 290 / 322 taps: 11 / 12), 14, 16 (354-450 taps); several chunks of 6 and 8 (4-tile runs)
-@pytest.mark.parametrize("L", [65, 66, 100, 129, 130, 162, 194, 257, 258, 290, 322, 354, 386, 449, 450, 500, 930, 1000, 2048,
+# 290 / 322 taps: 11 / 12), 14, 16 (354-450 taps), u8 out 18 .. 32 (500-930 taps; int32 out: several
+# chunks of 8 .. 16 past 16); several chunks of 6 and 8 (4-tile runs, u8 out past 32)
+@pytest.mark.parametrize("L", [65, 66, 100, 129, 130, 162, 194, 257, 258, 290, 322, 354, 386, 449, 450, 500, 580, 660,
+                               720, 800, 860, 900, 930, 1000, 2048,
                                2658, 4099])
 def test_u8_long_filter_run_kernel_vs_oracle(L):
     """u8 filters past 64 taps (fir1d_mfma_run_kernel: runs of 1-2 tiles sharing each chunk of

@@ -938,8 +938,11 @@ static hipError_t launch_mfma_long(const void* x, void* y, int64_t rl, int64_t t
 #ifndef FIR_MR_DEPTH1                // window iterations in flight with one tile per run (u8 out; 12 waves
 #define FIR_MR_DEPTH1 3               // per CU: (DEPTH1 + 1) x 2 KiB of LDS each)
 #endif
+#ifndef FIR_MR_U8_ONE                // u8 out: one chunk (fragments loaded once per wave) up to this many k-steps
+#define FIR_MR_U8_ONE 32
+#endif
 #ifndef FIR_MR_T1_NS                 // one-chunk filters up to this many k-steps: one tile per run (A/B
-#define FIR_MR_T1_NS 16               // vs 10, 2-tile runs past it: 290 / 322 / 450 taps 165 / 173 / 212 us
+#define FIR_MR_T1_NS 32               // vs 10, 2-tile runs past it: 290 / 322 / 450 taps 165 / 173 / 212 us
 #endif                               // vs 196 / 189 / 221, profiles/r04/long_taps_t1ns_ab.txt)
 #ifndef FIR_MR_BLOCKS                // grid-stride blocks (4 waves each): one resident round
 #define FIR_MR_BLOCKS (256 * FIR_MR_WAVES)
@@ -984,11 +987,14 @@ constexpr int kMrTileLds = 2048;     // LDS bytes per tile window (128 vectors o
 #ifndef FIR_MR_W3_NS                 // one-tile runs of up to this many k-steps: 3 waves per SIMD (2 past it)
 #define FIR_MR_W3_NS 12
 #endif
+#ifndef FIR_MR_W2_NS                 // ... 2 waves up to this many (1 past it)
+#define FIR_MR_W2_NS 24
+#endif
 constexpr int mr_waves_of(int stage, int tps, bool multi, int ns) {
     return multi ? FIR_MR_MWAVES
                  : tps == 1 ? (ns <= FIR_MR_W4_NS && stage == FIR_OUT_U8_SAT ? 4
                                : ns <= (stage == FIR_OUT_U8_SAT ? FIR_MR_W3_NS : 11) ? 3  // (int32 out: 12 spilled)
-                                                                                      : 2)
+                               : ns <= FIR_MR_W2_NS ? 2 : 1)
                             : FIR_MR_WAVES;
 }
 template <int STAGE, int TPS_, bool MULTI, int NS>
@@ -1043,8 +1049,11 @@ __global__ __launch_bounds__(kBlock, (mr_waves<STAGE, TPS_, MULTI, NS>())) void 
     // descriptors have size 0.
     constexpr bool CUR = TPS == 1 && !MULTI && FIR_MR_CURSOR;
     // the bias as the first MFMA's accumulator input (16 VGPRs) or one add per output
-    constexpr bool BIASV = FIR_MR_BIASV && mr_waves<STAGE, TPS_, MULTI, NS>() < 4;
-    constexpr int BPD = TPS == 4 ? 1 : mr_waves<STAGE, TPS_, MULTI, NS>() < 4 ? kMrBpd : 2;  // B reads ahead (registers)
+    // (23-24 k-steps at 2 waves per SIMD: no bias registers and 2 reads ahead, or they spill; at 1
+    // wave both cost ~4 %: 800 / 930 taps 430 / 478 vs 414 / 461 us, profiles/r04/long_taps_one_chunk_ab.txt)
+    constexpr bool TRIM = NS > 22 && mr_waves<STAGE, TPS_, MULTI, NS>() == 2;
+    constexpr bool BIASV = FIR_MR_BIASV && mr_waves<STAGE, TPS_, MULTI, NS>() < 4 && !TRIM;
+    constexpr int BPD = TPS == 4 ? 1 : TRIM ? 2 : mr_waves<STAGE, TPS_, MULTI, NS>() < 4 ? kMrBpd : 2;  // B reads ahead
     struct Cursor {
         uint32_t row, col;
         int64_t rs;
@@ -1291,9 +1300,9 @@ __global__ __launch_bounds__(kBlock, (mr_waves<STAGE, TPS_, MULTI, NS>())) void 
 // k-steps per chunk for KS k-steps: one chunk of exactly KS (rounded up to an even count past 12)
 // when KS <= kMrC; past it the chunk size among 8..kMrC (even) with the least zero padding, the
 // larger on a tie (fewer iterations)
-static int mfma_run_ns(int KS, int multi_max) {
-    if (KS <= FIR_MR_T1_NS) return KS < 4 ? 4 : KS <= 12 ? KS : (KS + 1) & ~1;
-    if (KS <= kMrC) return (KS + 1) & ~1;
+static int mfma_run_ns(int KS, int multi_max, int one_max) {
+    if (KS <= 12) return KS < 4 ? 4 : KS;
+    if (KS <= one_max) return (KS + 1) & ~1;
     int best = multi_max, pad = (KS + multi_max - 1) / multi_max * multi_max;
     for (int ns = multi_max - 2; ns >= (multi_max <= 8 ? FIR_MR_MNS_MIN : 8); ns -= 2) {
         const int p = (KS + ns - 1) / ns * ns;
@@ -1311,7 +1320,7 @@ static hipError_t launch_mfma_run(const void* x, void* y, int64_t rl, int64_t tp
     // per iteration from L2, feed 4 tiles, so their latency is paid per 4 tiles), chunks of <= 8
     // k-steps (the accumulators of 4 tiles and one fragment set fit two waves per SIMD)
     constexpr int MTPS = STAGE == FIR_OUT_U8_SAT ? FIR_MR_MTPS : kMrTps;
-    const int ns = mfma_run_ns(KS, MTPS == 4 ? 8 : kMrC);
+    const int ns = mfma_run_ns(KS, MTPS == 4 ? 8 : kMrC, STAGE == FIR_OUT_U8_SAT ? FIR_MR_U8_ONE : kMrC);
     const int ksp = (KS + ns - 1) / ns * ns;  // the table padded to whole chunks (zero fragments)
     const mf_i32x4* fr = mfma_frag_table(hq, L, P, ksp, &err);
     if (!fr) return hipErrorOutOfMemory;
@@ -1342,15 +1351,17 @@ static hipError_t launch_mfma_run(const void* x, void* y, int64_t rl, int64_t tp
 #define FIR_MR_NS(n)                                                                       \
     case n:                                                                                \
         if (multi) {                                                                       \
-            if constexpr (MTPS == 4 ? (n == 6 || n == 8) : n >= 8 && n % 2 == 0)                  \
+            if constexpr (MTPS == 4 ? (n == 6 || n == 8) : n >= 8 && n <= kMrC && n % 2 == 0)     \
                 go(integral_constant<int, n>{}, std::true_type{});                         \
         } else {                                                                           \
-            go(integral_constant<int, n>{}, std::false_type{});                            \
+            if constexpr (n <= (STAGE == FIR_OUT_U8_SAT ? FIR_MR_U8_ONE : kMrC))             \
+                go(integral_constant<int, n>{}, std::false_type{});                        \
         }                                                                                  \
         break;
     switch (ns) {
         FIR_MR_NS(4) FIR_MR_NS(5) FIR_MR_NS(6) FIR_MR_NS(7) FIR_MR_NS(8) FIR_MR_NS(9) FIR_MR_NS(10) FIR_MR_NS(11) FIR_MR_NS(12)
-        FIR_MR_NS(14) FIR_MR_NS(16)
+        FIR_MR_NS(14) FIR_MR_NS(16) FIR_MR_NS(18) FIR_MR_NS(20) FIR_MR_NS(22) FIR_MR_NS(24) FIR_MR_NS(26)
+        FIR_MR_NS(28) FIR_MR_NS(30) FIR_MR_NS(32)
         default: return hipErrorInvalidValue;
     }
 #undef FIR_MR_NS
