@@ -914,7 +914,7 @@ static hipError_t launch_mfma_long(const void* x, void* y, int64_t rl, int64_t t
 #define FIR_MR_EXP 0
 #endif
 #ifndef FIR_MR_W4_NS                 // one-tile runs of up to this many k-steps: 4 waves per SIMD
-#define FIR_MR_W4_NS 6
+#define FIR_MR_W4_NS 8                // (vs 6: 162 / 194 taps 140 / 136 us vs 149 / 139, profiles/r04/long_taps_w4ns_ab.txt)
 #endif
 #ifndef FIR_MR_BIASV                 // 1: bias folded into the first MFMA (below 4 waves per SIMD)
 #define FIR_MR_BIASV 1
