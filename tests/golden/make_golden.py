@@ -29,6 +29,12 @@ Files written:
                                      outside [0, 255]) with the reference's outputs
   long_taps.npz                      long filters (257 / 1000 / 2048 / 4099 taps, shorter and
                                      longer than x): fir_1d_fixed_golden and fir_1d_ideal outputs
+  input_contract.json                the input contract: fir_1d_fixed_golden / fir_1d_ideal on
+                                     inputs that are not plain number lists (str, complex, None,
+                                     scalars, 0-d / 2-D arrays, bytes, generators, Decimal ...),
+                                     and the row drivers on non-u8 images (float / int16 / f16
+                                     values outside [0, 255], x.5 ties, NaN in row k, error
+                                     order against bad bit widths): output or exception + text
   meta.json                          generator environment
 
 Usage:  python tests/golden/make_golden.py [--jobs 8]
@@ -432,6 +438,181 @@ def _ragged(xs, hs, ys):
     return (*cat(xs, np.float64), *cat(hs, np.float64), *cat(ys, ys[0].dtype))
 
 
+# ----------------------------------------------------------------------------
+# Input contract: what the reference accepts / raises for inputs beyond plain number lists
+# (fir_1d_ref.py:27-41 applied at fir_1d_fixed_ref.py:33-36; row drivers
+# gen_fixed_output.py:34-60, gen_ideal_output.py:37-50).  Encoded with tests/contract_codec.py.
+# ----------------------------------------------------------------------------
+def _contract_cases():
+    from decimal import Decimal
+    from fractions import Fraction
+
+    from contract_codec import Gen
+
+    rng = np.random.default_rng(2718)
+    nan, inf = float("nan"), float("inf")
+    lp3, sharpen5 = [0.25, 0.5, 0.25], [-0.0625, -0.25, 1.625, -0.25, -0.0625]
+    f32_ties = np.array([0.49999997, 0.5, 1.4999999, 2.5, 254.49998, 254.5, 255.5, -0.5, -0.50000006, 3.0],
+                        dtype=np.float32)
+    models = [  # (id, x, h, kwargs) -> both models (kwargs only for the fixed one)
+        ("str_list", ["10", "20"], lp3, {}),
+        ("str", "12", lp3, {}),
+        ("str_elem_late", [1, 2, "3"], lp3, {}),
+        ("complex_list", [1 + 0j, 2], lp3, {}),
+        ("complex_array", np.array([1 + 0j, 2, 3.5 - 1j]), lp3, {}),
+        ("none_elem", [1, None], lp3, {}),
+        ("none", None, lp3, {}),
+        ("scalar_int", 5, lp3, {}),
+        ("scalar_float", 5.0, lp3, {}),
+        ("np_scalar", np.float64(7.0), lp3, {}),
+        ("array_0d", np.array(5), lp3, {}),
+        ("array_2d_f64", np.array([[1.0, 2.0], [3.0, 4.0]]), lp3, {}),
+        ("array_2d_u8", np.array([[1, 2], [3, 4]], dtype=np.uint8), lp3, {}),
+        ("array_2d_col", np.array([[1.0], [2.6], [254.5], [300.0]]), lp3, {}),
+        ("array_2d_col_nan", np.array([[1.0], [nan]]), lp3, {}),
+        ("array_2d_1x1", np.array([[9.5]]), lp3, {}),
+        ("array_2d_row", np.array([[1.0, 2.0, 3.0]]), lp3, {}),
+        ("array_3d", np.zeros((2, 2, 2)), lp3, {}),
+        ("nested_list", [[1], [2]], lp3, {}),
+        ("bytes", b"\x01\x02\xff\x80", lp3, {}),
+        ("bytearray", bytearray(b"\x05\x06"), lp3, {}),
+        ("range", range(0, 300, 7), lp3, {}),
+        ("generator", Gen([1, 2, 3]), lp3, {}),
+        ("generator_nan", Gen([1, nan]), lp3, {}),
+        ("dict_keys", {3: "a", 40: "b", 2.5: "c"}, lp3, {}),
+        ("tuple_floats", (0.5, 1.5, 2.5, 254.5), lp3, {}),
+        ("bool_list", [True, False, True], lp3, {}),
+        ("bool_array", np.array([True, False, True]), lp3, {}),
+        ("decimal", [Decimal("1.5")], lp3, {}),
+        ("decimal_nan", [Decimal("NaN")], lp3, {}),
+        ("fraction", [Fraction(5, 2), Fraction(1, 3), Fraction(509, 2)], lp3, {}),
+        ("big_int", [10 ** 400], lp3, {}),
+        ("big_int_after_nan", [nan, 10 ** 400], lp3, {}),
+        ("nan_after_big_int", [10 ** 400, nan], lp3, {}),
+        ("int_beyond_2p53", [2 ** 53 + 1, -(2 ** 60), 2 ** 63, 7], lp3, {}),
+        ("py_float_ties", [0.49999999999999994, 0.5, 1.5, 2.5, -0.5, -0.5000000000000001, 254.5, 255.5, -0.0], [1.0], {}),
+        ("np_float64_elems", [np.float64(2.5), np.float64(300.2)], lp3, {}),
+        ("np_float32_elems", [np.float32(0.49999997), np.float32(2.5)], [1.0], {}),
+        ("np_float64_nan_elem", [np.float64(1.0), np.float64(nan)], lp3, {}),
+        ("mixed_numbers", [True, 3, 4.5, np.uint8(200), np.int64(-7), np.float32(8.5)], [1.0], {}),
+        ("f32_array_ties", f32_ties, [1.0], {}),
+        ("f32_array_inf", np.array([1.0, inf], dtype=np.float32), lp3, {}),
+        ("f16_array", np.array([0.4998, 0.5, 2.5, 254.5, 300.0, -1.0], dtype=np.float16), [1.0], {}),
+        ("f64_array_nan", np.array([1.0, 2.0, nan]), lp3, {}),
+        ("i16_array", np.array([-300, -1, 0, 17, 255, 256, 32767], dtype=np.int16), [1.0], {}),
+        ("u64_array", np.array([0, 255, 256, 2 ** 64 - 1], dtype=np.uint64), [1.0], {}),
+        ("i64_array_big", np.array([2 ** 62, -(2 ** 62), 3], dtype=np.int64), [1.0], {}),
+        ("object_array", np.array([1, 2.5, np.float32(3.5), Fraction(7, 2)], dtype=object), [1.0], {}),
+        ("object_array_str", np.array([1, "2"], dtype=object), lp3, {}),
+        ("longdouble_overflow", np.array([1.0, 2.0], dtype=np.longdouble) * np.longdouble(10) ** 400, lp3, {}),
+        ("str_array", np.array(["1", "2"]), lp3, {}),
+        ("timedelta_array", np.array([1, 2], dtype="m8[s]"), lp3, {}),
+        ("masked_array", np.ma.MaskedArray([1.0, 2.0, 3.0], mask=[False, True, False]), lp3, {}),
+        ("empty_tuple", (), lp3, {}),
+        ("empty_array_f32", np.zeros(0, dtype=np.float32), lp3, {}),
+        ("float_sample_list_long", (rng.uniform(-20, 280, 300)).tolist(), sharpen5, {}),
+        # error order: h before x, x before the bit widths
+        ("bad_h_and_str_x", ["a"], [], {}),
+        ("str_x_and_bad_frac", ["a"], lp3, {"frac_bits": 0}),
+        ("nan_x_and_bad_coeff", [nan], lp3, {"coeff_bits": 12}),
+        # bit widths of non-int type (the reference's shifts raise TypeError)
+        ("acc_bits_float", [1, 2], lp3, {"acc_bits": 32.0}),
+        ("acc_bits_float_empty_x", [], lp3, {"acc_bits": 32.0}),
+        ("frac_bits_float", [1, 2], lp3, {"frac_bits": 12.0}),
+        ("coeff_bits_float", [1, 2], lp3, {"coeff_bits": 16.0}),
+        ("acc_bits_np_int", [100, 200, 50], lp3, {"acc_bits": np.int64(20)}),
+        ("frac_bits_bool", [100, 200], [1.0], {"frac_bits": True, "coeff_bits": 8}),
+    ]
+    img_f64 = rng.uniform(-40.0, 300.0, (6, 37))
+    img_f64[1, :8] = [-0.5, 0.5, 1.5, 2.5, 254.5, 255.5, 0.49999999999999994, -0.0]
+    img_f32 = rng.uniform(-40.0, 300.0, (5, 21)).astype(np.float32)
+    img_f32[0, :10] = f32_ties  # tolist widens to float64: 0.49999997 rounds to 0 here, 1 in a 1-D call
+    img_f16 = rng.uniform(-40.0, 300.0, (4, 19)).astype(np.float16)
+    img_i16 = rng.integers(-300, 600, (5, 23)).astype(np.int16)
+    img_nan_r3 = rng.uniform(0.0, 255.0, (6, 17))
+    img_nan_r3[3, 5] = nan
+    img_nan_r3[4, 1] = inf
+    img_inf_r0 = rng.uniform(0.0, 255.0, (3, 9))
+    img_inf_r0[0, 7] = -inf
+    img_obj = np.array([[1, 2.5, Fraction(9, 2)], [300, -4, 7.5]], dtype=object)
+    rows = [  # (id, image, h, fixed kwargs)
+        ("img_f64_out_of_range_ties", img_f64, sharpen5, {}),
+        ("img_f32_ties", img_f32, [1.0], {}),
+        ("img_f32_lp", img_f32, lp3, {}),
+        ("img_f16", img_f16, sharpen5, {}),
+        ("img_i16", img_i16, sharpen5, {}),
+        ("img_i64_big", np.array([[2 ** 62, -(2 ** 62), 5, 255], [256, -1, 0, 128]], dtype=np.int64), lp3, {}),
+        ("img_u16", rng.integers(0, 65536, (3, 11)).astype(np.uint16), lp3, {}),
+        ("img_bool", rng.integers(0, 2, (3, 8)).astype(bool), [2.0], {}),
+        ("img_col", np.array([[3.5], [-2.0], [400.0]]), lp3, {}),
+        ("img_object", img_obj, lp3, {}),
+        ("img_nan_row3", img_nan_r3, lp3, {}),
+        ("img_inf_row0", img_inf_r0, lp3, {}),
+        ("img_nan_row3_bad_frac", img_nan_r3, lp3, {"frac_bits": 0}),
+        ("img_inf_row0_bad_frac", img_inf_r0, lp3, {"frac_bits": 0}),
+        ("img_nan_row3_q_range", img_nan_r3, sharpen5, {"coeff_bits": 8}),
+        ("img_nan_row3_bad_h", img_nan_r3, [nan], {}),
+        ("img_no_rows_bad_h", np.zeros((0, 5)), [], {"frac_bits": 0}),
+        ("img_no_rows_nan_h", np.zeros((0, 5)), [nan], {}),
+        ("img_no_cols_bad_frac", np.zeros((3, 0)), lp3, {"frac_bits": 0}),
+        ("img_no_cols_bad_h", np.zeros((3, 0)), [], {}),
+        ("img_no_cols", np.zeros((3, 0), dtype=np.float32), lp3, {}),
+        ("img_complex", np.array([[1 + 0j, 2], [3, 4]]), lp3, {}),
+        ("img_str", np.array([["1", "2"], ["3", "4"]]), lp3, {}),
+        ("img_1d", np.array([1.0, 2.0, 3.0]), lp3, {}),
+        ("img_3d", np.zeros((2, 2, 2)), lp3, {}),
+        ("img_nested_list", [[1, 2], [3, 4]], lp3, {}),
+        ("img_u8_acc_bits_float", rng.integers(0, 256, (2, 6)).astype(np.uint8), lp3, {"acc_bits": 32.0}),
+    ]
+    return models, rows
+
+
+def gen_input_contract(fixed_ref, ideal_ref, gfo, gio):
+    sys.path.insert(0, str(OUT.parent))
+    import warnings
+
+    from contract_codec import dec, enc
+
+    models, rows = _contract_cases()
+    kw_fixed = {"frac_bits": 12, "acc_bits": 32, "coeff_bits": 16}
+
+    def record(fn, *args, **kw):
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")  # ComplexWarning / DeprecationWarning on some inputs
+            r = _call(fn, *args, **kw)
+        return {"result": enc(r["ok"])} if "ok" in r else {"error": r["error"], "message": r["message"]}
+
+    def prepared(x):  # the reference's own x chain (fir_1d_ref.py:27-41), as ints in [0, 255]
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            return [int(v) for v in ideal_ref._clamp_x(ideal_ref._round_half_up_x(ideal_ref._validate_x(x)))]
+
+    recs = []
+    for cid, x, h, kw in models:
+        ex, eh, ekw = enc(x), enc(h), {k: enc(v) for k, v in kw.items()}
+        dkw = {k: dec(v) for k, v in ekw.items()}
+        recs.append({"id": cid, "fn": "fixed", "x": ex, "h": eh, "kwargs": ekw,
+                     **record(fixed_ref.fir_1d_fixed_golden, dec(ex), dec(eh), **dkw)})
+        if not kw:
+            recs.append({"id": cid, "fn": "ideal", "x": ex, "h": eh, "kwargs": {},
+                         **record(ideal_ref.fir_1d_ideal, dec(ex), dec(eh))})
+        if "result" in recs[-1]:
+            recs[-1]["prepared"] = prepared(dec(ex))
+    for cid, x, h, kw in rows:
+        ex, eh = enc(x), enc(h)
+        ekw = {k: enc(v) for k, v in {**kw_fixed, **kw}.items()}
+        dkw = {k: dec(v) for k, v in ekw.items()}
+        recs.append({"id": cid, "fn": "fixed_rows", "x": ex, "h": eh, "kwargs": ekw,
+                     **record(gfo._run_fixed_rowwise, dec(ex), dec(eh), **dkw)})
+        if not kw:
+            recs.append({"id": cid, "fn": "ideal_rows", "x": ex, "h": eh, "kwargs": {},
+                         **record(gio._run_ideal_rowwise, dec(ex), dec(eh))})
+        if "result" in recs[-1]:
+            recs[-1]["prepared"] = [prepared(row.tolist()) for row in dec(ex)]
+    (OUT / "input_contract.json").write_text(json.dumps(recs, indent=0) + "\n")
+    return len(recs)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
@@ -439,11 +620,15 @@ def main():
     ap.add_argument("--only-restore", action="store_true")
     ap.add_argument("--only-long", action="store_true")
     ap.add_argument("--only-metrics", action="store_true")
+    ap.add_argument("--only-contract", action="store_true")
     args = ap.parse_args()
     if args.only_restore:
         print("restore", gen_restore())
         return
     fixed_ref, ideal_ref, _gf, _gi, _gv, rep, _h = _ref_imports()
+    if args.only_contract:
+        print("input_contract", gen_input_contract(fixed_ref, ideal_ref, _gf, _gi))
+        return
     if args.only_metrics:
         print("metrics_dtypes", gen_metrics_dtypes(rep))
         return
@@ -461,6 +646,7 @@ def main():
     print("restore", gen_restore())
     print("long_taps", gen_long_taps(fixed_ref, ideal_ref))
     print("metrics_dtypes", gen_metrics_dtypes(rep))
+    print("input_contract", gen_input_contract(fixed_ref, ideal_ref, _gf, _gi))
     (OUT / "meta.json").write_text(json.dumps(meta, indent=1) + "\n")
 
 

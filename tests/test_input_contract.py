@@ -1,0 +1,106 @@
+"""The drop-in input contract, on the CPU: exception type and text for every input the
+reference rejects, the prepared samples for every input it accepts, and the empty outputs
+that need no device.  The computing cases run in test_gpu_input_contract.py.
+
+Fixture: tests/golden/input_contract.json, recorded by running the reference itself
+(tests/golden/make_golden.py --only-contract) on inputs beyond plain number lists: str,
+complex, None, Decimal, Fraction, big ints, scalars, 0-d / 2-D / 3-D arrays, bytes, ranges,
+generators, masked / object / longdouble arrays, and non-u8 images for the row drivers
+(values outside [0, 255], x.5 ties, NaN in row k, error order against bad bit widths).
+
+Reference: fir_1d/model/python/fir_1d_ref.py:27-41 (x chain), fir_1d_fixed_ref.py:33-94
+(validation order), fir_1d/sim/vector/gen_fixed_output.py:34-60 and
+gen_ideal_output.py:37-50 (row drivers).
+"""
+from __future__ import annotations
+
+import json
+import warnings
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from contract_codec import dec, same
+from fir_1d.model.python.fir_1d_fixed_ref import fir_1d_fixed_golden
+from fir_1d.model.python.fir_1d_ref import _prepare_rows_u8, _prepare_x_u8, fir_1d_ideal
+from fir_1d.sim.vector.gen_fixed_output import _run_fixed_rowwise
+from fir_1d.sim.vector.gen_ideal_output import _run_ideal_rowwise
+
+RECORDS = json.loads((GOLDEN / "input_contract.json").read_text())
+FNS = {"fixed": fir_1d_fixed_golden, "ideal": fir_1d_ideal,
+       "fixed_rows": _run_fixed_rowwise, "ideal_rows": _run_ideal_rowwise}
+
+
+def call(rec):
+    fn = FNS[rec["fn"]]
+    kw = {k: dec(v) for k, v in rec["kwargs"].items()}
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        return fn(dec(rec["x"]), dec(rec["h"]), **kw)
+
+
+def _empty(rec) -> bool:
+    r = dec(rec["result"])
+    return (r.size if isinstance(r, np.ndarray) else len(r)) == 0
+
+
+def _rid(rec):
+    return f"{rec['fn']}-{rec['id']}"
+
+
+def test_fixture_covers_the_verdict_cases():
+    ids = {r["id"] for r in RECORDS}
+    for need in ("str_list", "str", "array_2d_f64", "array_2d_u8", "complex_list", "scalar_int", "none_elem",
+                 "bytes", "img_f64_out_of_range_ties", "img_i16", "img_nan_row3", "img_nan_row3_bad_frac"):
+        assert need in ids
+    assert sum("error" in r for r in RECORDS) >= 60 and sum("result" in r for r in RECORDS) >= 70
+
+
+@pytest.mark.parametrize("rec", [r for r in RECORDS if "error" in r], ids=_rid)
+def test_rejected_inputs_raise_the_reference_exception(rec):
+    with pytest.raises(Exception) as ei:
+        call(rec)
+    assert type(ei.value).__name__ == rec["error"]
+    assert str(ei.value) == rec["message"]
+
+
+@pytest.mark.parametrize("rec", [r for r in RECORDS if "result" in r and _empty(r)], ids=_rid)
+def test_accepted_inputs_with_empty_output(rec):
+    assert same(call(rec), dec(rec["result"]))
+
+
+@pytest.mark.parametrize("rec", [r for r in RECORDS if "prepared" in r], ids=_rid)
+def test_accepted_inputs_prepare_to_the_reference_samples(rec):
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        if rec["fn"].endswith("_rows"):
+            got = _prepare_rows_u8(dec(rec["x"]))
+            want = np.array(rec["prepared"], dtype=np.uint8).reshape(got.shape)
+        else:
+            got = _prepare_x_u8(dec(rec["x"]))
+            want = np.array(rec["prepared"], dtype=np.uint8)
+    assert got.dtype == np.uint8 and got.shape == want.shape
+    assert np.array_equal(got, want)
+
+
+def test_float32_rounds_in_float32_for_the_model_but_float64_per_row():
+    """The same float32 samples prepare differently through the two entry points, as in the
+    reference: a 1-D call adds 0.5 in float32, the row driver widens via tolist() first."""
+    x = np.array([0.49999997, 2.5], dtype=np.float32)
+    assert _prepare_x_u8(x).tolist() == [1, 3]
+    assert _prepare_rows_u8(x.reshape(1, 2)).tolist() == [[0, 3]]
+
+
+def test_u8_list_fast_path_rate():
+    """The reference's row driver passes ``row.tolist()`` of a uint8 image: that list must stay
+    on the one-copy bytearray path (the GPU call itself adds ~20 us)."""
+    import time
+
+    row = np.random.default_rng(3).integers(0, 256, 4499).astype(np.uint8).tolist()
+    _prepare_x_u8(row)
+    t0 = time.perf_counter()
+    for _ in range(200):
+        _prepare_x_u8(row)
+    per_call = (time.perf_counter() - t0) / 200
+    assert per_call < 40e-6, per_call

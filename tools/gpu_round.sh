@@ -31,8 +31,8 @@ fatal() {  # rc: anything but 0/1 (crash, abort, timeout) ends the session
 for s in $STEPS; do
     case $s in
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; rc=$?; [ $rc -ne 0 ] && exit $rc ;;
-        pytest) run pytest_gpu 700 python -m pytest tests -m gpu -q -p no:cacheprovider -x; fatal $? ;;
-        pytestall) run pytest_gpu 700 python -m pytest tests -m gpu -q -p no:cacheprovider; fatal $? ;;
+        pytest) run pytest_gpu 700 python -u -m pytest tests -m gpu -q -p no:cacheprovider -x --timeout 120 --timeout-method thread; fatal $? ;;
+        pytestall) run pytest_gpu 700 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread; fatal $? ;;
         bench) run bench 300 python bench.py; fatal $? ;;
         benchcplx) run bench_cplx 300 python bench.py --workload cplx_i16 --cpu-seconds 5; fatal $? ;;
         bench2d) run bench_2d 300 python bench.py --workload fir2d_u8 --cpu-seconds 5; fatal $? ;;

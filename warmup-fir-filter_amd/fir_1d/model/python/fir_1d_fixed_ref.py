@@ -9,7 +9,8 @@ libfir_hip.so.  There is no CPU fallback: without the library or a gfx950 device
 call raises ``fir_hip.FirHipError``.
 
 Reference lines mirrored (paths relative to the reference root):
-  validation order          fir_1d_fixed_ref.py:33-47 (h, then x, then frac/acc/coeff bits)
+  validation order          fir_1d_fixed_ref.py:33-47 (h, then x, then frac/acc/coeff bits;
+                            x's own contract is fir_1d_ref._prepare_x_u8)
   Q-format range check      fir_1d_fixed_ref.py:52-72
   quantization              fir_1d_fixed_ref.py:78-81 (np.rint ties-to-even, clip, cast)
   MAC / wrap / round / sat  fir_1d_fixed_ref.py:95-126 (device kernel)
@@ -59,12 +60,23 @@ def _quantize_checked(h, frac_bits: int, coeff_bits: int) -> np.ndarray:
     return hf.astype(_DTYPE_H[coeff_bits]).astype(np.int32)
 
 
+def _coeff_stage(h, frac_bits, acc_bits, coeff_bits) -> np.ndarray:
+    """What fir_1d_fixed_golden does between its x preparation and its MAC loop
+    (fir_1d_fixed_ref.py:39-94): bit-width checks, Q-range check, quantization, and the
+    accumulator mask ``1 << acc_bits`` (:94), which raises TypeError for a non-integer
+    acc_bits even when x is empty.  Returns int32 taps."""
+    _check_bits(frac_bits, acc_bits, coeff_bits)
+    hq = _quantize_checked(h, frac_bits, coeff_bits)
+    if not isinstance(acc_bits, (int, np.integer)):
+        1 << acc_bits  # noqa: B018 -- the reference's own TypeError for float / Fraction widths
+    return hq
+
+
 def quantize_fixed_taps(h, frac_bits: int = 12, acc_bits: int = 32, coeff_bits: int = 16) -> np.ndarray:
     """All coefficient-side checks of fir_1d_fixed_golden, in the reference's order, for a
     caller whose samples are already uint8 (so the x checks cannot fail): returns int32 taps."""
     _validate_h_coefficients(h)
-    _check_bits(frac_bits, acc_bits, coeff_bits)
-    return _quantize_checked(h, frac_bits, coeff_bits)
+    return _coeff_stage(h, frac_bits, acc_bits, coeff_bits)
 
 
 def device_bits(frac_bits: int, acc_bits: int) -> tuple[int, int]:
@@ -95,8 +107,7 @@ def fir_1d_fixed_golden(
     """
     _validate_h_coefficients(h)
     x_u8 = _prepare_x_u8(x)
-    _check_bits(frac_bits, acc_bits, coeff_bits)
-    hq = _quantize_checked(h, frac_bits, coeff_bits)
+    hq = _coeff_stage(h, frac_bits, acc_bits, coeff_bits)
     if x_u8.size == 0:
         return np.zeros(0, dtype=np.uint8)
     f, a = device_bits(frac_bits, acc_bits)

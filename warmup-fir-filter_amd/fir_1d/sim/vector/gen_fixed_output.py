@@ -19,7 +19,8 @@ from time import perf_counter
 import numpy as np
 
 import fir_hip
-from fir_1d.model.python.fir_1d_fixed_ref import device_bits, quantize_fixed_taps
+from fir_1d.model.python.fir_1d_fixed_ref import _coeff_stage, device_bits, quantize_fixed_taps
+from fir_1d.model.python.fir_1d_ref import _prepare_rows_u8, _validate_h_coefficients
 from fir_1d.sim.vector.h_coeff import h_coeff_3tap_map, h_coeff_5tap_map
 
 THIS_FILE = Path(__file__).resolve()
@@ -46,14 +47,20 @@ def _case_stem_from_input(path: Path) -> str:
 
 def _run_fixed_rowwise(x_u8: np.ndarray, h: list[float], *, frac_bits: int, acc_bits: int,
                        coeff_bits: int, devices=None) -> np.ndarray:
-    """Every row of an H x W uint8 image through the fixed model: one GPU launch (one per
-    device when ``devices`` lists several)."""
+    """Every row of an H x W image through the fixed model: one GPU launch (one per device
+    when ``devices`` lists several).  A non-uint8 image is prepared row by row with the
+    model's own rules and exception order (fir_1d_ref._prepare_rows_u8): the reference calls
+    the model per row on ``row.tolist()`` (gen_fixed_output.py:44-52), so h is checked first,
+    then row 0's samples, then the bit widths and Q-range, then rows 1..H-1.  An image with
+    no rows returns without any check, as the reference's loop never runs."""
     height, width = x_u8.shape
     if height == 0:
         return np.zeros((0, width), dtype=np.uint8)
-    hq = quantize_fixed_taps(h, frac_bits, acc_bits, coeff_bits)
+    _validate_h_coefficients(h)
+    taps = []
+    xc = _prepare_rows_u8(x_u8, lambda: taps.append(_coeff_stage(h, frac_bits, acc_bits, coeff_bits)))
+    hq = taps[0]
     f, a = device_bits(frac_bits, acc_bits)
-    xc = np.ascontiguousarray(x_u8, dtype=np.uint8)
     devs = fir_hip.parse_devices(devices)
     if len(devs) > 1:
         y = fir_hip.fir1d_fixed_rows_sharded(xc, hq, f, a, fir_hip.OUT_U8_SAT, devices=devs)
@@ -94,6 +101,10 @@ def _run_bank(x_u8: np.ndarray, pending: list, *, frac_bits: int, acc_bits: int,
     if not pending:
         return 0
     height, width = x_u8.shape
+    if height == 0:  # the reference's row loop never calls the model: no checks, empty outputs
+        for out_path, _ in pending:
+            np.save(out_path, np.zeros((0, width), dtype=np.uint8))
+        return len(pending)
     taps, error = [], None
     for out_path, h in pending:
         try:
@@ -107,7 +118,7 @@ def _run_bank(x_u8: np.ndarray, pending: list, *, frac_bits: int, acc_bits: int,
         while j < len(taps) and len(taps[j][1]) == len(taps[i][1]):
             j += 1
         group = taps[i:j]
-        if height == 0 or width == 0:
+        if width == 0:
             ys = np.zeros((len(group), height, width), dtype=np.uint8)
         else:
             f, a = device_bits(frac_bits, acc_bits)

@@ -15,7 +15,7 @@ from time import perf_counter
 import numpy as np
 
 import fir_hip
-from fir_1d.model.python.fir_1d_ref import _validate_h_coefficients
+from fir_1d.model.python.fir_1d_ref import _prepare_rows_u8, _validate_h_coefficients
 from fir_1d.sim.vector.gen_fixed_output import _case_stem_from_input, _iter_input_npy_files, _load_input_image_u8
 from fir_1d.sim.vector.h_coeff import h_coeff_3tap_map, h_coeff_5tap_map
 
@@ -25,14 +25,19 @@ DEFAULT_OUTPUT_DIR = THIS_FILE.parent / "output"
 
 
 def _run_ideal_rowwise(x_u8: np.ndarray, h: list[float], devices=None) -> np.ndarray:
+    """Every row of an H x W image through the ideal model in one launch.  A non-uint8 image
+    is prepared row by row as the reference's per-row ``fir_1d_ideal(row.tolist(), h)`` calls
+    would (gen_ideal_output.py:40-42): h is checked first, then rows in order, each non-finite
+    sample reported with its index in its row (fir_1d_ref._prepare_rows_u8)."""
     height, width = x_u8.shape
     if height == 0:
         return np.zeros((0, width), dtype=np.float64)
     _validate_h_coefficients(h)
+    xc = _prepare_rows_u8(x_u8)
     if width == 0:
         return np.zeros((height, 0), dtype=np.float64)
     devs = fir_hip.parse_devices(devices)
-    return fir_hip.fir1d_ideal_rows(np.ascontiguousarray(x_u8, dtype=np.uint8), [float(v) for v in h],
+    return fir_hip.fir1d_ideal_rows(xc, [float(v) for v in h],
                                     device=devs[0], devices=devs if len(devs) > 1 else None)
 
 
