@@ -70,6 +70,7 @@ SIMPLE_LP3 = [1024, 2048, 1024]              # h_coeff_3tap_map["simple_lp"] in 
 SIMPLE_LP5 = [256, 1024, 1536, 1024, 256]    # h_coeff_5tap_map["simple_lp"] in Q4.12
 SHARPEN5_F64 = [-1 / 16, -4 / 16, 26 / 16, -4 / 16, -1 / 16]  # h_coeff_5tap_map["sharpen"]
 BANK3 = [[1365] * 3, [1024, 2048, 1024], [-4096, 0, 4096], [-512, 5120, -512]]  # h_coeff_3tap_map, Q4.12
+BANK3_NAMES = ("moving_avg", "simple_lp", "edge", "sharpen")  # the bank's order (h_coeff.py:3-8)
 ROW_W = 4096
 # FIR_SELF_HALO=1 (N = 1 only): post the RCCL halo exchange every step with the segment as its
 # own neighbour (a ring of one), so the sharded step's exchange + edge kernel run and are timed
@@ -88,8 +89,9 @@ GATE_MODE = os.environ.get("FIR_GATE_MODE", "serial")
 KERNELS = {"fir1d_i16": "fir1d_reg_kernel", "cplx_i16": "fir1d_reg_kernel", "fir2d_u8": "fir2d_pk16_strip_kernel",
            "fir1d_u8": "fir1d_reg_kernel", "ideal_u8": "fir1d_ideal_kernel", "bank_u8": "fir1d_reg_kernel",
            "restore_u8": "restore_map_kernel",
+           "pipeline_fixed3": "fir1d_reg_kernel (4-filter bank, one launch per image, 7 launches in one hipGraph)",
            "metrics_u8": "metrics_leaf_kernel<true> (+ progress-word reset; chain and final in the launch)"}
-NUMPY_ONLY = ("restore_u8", "metrics_u8")  # no C oracle leg: the NumPy restatement is the CPU baseline
+NUMPY_ONLY = ("restore_u8", "metrics_u8", "pipeline_fixed3")  # no C oracle leg: the NumPy restatement is the CPU baseline
 ROOF_RAMP, ROOF_LAUNCHES = 100, 200  # roofline loop: untimed ramp, then timed launches of the dominant kernel
 
 
@@ -234,6 +236,24 @@ class Workload:
             self.dtype = "f64 in, u8 out (rint, clip)"
             self.config = {"workload": "restore_f64_to_u8_clip_rows4096", "samples_per_gpu": self.n,
                            "parallelism": "single GPU (replicas when N > 1)"}
+        elif name == "pipeline_fixed3":
+            # configs[0]: the fixed 3-tap stage of pipeline_fir_1d.py on the 7 golden images (the
+            # reference's decoded u8 inputs, tests/golden/images_u8.npz) x the 4 filters of
+            # h_coeff_3tap_map: one fused 4-filter launch per image, the 7 launches captured once
+            # into a hipGraph (torch.cuda.CUDAGraph) and replayed as one step
+            with np.load(ROOT / "tests" / "golden" / "images_u8.npz") as d:
+                self.images = [(k, np.ascontiguousarray(d[k])) for k in sorted(d.files)]
+            self.x_host = self.images[0][1]
+            px = sum(a.size for _, a in self.images)
+            self.units = px * len(BANK3)  # output samples per stage (67,975,252)
+            self.bytes_per_unit = (1 + len(BANK3)) / len(BANK3)  # 1 B in per pixel, 1 B out per output
+            self.unit = "Gsamples/s"
+            self.dtype = "int32 (u8 in, int32 wrap-around acc, u8 saturated out x 4 filters)"
+            self.config = {"workload": "pipeline_fixed_3tap_stage_7_golden_images_x4_filters",
+                           "images": len(self.images), "pixels": px, "filters": len(BANK3),
+                           "output_samples": self.units, "parallelism": "single GPU (replicas when N > 1)",
+                           "note": "85 MB per stage fits the 256 MB Infinity Cache: frac is against HBM peak "
+                                   "but replays may be served partly from the MALL"}
         elif name == "metrics_u8":
             self.n = 1 << log2n
             self.x_host = rng.uniform(-64.0, 320.0, self.n)  # ideal-output-like f64
@@ -248,7 +268,12 @@ class Workload:
                            "parallelism": "single GPU (replicas when N > 1)"}
         else:
             raise SystemExit(f"unknown workload {name}")
-        if name == "fir2d_u8":  # the resident batch of frames
+        self.graph = None
+        if name == "pipeline_fixed3":
+            self.xs = [torch.from_numpy(a).to(dev) for _, a in self.images]
+            self.ys = [torch.empty((len(BANK3),) + a.shape, dtype=torch.uint8, device=dev) for _, a in self.images]
+            self.x, self.y = self.xs[0], self.ys[0]
+        elif name == "fir2d_u8":  # the resident batch of frames
             self.x = torch.from_numpy(self.frames_host).to(dev)
             self.y = torch.empty(self.x.shape, dtype=torch.uint8, device=dev)
         else:
@@ -272,8 +297,25 @@ class Workload:
         # FIR_SELF_HALO=1 rehearses the RCCL exchange at N = 1 (the segment is its own neighbour)
         return (self.world > 1 or SELF_HALO) and self.name in ("fir1d_i16", "cplx_i16")
 
+    @property
+    def alg_bytes(self) -> int:
+        """Algorithmic bytes of one step (in + out bytes per unit x units)."""
+        return int(round(self.units * self.bytes_per_unit))
+
+    def _bank_images(self):
+        for x, y in zip(self.xs, self.ys):
+            torch_ops.fir1d_fixed_rows_multi_dev(x, BANK3, 12, 32, fir_hip.OUT_U8_SAT, out=y)
+
     def bulk(self):
-        if self.name == "fir2d_u8":
+        if self.name == "pipeline_fixed3":
+            if self.graph is None:  # capture the 7 launches once (warmed outside the capture)
+                self._bank_images()
+                torch.cuda.current_stream().synchronize()
+                self.graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.graph, stream=torch.cuda.current_stream()):
+                    self._bank_images()
+            self.graph.replay()
+        elif self.name == "fir2d_u8":
             torch_ops.fir2d_fixed_dev(self.x, self.hq2, 12, 32, fir_hip.OUT_U8_SAT, out=self.y)
         elif self.name == "ideal_u8":
             torch_ops.fir1d_ideal_rows_dev(self.x, SHARPEN5_F64, out=self.y)
@@ -349,7 +391,10 @@ class Workload:
         co = c_oracle()
         out = None
         for _ in range(reps):
-            if self.name == "fir2d_u8":
+            if self.name == "pipeline_fixed3":
+                out = [np.stack([co.fir1d_rows(a, h, 12, 32, co.OUT_U8_SAT, nthreads=nthreads) for h in BANK3])
+                       for _, a in self.images]
+            elif self.name == "fir2d_u8":
                 out = np.stack([co.fir2d(f, self.hq2, 12, 32, co.OUT_U8_SAT, nthreads=nthreads)
                                 for f in self.frames_host])
             elif self.name == "ideal_u8":
@@ -385,7 +430,16 @@ class Workload:
 
         if nthreads <= 1:
             return self.numpy_oracle(max_units)
-        if self.name in ("fir1d_i16", "cplx_i16"):
+        if self.name == "pipeline_fixed3":  # the 28 (image, filter) outputs over the pool
+            def job(i):
+                done = 0
+                for k, (_, a) in enumerate(self.images):
+                    for f, h in enumerate(BANK3):
+                        if (k * len(BANK3) + f) % nthreads == i:
+                            fo.fir1d_rows(a, h, 12, 32, fo.OUT_U8_SAT)
+                            done += a.size
+                return done
+        elif self.name in ("fir1d_i16", "cplx_i16"):
             n = min(self.units, max_units)
             ch = self.channels
             hl, hr = fo.halo_sizes(self.taps.n)
@@ -414,6 +468,11 @@ class Workload:
         the row workloads); returns the units done."""
         from oracle import fir_oracle as fo
 
+        if self.name == "pipeline_fixed3":  # whole stage (all 28 outputs), whatever max_units is
+            for _, a in self.images:
+                for h in BANK3:
+                    fo.fir1d_rows(a, h, 12, 32, fo.OUT_U8_SAT)
+            return self.units
         if self.name == "fir2d_u8":
             r0 = offset // self.w
             rows = max(1, min(self.h - r0, max_units // self.w))
@@ -442,12 +501,212 @@ class Workload:
         fo.fir1d_i16_i32(self.x_host[offset * c:(offset + n) * c], self.taps.h, 12, 32, channels=c)
         return n
 
+    def matches_reference(self) -> bool:
+        """pipeline_fixed3: the 28 outputs' SHA-256 against the reference's own (recorded by
+        tests/golden/make_golden.py from gen_fixed_output._run_fixed_rowwise)."""
+        import hashlib
+
+        outs = json.loads((ROOT / "tests" / "golden" / "image_outputs.json").read_text())["outputs"]
+        want = {(o["case_stem"], o["coeff_name"]): o["fixed_u8_sha256"] for o in outs if o["tap"] == "3tap"}
+        names = list(BANK3_NAMES)
+        for (stem, _), y in zip(self.images, self.ys):
+            yh = y.cpu().numpy()
+            for f, name in enumerate(names):
+                if hashlib.sha256(np.ascontiguousarray(yh[f]).tobytes()).hexdigest() != want[(stem, name)]:
+                    return False
+        return True
+
     def matches(self, ref) -> bool:
         """Full-output parity: every output, and every report metric, bit for bit."""
+        if self.name == "pipeline_fixed3":
+            return all(np.array_equal(y.cpu().numpy(), r) for y, r in zip(self.ys, ref)) and self.matches_reference()
         got = self.y.cpu().numpy()
         if self.name != "metrics_u8":
             return bool(np.array_equal(got, ref))
         return fir_hip.metrics_from_sums(got, self.n) == ref
+
+
+def measure(wl: Workload, steps: int, warmup: int, ramp: int, launches: int, world: int = 1,
+            barrier=lambda: None, red_dev=None):
+    """Time ``steps`` steps after ``warmup`` untimed ones (barrier + synchronize on both sides, max
+    over ranks), then the dominant kernel alone: ``ramp`` untimed launches (clocks ramp over ~40),
+    then ``launches`` back to back on the stream it runs on, bracketed by two HIP events (events
+    between launches would perturb the stream: each record adds a ~11 us gap).  Leaves the full
+    step's output in place.  Returns (elapsed s, host issue s, mean dominant-kernel s)."""
+    for _ in range(warmup):
+        wl.step()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        wl.step()
+    t_issue = time.perf_counter() - t0  # host time to issue the steps (diagnostic: host-bound?)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n_roof = max(1, launches)
+    for _ in range(max(0, ramp)):
+        wl.dominant()
+    torch.cuda.synchronize()
+    ev0.record()
+    for _ in range(n_roof):
+        wl.dominant()
+    ev1.record()
+    ev1.synchronize()
+    kern_avg_s = ev0.elapsed_time(ev1) / 1e3 / n_roof
+    wl.step()  # restore the full step's output (the loop above ran the dominant kernel alone)
+    torch.cuda.synchronize()
+    return elapsed, t_issue, kern_avg_s
+
+
+def _sync() -> None:
+    if torch.cuda.is_available():  # (the CPU tests drive the collective helpers below over gloo)
+        torch.cuda.synchronize()
+
+
+def gather_floats(v: float, world: int, red_dev) -> list[float]:
+    """Every rank's value of ``v`` (collective)."""
+    if world == 1:
+        return [v]
+    t = torch.tensor([v], dtype=torch.float64, device=red_dev)
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return [float(p.item()) for p in parts]
+
+
+def halo_report(wl: Workload, world: int, barrier, red_dev, n: int = 100) -> dict:
+    """config.halo of a sharded run (collective: every rank runs it after the timed steps): the
+    halo source, why RCCL was chosen if it was, and what the hand-off alone costs per step --
+    the xGMI gate kernel timed by HIP events around ``n`` back-to-back gates on the step stream
+    (every rank runs the same count, so every wait is met), or RCCL's post + wait timed on the
+    host -- as the max and min over ranks."""
+    src = wl.halo_src
+    info = {"source": wl.halo_kind}
+    if wl.halo_kind == "xgmi":
+        info["gate_mode"] = GATE_MODE
+        barrier()
+        _sync()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        for _ in range(n):
+            src.gate()
+        ev1.record()
+        ev1.synchronize()
+        per = gather_floats(ev0.elapsed_time(ev1) * 1e3 / n, world, red_dev)
+        info["gate_us_per_step"] = {"max": round(max(per), 2), "min": round(min(per), 2),
+                                    "timing": f"HIP events around {n} gate launches alone"}
+    else:
+        info["fallback_reason"] = getattr(src, "fallback_reason", None)
+        barrier()
+        _sync()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            sharded.wait_all(src.post())
+        _sync()
+        per = gather_floats((time.perf_counter() - t0) * 1e6 / n, world, red_dev)
+        info["exchange_us_per_step"] = {"max": round(max(per), 2), "min": round(min(per), 2),
+                                        "timing": f"host clock around {n} post + wait alone"}
+    barrier()
+    return info
+
+
+def gate_failures(wl: Workload, world: int, red_dev) -> list[int]:
+    """Ranks whose gated hand-off timed out in this run (collective; [] for other sources).  The
+    gate's waits are bounded (timeout_s), so this is reached even when a neighbour never
+    published: the run then ends with a line and a non-zero status instead of hanging."""
+    bad = int(isinstance(wl.halo_src, sharded.XgmiHalo) and int(wl.halo_src.status.item()) != 0)
+    flags = gather_floats(float(bad), world, red_dev)
+    return [r for r, f in enumerate(flags) if f]
+
+
+def pmc_traffic(wl: Workload):
+    """HBM bytes per launch (per step for pipeline_fixed3) from the committed rocprofv3 PMC summary
+    profiles/pmc_<workload>.json, when it was taken at this workload's size; else None."""
+    pmc = ROOT / "profiles" / f"pmc_{wl.name}{'_gen5x5' if wl.gen2d else ''}.json"
+    if not pmc.exists():
+        return None
+    try:
+        summary = json.loads(pmc.read_text())
+    except (ValueError, OSError):
+        return None
+    if summary.get("algorithmic_bytes_per_launch") == wl.alg_bytes:
+        return summary.get("hbm_bytes_per_launch")
+    return None
+
+
+# The other single-GPU BASELINE configs, timed after the headline when bench.py runs without
+# --workload at N = 1 (the driver's own run): configs[2] complex int16 2^27, configs[4] fir_2d 5x5
+# on 8192^2 frames, configs[0] the pipeline's fixed 3-tap stage on the 7 golden images.
+SUB_CONFIGS = (("configs[2]", "cplx_i16"), ("configs[4]", "fir2d_u8"), ("configs[0]", "pipeline_fixed3"))
+
+
+def pipeline_stage_wall(reps: int = 3) -> dict:
+    """configs[0] end to end through the host API, as pipeline_fir_1d.py runs it:
+    generate_fixed_3tap_output_vector over the 7 golden images in a scratch input dir (np.load,
+    H2D, the fused bank launch, D2H, np.save of 28 .npy files).  Best of ``reps`` runs."""
+    import tempfile
+
+    from fir_1d.sim.vector.gen_fixed_output import generate_fixed_3tap_output_vector
+
+    with tempfile.TemporaryDirectory(prefix="fir_stage_") as tmp:
+        ind, outd = Path(tmp) / "input", Path(tmp) / "output"
+        ind.mkdir()
+        with np.load(ROOT / "tests" / "golden" / "images_u8.npz") as d:
+            for k in d.files:
+                np.save(ind / f"{k}_x_u8.npy", d[k])
+        best, n = float("inf"), 0
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            n = generate_fixed_3tap_output_vector(input_dir=ind, output_dir=outd, overwrite=True)
+            best = min(best, time.perf_counter() - t0)
+    return {"ms": round(best * 1e3, 2), "files": n,
+            "what": "generate_fixed_3tap_output_vector (host API, .npy in -> 28 .npy out incl. H2D/D2H and "
+                    f"file I/O), best of {reps}; the reference's own CPU stage took 92.6 s (SURVEY §3.1)"}
+
+
+def run_sub_configs(args, dev) -> tuple[dict, bool]:
+    """Each SUB_CONFIGS workload on its own: step rate, dominant-kernel roofline, PMC traffic when a
+    matching summary is committed, full-output parity against the C oracle (configs[0] also
+    against the reference's own output digests), and the C oracle's rate as its CPU baseline."""
+    out, all_ok = {}, True
+    nthr = _cpu_threads()
+    for label, name in SUB_CONFIGS:
+        wl = Workload(name, 0, 1, dev, args.log2n)
+        torch.cuda.synchronize()
+        elapsed, _, kern = measure(wl, args.steps, args.warmup, args.roofline_ramp, args.roofline_launches)
+        tc0 = time.perf_counter()
+        ref = wl.oracle(nthr)
+        tc = time.perf_counter() - tc0
+        ok = wl.matches(ref)
+        all_ok &= ok
+        achieved = wl.alg_bytes / kern / 1e9
+        entry = {
+            "workload": wl.config["workload"], "value": round(wl.units * args.steps / elapsed / 1e9, 3),
+            "unit": wl.unit, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "dtype": wl.dtype,
+            "config": wl.config,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(wl),
+                         "kernel": KERNELS[name], "kernel_avg_us": round(kern * 1e6, 2),
+                         "algorithmic_bytes_per_launch": wl.alg_bytes},
+            "parity": ("bit-exact vs oracle (full output)" + (" and the reference's 28 output SHA-256s"
+                                                              if name == "pipeline_fixed3" else ""))
+            if ok else "MISMATCH",
+            "cpu_baseline": {"value": round(wl.units / tc / 1e9, 4), "unit": wl.unit, "cores": nthr, "kind": "port",
+                             "sample": f"C oracle (oracle/fir_oracle.c, OpenMP {nthr} threads), the parity run on the "
+                                       f"full workload ({wl.units} units), {tc:.2f} s"},
+        }
+        if name == "pipeline_fixed3":
+            entry["roofline"]["kernel_avg_us_is"] = "one graph replay = 7 launches (one stage)"
+            entry["stage_wall"] = pipeline_stage_wall()
+        out[label] = entry
+        del wl, ref
+        torch.cuda.empty_cache()
+    return out, all_ok
 
 
 def main() -> int:
@@ -455,7 +714,10 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=100, help="untimed steps (clocks take ~40 launches to ramp)")
-    ap.add_argument("--workload", default="fir1d_i16", choices=tuple(KERNELS))
+    ap.add_argument("--workload", default=None, choices=tuple(KERNELS),
+                    help="default fir1d_i16 (configs[1]); without this flag an N = 1 run also times "
+                         "configs[2], [4] and [0] (the line's 'configs' key)")
+    ap.add_argument("--no-configs", action="store_true", help="time the headline workload only")
     ap.add_argument("--log2n", type=int, default=28, help="int16 values per GPU (2^28 = BASELINE configs[1])")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0 = skip)")
     ap.add_argument("--no-parity", action="store_true", help="skip the full-size oracle comparison")
@@ -463,6 +725,8 @@ def main() -> int:
                     help="timed launches of the dominant kernel (after as many as --roofline-ramp untimed)")
     ap.add_argument("--roofline-ramp", type=int, default=ROOF_RAMP)
     args = ap.parse_args()
+    sub_configs = args.workload is None and not args.no_configs and not SELF_HALO
+    args.workload = args.workload or "fir1d_i16"
 
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
@@ -519,42 +783,22 @@ def main() -> int:
                 dist.barrier()
 
     barrier()  # every rank's segment is resident and its communicator up before the first step
-    for _ in range(args.warmup):
-        wl.step()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        wl.step()
-    t_issue = time.perf_counter() - t0  # host time to issue the steps (diagnostic: host-bound?)
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    # Roofline: the dominant kernel alone (wl.dominant), ROOF_RAMP untimed launches (clocks ramp over
-    # ~40) then ROOF_LAUNCHES back-to-back launches on the stream it runs on, bracketed by two HIP
-    # events (events between launches would perturb the stream: each record adds a ~11 us gap).
-    # Average duration = event time / launches.  Independent of --steps / --warmup.
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    elapsed, t_issue, kern_avg_s = measure(wl, args.steps, args.warmup, args.roofline_ramp, args.roofline_launches,
+                                           world, barrier, red_dev)
     n_roof = max(1, args.roofline_launches)
-    for _ in range(max(0, args.roofline_ramp)):
-        wl.dominant()
-    torch.cuda.synchronize()
-    ev0.record()
-    for _ in range(n_roof):
-        wl.dominant()
-    ev1.record()
-    ev1.synchronize()
-    kern_avg_s = ev0.elapsed_time(ev1) / 1e3 / n_roof
-
-    wl.step()  # restore the full step's output (the loop above ran the bulk kernel alone)
-    torch.cuda.synchronize()
-    if isinstance(wl.halo_src, sharded.XgmiHalo):
-        wl.halo_src.check()  # every gate's wait arrived (raises otherwise)
+    kern_ranks = gather_floats(kern_avg_s, world, red_dev)
+    halo = halo_report(wl, world, barrier, red_dev) if wl.sharded_1d and world > 1 else None
+    failed = gate_failures(wl, world, red_dev) if wl.sharded_1d else []
+    if failed:
+        if rank == 0:
+            timeout = wl.halo_src.timeout_s
+            emit_result(json.dumps({"metric": METRIC, "value": None, "unit": wl.unit, "n_gpus": world,
+                                    "error": f"halo gate timed out (a neighbour's epoch did not arrive within "
+                                             f"{timeout} s) on rank(s) {failed}", "config": wl.config}))
+        print(f"bench.py: halo gate timed out on rank(s) {failed}", file=sys.stderr)
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        return 3
 
     # parity: full output vs the C oracle (every rank, its own segment with the received halos)
     parity = "skipped"
@@ -612,19 +856,11 @@ def main() -> int:
 
     barrier()  # rank 0's CPU legs are done
 
-    traffic = None
-    pmc = ROOT / "profiles" / f"pmc_{args.workload}{'_gen5x5' if wl.gen2d else ''}.json"
-    if pmc.exists():
-        try:
-            summary = json.loads(pmc.read_text())
-        except (ValueError, OSError):
-            summary = {}
-        if summary.get("algorithmic_bytes_per_launch") == wl.units * wl.bytes_per_unit:
-            traffic = summary.get("hbm_bytes_per_launch")  # only for the profiled workload size
+    traffic = pmc_traffic(wl)
 
     total_units = wl.units * world * args.steps
     value = total_units / elapsed / 1e9
-    alg_bytes = wl.units * wl.bytes_per_unit
+    alg_bytes = wl.alg_bytes
     achieved = alg_bytes / kern_avg_s / 1e9
     line = {
         "metric": METRIC if args.workload == "fir1d_i16" else f"{wl.unit}, {wl.config['workload']}",
@@ -649,6 +885,8 @@ def main() -> int:
                                  "strips share are read once, PMC 1.001x; DESIGN.md §5)")
                      if args.workload == "fir2d_u8" else "HBM",
                      "kernel_avg_us": round(kern_avg_s * 1e6, 2), "algorithmic_bytes_per_launch": alg_bytes,
+                     "kernel_avg_us_ranks": {"max": round(max(kern_ranks) * 1e6, 2),
+                                             "min": round(min(kern_ranks) * 1e6, 2)},
                      "timing": f"HIP events around {n_roof} back-to-back launches of the kernel after "
                                f"{max(0, args.roofline_ramp)} untimed ones"},
         "cpu_baseline": cpu,
@@ -662,9 +900,14 @@ def main() -> int:
         line["config"] = dict(line["config"], rehearsal=(
             f"{os.environ['FIR_BENCH_REHEARSAL']}: gloo process group, ranks share the GPU's HBM; not a "
             "scaling number"))
+    if halo is not None:
+        line["config"] = dict(line["config"], halo=halo)
     if wl.sharded_1d and world == 1:
         line["config"] = dict(wl.config, rehearsal=f"FIR_SELF_HALO=1: {wl.halo_kind} halo hand-off with itself every "
                                                     f"step (ring of one), gate mode {GATE_MODE}")
+    subs_ok = True
+    if sub_configs and world == 1:
+        line["configs"], subs_ok = run_sub_configs(args, dev)
     if rank == 0:
         emit_result(json.dumps(line))
     if dist.is_initialized():
@@ -673,7 +916,7 @@ def main() -> int:
         if isinstance(wl.halo_src, sharded.XgmiHalo):
             wl.halo_src.close()
         dist.destroy_process_group()
-    return 0 if parity != "MISMATCH" else 1
+    return 0 if parity != "MISMATCH" and subs_ok else 1
 
 
 if __name__ == "__main__":

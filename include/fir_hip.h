@@ -170,7 +170,8 @@ int fir1d_ideal_rows_dev(const uint8_t* x_dev, int64_t rows, int64_t width, cons
  * the reference's np.mean values bit for bit; counts are exact; max|d| is NaN when any |d| is
  * (np.max propagates NaN).  `work_dev` of the _dev form holds at least fir_metrics_work_bytes(n)
  * bytes.  status (out[8]) is 0; 1 means the one-launch pass's in-kernel hand-off gave up waiting
- * (about 1 s; no correct run reaches it): the sums are then NaN, and fir_compare_metrics returns
+ * (10 s after the launch starts, on the GPU's 100 MHz clock; no correct run comes near it): the
+ * sums are then NaN, and fir_compare_metrics returns
  * FIR_EHIP.  ABI 4: the fixed dtype argument. */
 typedef enum {
     FIR_DT_U8 = 0, FIR_DT_I8 = 1, FIR_DT_U16 = 2, FIR_DT_I16 = 3, FIR_DT_U32 = 4, FIR_DT_I32 = 5,

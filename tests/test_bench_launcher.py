@@ -98,3 +98,68 @@ def test_bench_script_runs_launcher_end_to_end(tmp_path):
                         "--cpu-seconds", "0"], capture_output=True, text=True, timeout=300)
     assert p.returncode != 0
     assert p.stdout == ""
+
+
+def _halo_report_worker(rank, world, port, q):
+    import os
+    import sys
+
+    sys.path[:0] = [str(ROOT), str(ROOT / "warmup-fir-filter_amd")]
+    import torch
+    import torch.distributed as dist
+
+    import bench as b
+    from fir_hip import sharded
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        seg = torch.arange(rank * 100, rank * 100 + 40, dtype=torch.int16)
+
+        class WL:  # the fields halo_report / gate_failures read
+            pass
+
+        wl = WL()
+        wl.halo_kind, wl.halo_src = sharded.make_halo_source(seg, 5)  # CPU tensors: RCCL path, with a reason
+        info = b.halo_report(wl, world, dist.barrier, torch.device("cpu"), n=5)
+
+        class StuckGate(sharded.XgmiHalo):  # a gate whose status word says "timed out" on rank 1
+            def __init__(self):
+                self.status = torch.tensor([1 if rank == 1 else 0], dtype=torch.int32)
+                self.timeout_s = 10.0
+
+        wl.halo_src = StuckGate()
+        failed = b.gate_failures(wl, world, torch.device("cpu"))
+        ranks = b.gather_floats(float(rank) + 0.5, world, torch.device("cpu"))
+        q.put((rank, info, failed, ranks))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_halo_report_and_gate_failures_over_gloo():
+    """The N > 1 bench line explains itself: config.halo names the source, why RCCL was chosen and
+    the hand-off's own per-step cost (max / min over ranks); a timed-out gate on any rank is seen
+    by every rank (the run then ends with a line and status 3, not a hang)."""
+    import multiprocessing as mp
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_halo_report_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    got = dict((r, (i, f, k)) for r, i, f, k in (q.get(timeout=5) for _ in range(2)))
+    for r in (0, 1):
+        info, failed, ranks = got[r]
+        assert info["source"] == "rccl"
+        assert info["fallback_reason"].startswith("rank 0: ")
+        assert set(info["exchange_us_per_step"]) == {"max", "min", "timing"}
+        assert info["exchange_us_per_step"]["max"] >= info["exchange_us_per_step"]["min"] > 0
+        assert failed == [1]
+        assert ranks == [0.5, 1.5]

@@ -168,6 +168,8 @@ def _fallback_worker(rank, world, port, q):
         sharded.wait_all(src.post())
         left, right = src.halos()
         ok = kind == "rccl" and isinstance(src, sharded.HaloExchange)
+        # every rank carries the same reason: the first refusing rank and its error
+        ok &= src.fallback_reason.startswith("rank 0: ") and "XgmiHalo needs a contiguous device segment" in src.fallback_reason
         if rank > 0:
             ok &= left.tolist() == list(range((rank - 1) * 100 + 38, (rank - 1) * 100 + 40))
         q.put((rank, ok))

@@ -14,18 +14,22 @@
 // with the elements past the last multiple of 8 added in order; larger n split at
 // n2 = floor(n/2) rounded down to a multiple of 8, sum = pw(left) + pw(right).
 //
-//   pass 1 (metrics_blocks): one wave per full 8192-sample block, grid-stride; a full block is
-//     a balanced tree of 64 leaves of 128: 8 rounds of 8 leaves, each round loaded as contiguous
-//     1 KiB rows and transposed through the wave's LDS so that lane (leaf, j) adds accumulator
-//     r[j]'s 16 terms in order; the leaf and round trees by DPP row shifts and permlane swaps (IEEE
-//     addition is commutative, so a lane adding its partner's value matches either order); counts
-//     and max per workgroup.  metrics_ragged: the ragged last block by the general recursion
-//     (leaves enumerated, summed one per thread, recombined in post-order).
-//   the chain: waves 0-2 of one workgroup add the block sums of |d|, d^2 and d in order (a
-//     dependent float64 chain, 2.7 ns per block).  The full blocks are split into parts of one
-//     launch each (8192 blocks, the last 2048), and the chain over part k-1 runs as an extra
-//     workgroup of the launch that streams part k, so only the last part's chain is exposed;
-//     metrics_final adds the last part (and the ragged block) and reduces the counts and max.
+// A full 8192-sample block is a balanced tree of 64 leaves of 128 samples; its sums are
+// reduced by one wave, the block sums then added in order by a dependent float64 chain (waves
+// 0-2 of one workgroup: |d|, d^2, d; 2.7 ns per block).  Two forms:
+//   16-byte aligned u8 (the pipeline's case): metrics_ragged zeroes the hand-off words and sums
+//     the ragged last block, then ONE launch of metrics_leaf_kernel: one lane per leaf (the leaf
+//     combine in registers, the block tree by DPP row shifts and permlane swaps -- IEEE addition
+//     is commutative, so a lane adding its partner's value matches either order), each block's
+//     sums published to workgroup 0, which follows them (chain_follow) and finishes the call
+//     (final_in_launch) inside the same launch.
+//   any other dtype or alignment: the full blocks in parts of one launch each (8192 blocks, the
+//     last 2048) of metrics_blocks (u8: 8 rounds of 8 leaves, transposed through the wave's LDS
+//     so that lane (leaf, j) adds accumulator r[j]'s 16 terms in order) or metrics_blocks_any
+//     (stride-8 loads, not a bandwidth path); the chain over part k-1 runs as an extra workgroup
+//     of the launch streaming part k; metrics_ragged sums the ragged block by the general
+//     recursion (leaves enumerated, summed one per thread, recombined in post-order), and
+//     metrics_final adds the last part and reduces the counts and max.
 #include <string>
 #include <type_traits>
 
@@ -34,24 +38,10 @@
 
 namespace fir {
 
-#ifndef FIR_METRIC_BLOCKS  // workgroups per part launch at most (512: each wave streams 4 blocks
-#define FIR_METRIC_BLOCKS 512  // of an 8192-block part; 2^28: 453 -> 430 us vs 2048, 4096 slower)
-#endif
-constexpr int kMetricBlocks = FIR_METRIC_BLOCKS;
-#ifndef FIR_METRIC_GLDS  // 1: the LDS-DMA double-buffered block pass (metrics_blocks_glds; A/B:
-#define FIR_METRIC_GLDS 0   // 446.6 vs 429.9 us for the register-staged pass, profiles/r04/metrics_glds_ab.txt)
-#endif
-constexpr bool kMetricGlds = FIR_METRIC_GLDS;
-#ifndef FIR_METRIC_LEAF  // 1: one lane per leaf (metrics_leaf_kernel)
-#define FIR_METRIC_LEAF 1
-#endif
-constexpr bool kMetricLeaf = FIR_METRIC_LEAF;
-#ifndef FIR_METRIC_EXP  // timing experiments (wrong sums): 1 no chain in the part launches,
-#define FIR_METRIC_EXP 0  // 2 no count reduction in metrics_final, 3 no chain in metrics_final,
-#endif                    // 4 no chain in the publishing launch, 5 = 4 with plain block-sum stores
-#ifndef FIR_METRIC_MINB  // waves per SIMD the block kernel's registers must allow
-#define FIR_METRIC_MINB 4
-#endif
+// Launch shapes (the forms measured against these and removed in round 5 are listed, with their
+// numbers)
+constexpr int kMetricBlocks = 512;  // workgroups per part launch at most (each wave streams 4 blocks
+                                    // of an 8192-block part; 2^28: 453 -> 430 us vs 2048, 4096 slower)
 constexpr int kPwBlock = 8192;   // NumPy's ufunc buffer (NPY_BUFSIZE elements)
 constexpr int kPwLeaf = 128;     // pairwise_sum's PW_BLOCKSIZE
 constexpr int kPwMaxLeaves = 128;  // leaves of a block shorter than 8192 (each >= 64 samples)
@@ -169,17 +159,8 @@ __device__ void block_counts(Cnt c, Cnt* dst) {
 // a VGPR operand per 8192 samples (2.7 ns; fed by v_readlane instead: 8.7 ns,
 // tools/microbench/chain_micro.hip).  `lds` holds 3 x kChainDepth x 64 doubles; no workgroup
 // barrier inside.
-#ifndef FIR_METRIC_ONEPOLL
-#define FIR_METRIC_ONEPOLL 1
-#endif
-#ifndef FIR_METRIC_CHAIN_D  // block sums per lane of a chain group (a group = 64 x this)
-#define FIR_METRIC_CHAIN_D 8
-#endif
-constexpr int kChainDepth = FIR_METRIC_CHAIN_D;
-#ifndef FIR_METRIC_CHAIN_NG  // groups of block sums chain_follow checks and takes per batch
-#define FIR_METRIC_CHAIN_NG 1
-#endif
-constexpr int kChainGroups = FIR_METRIC_CHAIN_NG;
+constexpr int kChainDepth = 8;   // block sums per lane of a chain group (a group = 64 x this)
+constexpr int kChainGroups = 1;  // groups of block sums chain_follow checks and takes per batch
 constexpr int kChainLds = 3 * kChainDepth * kWave * (int)sizeof(double);
 constexpr int kChainGS = kChainDepth * kWave;  // block sums per group
 // s += sh[0], sh[1], ..., sh[len - 1] in order (sh: a staged group in the wave's LDS)
@@ -253,21 +234,26 @@ __device__ __forceinline__ void chain_range(const double* __restrict__ bsum, int
     }
 }
 
-// The chain inside the launch that produces the block sums (metrics_leaf_kernel<true>).  Streaming
-// wave w takes blocks w, w + nw, w + 2 nw, ... (nw waves) and publishes them in that order: the
-// three sums of a block by write-through (sc1) stores, then -- one round later, once the wave's
-// next band has landed, which drains those stores (vmcnt retires in order) -- its progress word
-// prog[w] = blocks done, by an sc1 store (no read-modify-write: 2048 waves adding to shared
-// counters serialised in the memory-side atomic unit, +114 us at 2^28, profiles/r04/metrics_publish_ab.txt).
-// Waves 0-2 of this workgroup follow: a group of kChainGS blocks is ready when every block's wave
-// has passed it; ONE wave-wide check of the next group's progress words (s_sleep
-// between polls, bounded), every further group already ready taken with it (up to kChainGroups),
-// then the sums, every read of a handed-off word by a returning atomic (coherent_read below).
-// Blocks [nbf, nb) (the ragged
-// block) were written by an earlier launch.  The chain's waves run at raised priority (a
-// dependent float64 add per block, sharing a SIMD with streaming waves).  A wait past the spin
-// bound (no correct run reaches it: the producers never wait) makes the sums NaN.
-constexpr uint32_t kChainSpinCap = 1u << 24;  // x (s_sleep 2 + a poll): ~1 s
+// The chain inside the launch that produces the block sums (metrics_leaf_kernel).  Streaming wave
+// w takes blocks w, w + nw, w + 2 nw, ... (nw waves) and publishes them in that order, as a
+// release/acquire hand-off at agent scope (the HIP memory model; the waves may sit on other
+// XCDs): the three sums of a block by relaxed agent-scope (write-through) stores, then -- one
+// round later, once the wave's next band has landed -- its progress word prog[w] = blocks done
+// by an agent-scope RELEASE store (gfx950: buffer_wbl2 sc1 + s_waitcnt vmcnt(0) + an sc1 store;
+// the sums are ordered before the word for every observer).  No read-modify-write: 2048 waves
+// adding to shared counters serialised in the memory-side atomic unit, +114 us at 2^28,
+// profiles/r04/metrics_publish_ab.txt.  Wave 0 of this workgroup polls: a group of kChainGS
+// blocks is ready when every block's wave has passed it (ONE wave-wide check of the group's
+// progress words per poll, s_sleep between polls); once it is, an agent-scope ACQUIRE fence
+// (buffer_inv sc1) makes the producers' releases happen-before the sum reads, and wave 0 posts
+// the group count to waves 1-2 by a workgroup-scope release store they read with acquire loads.
+// Every read of a handed-off word is also a returning atomic (coherent_read below).  Blocks
+// [nbf, nb) (the ragged block) were written by an earlier launch.  The chain's waves run at
+// raised priority (a dependent float64 add per block, sharing a SIMD with streaming waves).  The
+// waits share one deadline on the 100 MHz s_memrealtime clock, kChainTimeoutTicks after the
+// chain starts (no correct run comes near it: the producers never wait, and a 288 GB call
+// streams in ~50 ms); past it the sums are NaN and out[8] = 1.
+constexpr uint64_t kChainTimeoutTicks = 1000000000ull;  // 10 s
 typedef __attribute__((address_space(1))) uint64_t gu64;
 typedef __attribute__((address_space(1))) uint32_t gu32;
 // A read of a word another XCD wrote in this launch (or the memset before it) that no cache of the
@@ -324,38 +310,43 @@ __device__ __forceinline__ void chain_follow(const double* __restrict__ bsum, in
         }
         return k;
     };
-    // FIR_METRIC_ONEPOLL: only wave 0 polls the progress words and posts how many groups are
-    // complete in an LDS word that waves 1-2 watch (one third of the polling atomics)
+    // only wave 0 polls the progress words; it posts how many groups are complete in an LDS word
+    // that waves 1-2 watch (one third of the polling atomics)
     int* posted = reinterpret_cast<int*>(lds + kChainLds);  // (past the three staging areas)
     int* failed = reinterpret_cast<int*>(lds + kChainLds + 52);  // a chain wave gave up waiting
+    uint64_t* deadline = reinterpret_cast<uint64_t*>(lds + kChainLds + 56);  // shared with final_in_launch
     if (wv == 0 && lane == 0) {
         __hip_atomic_store(posted, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_store(failed, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        *deadline = __builtin_amdgcn_s_memrealtime() + kChainTimeoutTicks;
     }
-    __builtin_amdgcn_s_barrier();  // (every wave of the workgroup: the word is zero before anyone reads it)
+    __syncthreads();  // (every wave of the workgroup: the words are set before anyone reads them)
     if (wv >= 3) return;
+    const uint64_t dl = *deadline;
     __builtin_amdgcn_s_setprio(3);
     for (int64_t g = 0; g < ngr && ok;) {
         int k = 0;
-        for (uint32_t spins = 0;;) {
-            if (!FIR_METRIC_ONEPOLL || wv == 0) {
+        for (;;) {
+            if (wv == 0) {
                 k = ready_prefix(g);
-                if (FIR_METRIC_ONEPOLL && k > 0 && lane == 0)
-                    __hip_atomic_store(posted, (int)(g + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (k > 0) {
+                    // the producers' release stores (progress words) were read: their sums are visible
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    if (lane == 0) __hip_atomic_store(posted, (int)(g + k), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
             } else {
                 const int p = __builtin_amdgcn_readfirstlane(
-                    __hip_atomic_load(posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                    __hip_atomic_load(posted, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
                 k = p > g ? (int)min<int64_t>(p - g, NG) : 0;
             }
             if (k > 0) break;
-            if (++spins > kChainSpinCap) {
+            if (__builtin_amdgcn_s_memrealtime() > dl) {
                 ok = false;
                 break;
             }
             __builtin_amdgcn_s_sleep(2);
         }
         if (!ok) break;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the reads below the polls)
         double q[NG][D];
 #pragma unroll
         for (int i = 0; i < NG; ++i) {
@@ -423,8 +414,8 @@ __device__ __forceinline__ void fold_round(Term (&st)[4], int rd, const Term& t)
 constexpr int kMetRow = 1024 + 64;                      // LDS bytes per leaf row (+64: conflict-free reads)
 constexpr int kMetWaveLds = 8 * kMetRow + 1024;         // + the round's 1 KiB of fixed bytes
 static_assert(kBlock / kWave * kMetWaveLds >= kChainLds, "the chain's staging shares the wave buffers");
-template <bool VEC>
-__global__ __launch_bounds__(kBlock, FIR_METRIC_MINB) void metrics_blocks(const double* __restrict__ ideal,
+// (u8 arrays not 16-byte aligned: the aligned ones take metrics_leaf_kernel)
+__global__ __launch_bounds__(kBlock, 4) void metrics_blocks(const double* __restrict__ ideal,
                                                                          const uint8_t* __restrict__ fixed,
                                                                          double* __restrict__ bsum, int64_t nb,
                                                                          int64_t b_lo, int64_t b_hi, int64_t c_lo,
@@ -452,20 +443,12 @@ __global__ __launch_bounds__(kBlock, FIR_METRIC_MINB) void metrics_blocks(const 
         for (int rd = 0; rd < 8; ++rd) {
             const int64_t base = b * kPwBlock + rd * 1024;
             d2 v[8];
-            u4 fx;
-            if constexpr (VEC) {
 #pragma unroll
-                for (int i = 0; i < 8; ++i)
-                    v[i] = __builtin_nontemporal_load(reinterpret_cast<const d2*>(ideal + base + 128 * i) + lane);
-                fx = *reinterpret_cast<const u4*>(fixed + base + 16 * lane);
-            } else {
+            for (int i = 0; i < 8; ++i) v[i] = d2{ideal[base + 128 * i + 2 * lane], ideal[base + 128 * i + 2 * lane + 1]};
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-                for (int i = 0; i < 8; ++i) v[i] = d2{ideal[base + 128 * i + 2 * lane], ideal[base + 128 * i + 2 * lane + 1]};
-                uint32_t w[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-                for (int e = 0; e < 16; ++e) w[e / 4] |= (uint32_t)fixed[base + 16 * lane + e] << (8 * (e % 4));
-                fx = u4{w[0], w[1], w[2], w[3]};
-            }
+            for (int e = 0; e < 16; ++e) w[e / 4] |= (uint32_t)fixed[base + 16 * lane + e] << (8 * (e % 4));
+            const u4 fx = u4{w[0], w[1], w[2], w[3]};
             __builtin_amdgcn_wave_barrier();  // the previous round's reads are done (one wave: in order)
 #pragma unroll
             for (int i = 0; i < 8; ++i) *reinterpret_cast<d2*>(wl + i * kMetRow + 16 * lane) = v[i];
@@ -488,9 +471,8 @@ __global__ __launch_bounds__(kBlock, FIR_METRIC_MINB) void metrics_blocks(const 
             for (int s = 0; s < 16; ++s) {
                 double id = *reinterpret_cast<const double*>(row + 64 * s);
                 uint32_t f = (frw[s / 4] >> (8 * (s % 4))) & 0xFFu;
-#if !FIR_METRIC_OLD_NOASM  // (A/B only) the register form as round 3 shipped it: one LDS read per term
+                // opaque: one LDS read per term, as round 3 measured it (hipcc otherwise hoists all 16)
                 asm volatile("" : "+v"(id), "+v"(f), "+v"(mx), "+v"(lo), "+v"(hi), "+v"(clip));
-#endif
                 const Term t = metrics_term(id, f, mx, lo, hi, clip);
                 if (s == 0) r = t;
                 else tadd(r, t);
@@ -499,106 +481,6 @@ __global__ __launch_bounds__(kBlock, FIR_METRIC_MINB) void metrics_blocks(const 
         }
         const Term s = st[3];
         if (lane == 0) bsum[b] = s.a, bsum[nb + b] = s.q, bsum[2 * nb + b] = s.d;
-    }
-    block_counts(Cnt{mx, lo, hi, clip}, parts + wg);
-}
-
-// The same block pass with the rounds streamed by LDS-DMA (global_load_lds_dwordx4: a load that
-// writes the wave's LDS directly, holding no VGPRs while in flight), double-buffered: round t+1's
-// 8 KiB of ideal values and 1 KiB of fixed bytes are in flight while round t is reduced, so each
-// wave always has one round outstanding (the register-staged form above loads, waits, then
-// computes; prefetching into registers spilled, profiles/r03/metrics_exact_ab.txt).  A wave walks
-// its blocks' rounds as one sequence t (block t / 8 of the wave's grid-stride list, round t % 8).
-// Ordering: round t's 9 DMAs are the wave's oldest outstanding VMEM ops once round t+1's are
-// issued, so `s_waitcnt vmcnt(9)` retires exactly them (explicit: hipcc does not count LDS-DMA
-// for the ds_reads that follow); a buffer is refilled two rounds after its last ds_read, whose
-// results the VALU has consumed by then.  The fixed bytes land linearly and are transposed in
-// place (one ds_read_b128 per lane, all of the wave's reads before any of its writes).
-// LDS: 2 x (8 rows of 1 KiB + 64 B pad + 1 KiB fixed) per wave = 76 KiB per workgroup, 2 per CU.
-constexpr int kGRow = 1024 + 64;
-constexpr int kGBuf = 8 * kGRow + 1024;
-constexpr int kGWaveLds = 2 * kGBuf;
-static_assert(kBlock / kWave * kGWaveLds >= kChainLds, "the chain's staging shares the wave buffers");
-#ifndef FIR_METRIC_AUX  // cache policy of the DMA loads (2 = nt: every byte is read once)
-#define FIR_METRIC_AUX 2
-#endif
-__device__ __forceinline__ void glds16(const void* g, uint8_t* lds) {
-    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 16, 0, FIR_METRIC_AUX);
-}
-__global__ __launch_bounds__(kBlock, 2) void metrics_blocks_glds(const double* __restrict__ ideal,
-                                                                              const uint8_t* __restrict__ fixed,
-                                                                              double* __restrict__ bsum, int64_t nb,
-                                                                              int64_t b_lo, int64_t b_hi, int64_t c_lo,
-                                                                              int64_t c_hi, double* __restrict__ state,
-                                                                              Cnt* __restrict__ parts) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock / kWave * kGWaveLds];
-    const bool chain = c_hi > c_lo;
-    if (chain && blockIdx.x == 0) {
-        chain_range(bsum, nb, c_lo, c_hi, state, smem);
-        return;
-    }
-    const int wg = blockIdx.x - (chain ? 1 : 0);
-    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x >> 6;
-    const int k = lane >> 3, j = lane & 7;
-    uint8_t* wl = smem + wv * kGWaveLds;
-    const int64_t nwaves = (int64_t)(gridDim.x - (chain ? 1 : 0)) * (kBlock / kWave);
-    const int64_t b0 = b_lo + (int64_t)wg * (kBlock / kWave) + wv;
-    const int64_t nrounds = b0 < b_hi ? ((b_hi - 1 - b0) / nwaves + 1) * 8 : 0;
-    double mx = 0.0;
-    uint32_t lo = 0, hi = 0, clip = 0;
-
-    auto issue = [&](int64_t t) {
-        const int64_t base = (b0 + (t >> 3) * nwaves) * kPwBlock + (t & 7) * 1024;
-        uint8_t* buf = wl + (t & 1) * kGBuf;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) glds16(ideal + base + 128 * i + 2 * lane, buf + i * kGRow);
-        glds16(fixed + base + 16 * lane, buf + 8 * kGRow);
-    };
-    if (nrounds) issue(0);
-    Term st[4];
-#pragma unroll 1
-    for (int64_t t = 0; t < nrounds; ++t) {
-        if (t + 1 < nrounds) {
-            issue(t + 1);
-            asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        uint8_t* buf = wl + (t & 1) * kGBuf;
-        uint8_t* fb = buf + 8 * kGRow;
-        {  // fixed bytes -> [leaf][accumulator j][step s], in place (see metrics_blocks)
-            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-            const u4 fx = *reinterpret_cast<const u4*>(fb + 16 * lane);
-            const uint32_t fw[4] = {fx.x, fx.y, fx.z, fx.w};
-            uint8_t* fdst = fb + 128 * (lane >> 3) + 2 * (lane & 7);
-#pragma unroll
-            for (int jj = 0; jj < 8; ++jj)
-                *reinterpret_cast<uint16_t*>(fdst + 16 * jj) =
-                    (uint16_t)__builtin_amdgcn_perm(fw[2 + jj / 4], fw[jj / 4], (uint32_t)(jj % 4) | ((4u + jj % 4) << 8));
-        }
-        __builtin_amdgcn_wave_barrier();
-        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-        const uint8_t* row = buf + k * kGRow + 8 * j;
-        const u4 fr = *reinterpret_cast<const u4*>(fb + 128 * k + 16 * j);
-        const uint32_t frw[4] = {fr.x, fr.y, fr.z, fr.w};
-        double idv[16];  // all 16 reads issued together (one LDS round trip per round, not 16)
-#pragma unroll
-        for (int s = 0; s < 16; ++s) idv[s] = *reinterpret_cast<const double*>(row + 64 * s);
-        Term r{0.0, 0.0, 0.0};
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-            const uint32_t f = (frw[s / 4] >> (8 * (s % 4))) & 0xFFu;
-            const Term tt = metrics_term(idv[s], f, mx, lo, hi, clip);
-            if (s == 0) r = tt;
-            else tadd(r, tt);
-        }
-        const int rd = (int)(t & 7);
-        fold_round(st, rd, round_tree(r));
-        if (rd == 7 && lane == 0) {
-            const int64_t b = b0 + (t >> 3) * nwaves;
-            bsum[b] = st[3].a, bsum[nb + b] = st[3].q, bsum[2 * nb + b] = st[3].d;
-        }
-        __builtin_amdgcn_wave_barrier();
     }
     block_counts(Cnt{mx, lo, hi, clip}, parts + wg);
 }
@@ -623,8 +505,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mt_rsrc(const void* p, uint32_
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
     return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0, (int)bytes, 0x00020000);
 }
-// block_counts for the publishing launch: the workgroup's counts stored write-through, drained,
-// then one agent-scope add to the done counter the chain workgroup waits on.
+// block_counts for the publishing launch: the workgroup's counts stored write-through, then one
+// agent-scope RELEASE add to the done counter the chain workgroup acquires.
 __device__ void block_counts_pub(Cnt c, Cnt* dst, uint32_t* done) {
     __shared__ Cnt red[kBlock / kWave];
 #pragma unroll
@@ -645,15 +527,14 @@ __device__ void block_counts_pub(Cnt c, Cnt* dst, uint32_t* done) {
         __hip_atomic_store((gu64*)(d + 1), (uint64_t)a.lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store((gu64*)(d + 2), (uint64_t)a.hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store((gu64*)(d + 3), (uint64_t)a.clip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add((gu32*)done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add((gu32*)done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
 // metrics_final's work inside the publishing launch (its chain workgroup, after the chain): wait
-// until every streaming workgroup has added to `done`, reduce the nparts workgroup counts (read by
-// returning atomics, like every handed-off word) and the chain's sums, write out[0..8].  A wait past
-// the spin bound writes NaN sums.
+// until every streaming workgroup has added to `done` (then an agent-scope acquire), reduce the
+// nparts workgroup counts (read by returning atomics, like every handed-off word) and the chain's
+// sums, write out[0..8].  A wait past the chain's deadline writes NaN sums and out[8] = 1.
 __device__ void final_in_launch(const Cnt* parts, int nparts, uint32_t* done, uint32_t ndone, int64_t n, double* out,
                                 uint8_t* lds) {
     const int t = threadIdx.x;
@@ -662,9 +543,18 @@ __device__ void final_in_launch(const Cnt* parts, int nparts, uint32_t* done, ui
     Cnt* red = reinterpret_cast<Cnt*>(lds + kChainLds + 64);
     __syncthreads();  // the chain's sums are in LDS
     if (t == 0) {
-        uint32_t spins = 0;
-        while (coherent_read(done) < ndone && ++spins <= kChainSpinCap) __builtin_amdgcn_s_sleep(2);
-        *flag = spins <= kChainSpinCap;
+        const uint64_t dl = *reinterpret_cast<const uint64_t*>(lds + kChainLds + 56);  // chain_follow's deadline
+        bool arrived = false;
+        for (;;) {
+            if (coherent_read(done) >= ndone) {
+                arrived = true;
+                break;
+            }
+            if (__builtin_amdgcn_s_memrealtime() > dl) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (arrived) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the workgroups' release adds were read
+        *flag = arrived;
     }
     __syncthreads();
     const bool ok = *flag != 0;
@@ -697,13 +587,12 @@ __device__ void final_in_launch(const Cnt* parts, int nparts, uint32_t* done, ui
     }
 }
 
-// PUB: one launch over every full block, publishing each block's sums to the chain workgroup
-// (chain_follow; c_lo/c_hi unused) instead of chaining the previous launch's part.
-template <bool PUB>
+// One launch over every full block [0, nbf) of a 16-byte aligned u8 call: the streaming workgroups
+// publish each block's sums to workgroup 0, which follows them (chain_follow) and finishes the
+// call (final_in_launch).
 __global__ __launch_bounds__(kBlock, 2) void metrics_leaf_kernel(const double* __restrict__ ideal,
                                                                 const uint8_t* __restrict__ fixed,
-                                                                double* __restrict__ bsum, int64_t nb, int64_t b_lo,
-                                                                int64_t b_hi, int64_t c_lo, int64_t c_hi,
+                                                                double* __restrict__ bsum, int64_t nb, int64_t nbf,
                                                                 double* __restrict__ state, Cnt* __restrict__ parts,
                                                                 uint32_t* __restrict__ cnt, const Cnt* parts_all,
                                                                 int nparts_all, int64_t n, double* __restrict__ out) {
@@ -711,25 +600,20 @@ __global__ __launch_bounds__(kBlock, 2) void metrics_leaf_kernel(const double* _
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     typedef int i4 __attribute__((ext_vector_type(4)));
     __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock / kWave * kLfWaveLds];
-    const bool chain = PUB || c_hi > c_lo;
-    if (chain && blockIdx.x == 0) {
-        if constexpr (PUB) {
-            const int64_t nw = (int64_t)(gridDim.x - 1) * (kBlock / kWave);
-            if (FIR_METRIC_EXP != 4 && FIR_METRIC_EXP != 5) chain_follow(bsum, nb, b_hi, cnt, nw, state, smem);
-            final_in_launch(parts_all, nparts_all, cnt + nw, gridDim.x - 1, n, out, smem);
-        }
-        else if (FIR_METRIC_EXP != 1)  // (EXP: timing experiments)
-            chain_range(bsum, nb, c_lo, c_hi, state, smem);
+    if (blockIdx.x == 0) {
+        const int64_t nw = (int64_t)(gridDim.x - 1) * (kBlock / kWave);
+        chain_follow(bsum, nb, nbf, cnt, nw, state, smem);
+        final_in_launch(parts_all, nparts_all, cnt + nw, gridDim.x - 1, n, out, smem);
         return;
     }
-    const int wg = blockIdx.x - (chain ? 1 : 0);
+    const int wg = blockIdx.x - 1;
     const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x >> 6;
     uint8_t* wl = smem + wv * kLfWaveLds;
     uint8_t* fl = wl + kWave * kLfRow;  // fixed rows
-    const int64_t nwaves = (int64_t)(gridDim.x - (chain ? 1 : 0)) * (kBlock / kWave);
+    const int64_t nwaves = (int64_t)(gridDim.x - 1) * (kBlock / kWave);
     const int64_t sw = (int64_t)wg * (kBlock / kWave) + wv;  // streaming wave index
-    const int64_t b0 = b_lo + sw;
-    const int64_t nrounds = b0 < b_hi ? ((b_hi - 1 - b0) / nwaves + 1) * 8 : 0;
+    const int64_t b0 = sw;
+    const int64_t nrounds = b0 < nbf ? ((nbf - 1 - b0) / nwaves + 1) * 8 : 0;
     double mx = 0.0;
     uint32_t nz_acc = 0, ff_acc = 0, ndw = 0;  // v_bcnt sums (28 + count per dword) and dwords seen
     uint64_t clip = 0;                          // wave-uniform (SALU)
@@ -787,14 +671,10 @@ __global__ __launch_bounds__(kBlock, 2) void metrics_leaf_kernel(const double* _
             for (int i = 0; i < 8; ++i) *reinterpret_cast<u4*>(fl + (8 * i + lrow) * kLfRow + 16 * lcol) = fx[i];
         }
         __builtin_amdgcn_wave_barrier();
-        if constexpr (PUB && FIR_METRIC_EXP != 5) {
-            if (q == 1 && t > 8) {  // the previous block's sums: stored two rounds ago, before the loads of
-                                    // the band just staged, so this (already satisfied) wait drains them
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0)
-                    __hip_atomic_store((gu32*)(cnt + sw), (uint32_t)(t >> 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
+        // the previous block's sums (stored two rounds ago, before the loads of the band just staged,
+        // so the release's vmcnt(0) finds them done): its progress word, a release
+        if (q == 1 && t > 8 && lane == 0)
+            __hip_atomic_store((gu32*)(cnt + sw), (uint32_t)(t >> 3), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         if (t + 1 < nrounds) load_band(t + 1, q == 7);  // the next band (+ the next block's fixed bytes)
         // this lane's leaf: 16 doubles and 16 fixed bytes of band q
         double idv[16];
@@ -824,33 +704,21 @@ __global__ __launch_bounds__(kBlock, 2) void metrics_leaf_kernel(const double* _
             lf = tadd2(lf, tshift<8>(lf));
             lf = tadd2(lf, tshift<16>(lf));
             lf = tadd2(lf, tshift<32>(lf));
-            if (lane == 0) {
+            if (lane == 0) {  // write-through; the progress word's release publishes them later
                 const int64_t b = b0 + (t >> 3) * nwaves;
-                if constexpr (PUB && FIR_METRIC_EXP != 5) {  // write-through; progress published later
-                    __hip_atomic_store((gu64*)(bsum + b), __builtin_bit_cast(uint64_t, lf.a), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store((gu64*)(bsum + nb + b), __builtin_bit_cast(uint64_t, lf.q), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store((gu64*)(bsum + 2 * nb + b), __builtin_bit_cast(uint64_t, lf.d), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                } else {
-                    bsum[b] = lf.a, bsum[nb + b] = lf.q, bsum[2 * nb + b] = lf.d;
-                }
+                __hip_atomic_store((gu64*)(bsum + b), __builtin_bit_cast(uint64_t, lf.a), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((gu64*)(bsum + nb + b), __builtin_bit_cast(uint64_t, lf.q), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((gu64*)(bsum + 2 * nb + b), __builtin_bit_cast(uint64_t, lf.d), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     }
-    if constexpr (PUB && FIR_METRIC_EXP != 5) {  // the wave's last block
-        if (nrounds) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0)
-                __hip_atomic_store((gu32*)(cnt + sw), (uint32_t)(nrounds >> 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    if (nrounds && lane == 0)  // the wave's last block
+        __hip_atomic_store((gu32*)(cnt + sw), (uint32_t)(nrounds >> 3), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t lo = 4 * ndw - (nz_acc - 28 * ndw), hi = ff_acc - 28 * ndw;
-    if constexpr (PUB)
-        block_counts_pub(Cnt{mx, lo, hi, lane == 0 ? clip : 0ull}, parts + wg, cnt + nwaves);
-    else
-        block_counts(Cnt{mx, lo, hi, lane == 0 ? clip : 0ull}, parts + wg);
+    block_counts_pub(Cnt{mx, lo, hi, lane == 0 ? clip : 0ull}, parts + wg, cnt + nwaves);
 }
 
 // Fixed arrays of any other dtype (int8..int64, uint16..uint64, float16/32/64: the reference's
@@ -972,12 +840,12 @@ __global__ __launch_bounds__(kBlock) void metrics_final(const double* __restrict
     __shared__ __attribute__((aligned(16))) uint8_t smem[kChainLds];
     const int t = threadIdx.x;
     Cnt c{0.0, 0, 0, 0};
-    for (int i = t; i < nparts && FIR_METRIC_EXP != 2; i += kBlock) {
+    for (int i = t; i < nparts; i += kBlock) {
         const Cnt& q = parts[i];
         c.mx = fmax(c.mx, q.mx), c.lo += q.lo, c.hi += q.hi, c.clip += q.clip;
     }
     red[t] = c;
-    if (c_lo < nb && FIR_METRIC_EXP != 3) chain_range(bsum, nb, c_lo, nb, state, smem, out);  // out[1..3]
+    if (c_lo < nb) chain_range(bsum, nb, c_lo, nb, state, smem, out);  // out[1..3]
     if (c_lo >= nb && t < 3) out[1 + t] = nb > 0 ? state[t] : 0.0;  // (no last part: n == 0)
     __syncthreads();
     for (int w = kBlock / 2; w > 0; w >>= 1) {
@@ -1005,23 +873,13 @@ static int64_t metrics_nblocks(int64_t n) { return (n + kPwBlock - 1) / kPwBlock
 
 // Work buffer: Cnt per workgroup of every launch (+ the ragged block's), the 3 running sums, then
 // the block sums [3][nb].
-#ifndef FIR_METRIC_TAIL  // blocks of the last part (its chain is the exposed one)
-#define FIR_METRIC_TAIL 2048
-#endif
-#ifndef FIR_METRIC_BODY  // blocks of every earlier part
-#define FIR_METRIC_BODY 8192
-#endif
-constexpr int64_t kTailPart = FIR_METRIC_TAIL, kBodyPart = FIR_METRIC_BODY;
+constexpr int64_t kTailPart = 2048;  // blocks of the last part (its chain is the exposed one)
+constexpr int64_t kBodyPart = 8192;  // blocks of every earlier part
 constexpr int kMaxParts = 16;
 constexpr int64_t kCntSlots = (int64_t)kMaxParts * kMetricBlocks + 1;
 
-#ifndef FIR_METRIC_PERSIST  // 1: u8 (aligned) in ONE launch whose chain workgroup follows the
-#define FIR_METRIC_PERSIST 1   // published block sums (metrics_leaf_kernel<true>)
-#endif
-#ifndef FIR_METRIC_PBLOCKS   // streaming workgroups of that launch
-#define FIR_METRIC_PBLOCKS 256
-#endif
-constexpr int kMetricPBlocks = FIR_METRIC_PBLOCKS;
+// aligned u8 with full blocks: ONE launch (metrics_leaf_kernel) of this many streaming workgroups
+constexpr int kMetricPBlocks = 256;
 static_assert(kMetricPBlocks + 1 <= kCntSlots, "count slots");
 // the progress words of the publishing launch's streaming waves (zeroed every call by the kernel
 // ahead of it), at the start of the work buffer
@@ -1047,16 +905,15 @@ int launch_metrics_t(const double* ideal, const FT* fixed, int64_t n, double* ou
     double* bsum = state + 8;
     const bool vec = (uintptr_t)ideal % 16 == 0 && (uintptr_t)fixed % 16 == 0;
     if constexpr (std::is_same_v<FT, uint8_t>) {
-        if (vec && kMetricLeaf && FIR_METRIC_PERSIST && nbf > 0) {  // one streaming launch
+        if (vec && nbf > 0) {  // one streaming launch
             // the progress words zeroed and the ragged block (if any) summed first: the chain adds it last
             const int slot = nb > nbf ? 1 : 0;
             hipLaunchKernelGGL(metrics_ragged<FT>, dim3(1), dim3(kBlock), 0, stream, ideal, fixed, n, bsum, nb, parts, cnt,
                                (int)(cb / 4));
             const int64_t want = (nbf + kBlock / kWave - 1) / (kBlock / kWave);
             const int g = (int)(want > kMetricPBlocks ? kMetricPBlocks : want);
-            hipLaunchKernelGGL(metrics_leaf_kernel<true>, dim3(g + 1), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb,
-                               (int64_t)0, nbf, (int64_t)0, (int64_t)0, state, parts + slot, cnt, (const Cnt*)parts,
-                               slot + g, n, out);
+            hipLaunchKernelGGL(metrics_leaf_kernel, dim3(g + 1), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, nbf,
+                               state, parts + slot, cnt, (const Cnt*)parts, slot + g, n, out);
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return *err = std::string("metrics launch failed: ") + hipGetErrorString(e), FIR_EHIP;
             return FIR_OK;
@@ -1086,22 +943,10 @@ int launch_metrics_t(const double* ideal, const FT* fixed, int64_t n, double* ou
         const int64_t want = (hi - lo + kBlock / kWave - 1) / (kBlock / kWave);
         const int g = (int)(want > kMetricBlocks ? kMetricBlocks : want);
         const unsigned grid = (unsigned)g + (prev_hi > prev_lo ? 1u : 0u);
-        if constexpr (std::is_same_v<FT, uint8_t>) {
-            if (vec && kMetricLeaf)
-                hipLaunchKernelGGL(metrics_leaf_kernel<false>, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb,
-                                   lo, hi, prev_lo, prev_hi, state, parts + slot, (uint32_t*)nullptr, (const Cnt*)nullptr, 0,
-                                   (int64_t)0, (double*)nullptr);
-            else if (vec && kMetricGlds)
-                hipLaunchKernelGGL(metrics_blocks_glds, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, lo,
-                                   hi, prev_lo, prev_hi, state, parts + slot);
-            else if (vec)
-                hipLaunchKernelGGL(metrics_blocks<true>, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, lo,
-                                   hi, prev_lo, prev_hi, state, parts + slot);
-            else
-                hipLaunchKernelGGL(metrics_blocks<false>, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, lo,
-                                   hi, prev_lo, prev_hi, state, parts + slot);
+        if constexpr (std::is_same_v<FT, uint8_t>) {  // (not 16-byte aligned)
+            hipLaunchKernelGGL(metrics_blocks, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, lo, hi,
+                               prev_lo, prev_hi, state, parts + slot);
         } else {
-            (void)vec;
             hipLaunchKernelGGL(metrics_blocks_any<FT>, dim3(grid), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, lo,
                                hi, prev_lo, prev_hi, state, parts + slot);
         }

@@ -61,6 +61,7 @@ class HaloExchange:
         buf_dev = torch.device("cpu") if self.staged else seg.device
         self.seg, self.group, self.hl, self.hr = seg, group, hl, hr
         self.left = self.right = None
+        self.fallback_reason = None  # set by make_halo_source when the xGMI path was refused
         self._sends = []  # (device view, host staging buffer or None)
         ops = []
         left_peer = _peer(group, rank - 1) if rank > 0 else (_peer(group, rank) if self_ring else None)
@@ -257,8 +258,9 @@ class XgmiHalo:
 def make_halo_source(seg: torch.Tensor, taps: int, channels: int = 1, group=None, prefer: str = "xgmi"):
     """The per-step halo source for a resident segment: XgmiHalo when every rank can map its
     neighbours and the first gated hand-off arrives intact on every rank (decided collectively,
-    so all ranks take the same path), else the RCCL HaloExchange.  Returns (kind, source) with
-    kind "xgmi" or "rccl"."""
+    so all ranks take the same path), else the RCCL HaloExchange, whose ``fallback_reason``
+    then names the first rank that refused the xGMI path and why (the same text on every rank).
+    Returns (kind, source) with kind "xgmi" or "rccl"."""
     world = dist.get_world_size(group)
 
     def agree(ok: int) -> bool:
@@ -289,7 +291,14 @@ def make_halo_source(seg: torch.Tensor, taps: int, channels: int = 1, group=None
             import sys
 
             print(f"fir_hip.sharded: xGMI halo path unavailable ({err}); using RCCL", file=sys.stderr)
-    return "rccl", HaloExchange(seg, taps, channels, group)
+        errs = [None] * world
+        dist.all_gather_object(errs, None if err is None else f"{type(err).__name__}: {err}", group=group)
+        reason = next((f"rank {r}: {e}" for r, e in enumerate(errs) if e), "xGMI path refused")
+    else:
+        reason = f"FIR_HALO={prefer} requested"
+    ex = HaloExchange(seg, taps, channels, group)
+    ex.fallback_reason = reason
+    return "rccl", ex
 
 
 def post_halo_exchange(seg: torch.Tensor, taps: int, channels: int = 1, group=None):
