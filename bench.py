@@ -90,7 +90,7 @@ KERNELS = {"fir1d_i16": "fir1d_reg_kernel", "cplx_i16": "fir1d_reg_kernel", "fir
            "fir1d_u8": "fir1d_reg_kernel", "ideal_u8": "fir1d_ideal_kernel", "bank_u8": "fir1d_reg_kernel",
            "restore_u8": "restore_map_kernel",
            "pipeline_fixed3": "fir1d_reg_kernel (4-filter bank, one launch per image, 7 launches in one hipGraph)",
-           "metrics_u8": "metrics_leaf_kernel<true> (+ progress-word reset; chain and final in the launch)"}
+           "metrics_u8": "metrics_leaf_kernel (+ metrics_prep: unset markers; chain and final in the launch)"}
 NUMPY_ONLY = ("restore_u8", "metrics_u8", "pipeline_fixed3")  # no C oracle leg: the NumPy restatement is the CPU baseline
 ROOF_RAMP, ROOF_LAUNCHES = 100, 200  # roofline loop: untimed ramp, then timed launches of the dominant kernel
 

@@ -1,7 +1,8 @@
-"""The u8 metrics pass in one launch (metrics.hip, metrics_leaf_kernel<true>): the streaming
-waves hand every block's three sums to the chain workgroup inside the launch (write-through
-stores, per-wave progress words, one agent-scope acquire per batch).  A stale read there shows as a
-sum off by whole blocks, so these tests re-run the pass on the SAME output and work buffers with
+"""The u8 metrics pass in one launch (metrics.hip, metrics_leaf_kernel): the streaming waves hand
+every block's three sums and every workgroup's counts to the chain workgroup inside the launch,
+each word its own ready flag (set to an unset signalling-NaN pattern by metrics_prep, published
+once by a write-through atomic store, read by returning atomics until published).  A stale read
+there shows as a sum off by whole blocks (or a count off by a workgroup's), so these tests re-run the pass on the SAME output and work buffers with
 new data each time (consumer caches warm with the previous call's lines), in eager calls and in
 graph replays, at sizes with and without a ragged last block and with one to many layers of
 blocks per wave, and compare every report metric with the oracle bit for bit."""

@@ -17,8 +17,8 @@
 // A full 8192-sample block is a balanced tree of 64 leaves of 128 samples; its sums are
 // reduced by one wave, the block sums then added in order by a dependent float64 chain (waves
 // 0-2 of one workgroup: |d|, d^2, d; 2.7 ns per block).  Two forms:
-//   16-byte aligned u8 (the pipeline's case): metrics_ragged zeroes the hand-off words and sums
-//     the ragged last block, then ONE launch of metrics_leaf_kernel: one lane per leaf (the leaf
+//   16-byte aligned u8 (the pipeline's case): metrics_prep marks the words the next launch
+//     publishes as unset and sums the ragged last block, then ONE launch of metrics_leaf_kernel: one lane per leaf (the leaf
 //     combine in registers, the block tree by DPP row shifts and permlane swaps -- IEEE addition
 //     is commutative, so a lane adding its partner's value matches either order), each block's
 //     sums published to workgroup 0, which follows them (chain_follow) and finishes the call
@@ -153,14 +153,13 @@ __device__ void block_counts(Cnt c, Cnt* dst) {
 
 // The running sums state[0..2] += block sums [lo, hi) of |d|, d^2, d, in order (from 0.0 when
 // lo == 0).  Waves 0-2 take one array each: groups of kChainDepth x 64 block sums, loaded
-// coalesced kChainGroups groups ahead (the loaded latency of one group, ~3 us beside a streaming
+// coalesced two groups ahead in chain_range (the loaded latency of one group, ~3 us beside a streaming
 // launch, exceeds the 1.4 us its adds take), each staged in the wave's LDS and read back in order
 // by every lane at the same address (a broadcast), so the dependent chain is one float64 add with
 // a VGPR operand per 8192 samples (2.7 ns; fed by v_readlane instead: 8.7 ns,
 // tools/microbench/chain_micro.hip).  `lds` holds 3 x kChainDepth x 64 doubles; no workgroup
 // barrier inside.
 constexpr int kChainDepth = 8;   // block sums per lane of a chain group (a group = 64 x this)
-constexpr int kChainGroups = 1;  // groups of block sums chain_follow checks and takes per batch
 constexpr int kChainLds = 3 * kChainDepth * kWave * (int)sizeof(double);
 constexpr int kChainGS = kChainDepth * kWave;  // block sums per group
 // s += sh[0], sh[1], ..., sh[len - 1] in order (sh: a staged group in the wave's LDS)
@@ -235,111 +234,77 @@ __device__ __forceinline__ void chain_range(const double* __restrict__ bsum, int
 }
 
 // The chain inside the launch that produces the block sums (metrics_leaf_kernel).  Streaming wave
-// w takes blocks w, w + nw, w + 2 nw, ... (nw waves) and publishes them in that order, as a
-// release/acquire hand-off at agent scope (the HIP memory model; the waves may sit on other
-// XCDs): the three sums of a block by relaxed agent-scope (write-through) stores, then -- one
-// round later, once the wave's next band has landed -- its progress word prog[w] = blocks done
-// by an agent-scope RELEASE store (gfx950: buffer_wbl2 sc1 + s_waitcnt vmcnt(0) + an sc1 store;
-// the sums are ordered before the word for every observer).  No read-modify-write: 2048 waves
-// adding to shared counters serialised in the memory-side atomic unit, +114 us at 2^28,
-// profiles/r04/metrics_publish_ab.txt.  Wave 0 of this workgroup polls: a group of kChainGS
-// blocks is ready when every block's wave has passed it (ONE wave-wide check of the group's
-// progress words per poll, s_sleep between polls); once it is, an agent-scope ACQUIRE fence
-// (buffer_inv sc1) makes the producers' releases happen-before the sum reads, and wave 0 posts
-// the group count to waves 1-2 by a workgroup-scope release store they read with acquire loads.
-// Every read of a handed-off word is also a returning atomic (coherent_read below).  Blocks
-// [nbf, nb) (the ragged block) were written by an earlier launch.  The chain's waves run at
-// raised priority (a dependent float64 add per block, sharing a SIMD with streaming waves).  The
+// w takes blocks w, w + nw, w + 2 nw, ... (nw waves); workgroup 0's waves 0-2 add the block sums
+// of |d|, d^2 and d in order as they appear.  The hand-off is per location: every published word
+// is its own "ready" flag.  The kernel ahead of the launch (metrics_prep) sets each block-sum and
+// workgroup-count word to kUnset, a signalling-NaN pattern no sum can take (arithmetic results
+// are quiet NaNs; a count never reaches 2^63); a producer stores each word once, by a relaxed
+// agent-scope atomic store (write-through); a chain wave reads a group of kChainGS words by
+// returning agent-scope atomics and takes it once none reads kUnset.  In the HIP memory model
+// that needs no ordering between locations: an atomic read returns either the kUnset stored
+// before the launch (kernel boundary) or the one value a producer stored, and per-location
+// coherence makes the latter visible eventually -- so there is no progress word, no release
+// fence and no acquire fence.  (An agent-scope release per published block -- buffer_wbl2 sc1 on
+// gfx950 -- made the pass 4.6x slower, 1828 vs 395.5 us at 2^28, profiles/r05/metrics_release_ab.txt.)
+// Blocks [nbf, nb) (the ragged block) were written by the earlier launch.  The chain's waves run
+// at raised priority (a dependent float64 add per block, sharing a SIMD with streaming waves).  The
 // waits share one deadline on the 100 MHz s_memrealtime clock, kChainTimeoutTicks after the
 // chain starts (no correct run comes near it: the producers never wait, and a 288 GB call
 // streams in ~50 ms); past it the sums are NaN and out[8] = 1.
 constexpr uint64_t kChainTimeoutTicks = 1000000000ull;  // 10 s
+constexpr uint64_t kUnset = 0x7FF0000000000001ull;      // a signalling NaN: "not published yet"
 typedef __attribute__((address_space(1))) uint64_t gu64;
 typedef __attribute__((address_space(1))) uint32_t gu32;
-// A read of a word another XCD wrote in this launch (or the memset before it) that no cache of the
+// A read of a word another XCD wrote in this launch (or the kernel before it) that no cache of the
 // reading XCD can answer: a returning agent-scope atomic (performed past the XCD's L2).  Loads --
 // plain, sc1, or behind an agent acquire -- are served by the reading XCD's L2, which can hold the
-// line from an earlier call: in a graph replay the chain then saw the previous replay's progress
-// words and sums (tests/test_gpu_graphs.py, all 9 full blocks of seed 1 in seed 2's sums).
+// line from an earlier call: in a graph replay the chain then saw the previous replay's words and
+// sums (tests/test_gpu_graphs.py, all 9 full blocks of seed 1 in seed 2's sums).
 // (The zero operand is opaque: with a literal 0 the compiler turns the idempotent RMW into a load.)
 __device__ __forceinline__ uint32_t opaque_zero() {
     uint32_t z;
     asm volatile("v_mov_b32 %0, 0" : "=v"(z));
     return z;
 }
-__device__ __forceinline__ uint32_t coherent_read(const uint32_t* p) {
-    return __hip_atomic_fetch_add((gu32*)p, opaque_zero(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ uint64_t coherent_read_bits(const void* p) {
+    return __hip_atomic_fetch_or((gu64*)p, (uint64_t)opaque_zero(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ double coherent_read(const double* p) {
-    return __builtin_bit_cast(double, __hip_atomic_fetch_or((gu64*)p, (uint64_t)opaque_zero(), __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT));
+    return __builtin_bit_cast(double, coherent_read_bits(p));
 }
-__device__ __forceinline__ void chain_follow(const double* __restrict__ bsum, int64_t nb, int64_t nbf, uint32_t* prog,
-                                             int64_t nw, double* state, uint8_t* lds) {
+__device__ __forceinline__ void publish_bits(void* p, uint64_t v) {
+    __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void chain_follow(const double* __restrict__ bsum, int64_t nb, int64_t nbf, double* state,
+                                             uint8_t* lds) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
     const double* src = bsum + (int64_t)wv * nb;
     double* sh = reinterpret_cast<double*>(lds) + wv * kChainDepth * kWave;
-    constexpr int D = kChainDepth, NG = kChainGroups, GS = kChainGS;
-    double s = 0.0;
-    bool ok = true;
-    const int64_t ngr = (nbf + GS - 1) / GS;
-    auto need = [&](int64_t g) { return (int)(nbf - g * GS < GS ? nbf - g * GS : GS); };
-    const uint32_t nw32 = (uint32_t)nw;  // (block indices < 2^32: n < 2^40)
-    // how many of groups g, g + 1, ..., g + NG - 1 are complete, counting from g (one round trip:
-    // every progress word of the NG groups in flight at once; wave-uniform)
-    auto ready_prefix = [&](int64_t g) {
-        uint32_t v[NG][D], lay[NG][D];
-#pragma unroll
-        for (int i = 0; i < NG; ++i) {
-            const uint32_t c0 = (uint32_t)((g + i) * GS), l0 = c0 / nw32, r0 = c0 - l0 * nw32;
-#pragma unroll
-            for (int d = 0; d < D; ++d) {  // block c0 + 64 d + lane = layer nw + w: wave w's (layer + 1)-th
-                const uint32_t r = r0 + d * kWave + lane, w = r % nw32;
-                lay[i][d] = l0 + r / nw32;
-                v[i][d] = coherent_read(prog + w);
-            }
-        }
-        int k = 0;
-#pragma unroll
-        for (int i = 0; i < NG; ++i) {
-            bool mine = true;
-#pragma unroll
-            for (int d = 0; d < D; ++d) mine &= (g + i) * GS + d * kWave + lane >= nbf || v[i][d] >= lay[i][d] + 1;
-            const bool all = __builtin_amdgcn_ballot_w64(!mine) == 0;
-            if (k == i && all && g + i < ngr) k = i + 1;
-        }
-        return k;
-    };
-    // only wave 0 polls the progress words; it posts how many groups are complete in an LDS word
-    // that waves 1-2 watch (one third of the polling atomics)
-    int* posted = reinterpret_cast<int*>(lds + kChainLds);  // (past the three staging areas)
+    constexpr int D = kChainDepth, GS = kChainGS;
     int* failed = reinterpret_cast<int*>(lds + kChainLds + 52);  // a chain wave gave up waiting
     uint64_t* deadline = reinterpret_cast<uint64_t*>(lds + kChainLds + 56);  // shared with final_in_launch
-    if (wv == 0 && lane == 0) {
-        __hip_atomic_store(posted, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_store(failed, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (threadIdx.x == 0) {
+        *failed = 0;
         *deadline = __builtin_amdgcn_s_memrealtime() + kChainTimeoutTicks;
     }
     __syncthreads();  // (every wave of the workgroup: the words are set before anyone reads them)
     if (wv >= 3) return;
     const uint64_t dl = *deadline;
     __builtin_amdgcn_s_setprio(3);
-    for (int64_t g = 0; g < ngr && ok;) {
-        int k = 0;
-        for (;;) {
-            if (wv == 0) {
-                k = ready_prefix(g);
-                if (k > 0) {
-                    // the producers' release stores (progress words) were read: their sums are visible
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    if (lane == 0) __hip_atomic_store(posted, (int)(g + k), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-            } else {
-                const int p = __builtin_amdgcn_readfirstlane(
-                    __hip_atomic_load(posted, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-                k = p > g ? (int)min<int64_t>(p - g, NG) : 0;
+    double s = 0.0;
+    bool ok = true;
+    for (int64_t g0 = 0; g0 < nbf; g0 += GS) {
+        const int len = (int)(nbf - g0 < GS ? nbf - g0 : GS);
+        uint64_t v[D];
+        for (;;) {  // one wave-wide read of the group; again after a sleep until every word is published
+            bool mine = true;
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const int e = d * kWave + lane;
+                v[d] = e < len ? coherent_read_bits(src + g0 + e) : 0ull;
+                mine &= v[d] != kUnset;
             }
-            if (k > 0) break;
+            if (__builtin_amdgcn_ballot_w64(!mine) == 0) break;
             if (__builtin_amdgcn_s_memrealtime() > dl) {
                 ok = false;
                 break;
@@ -347,27 +312,11 @@ __device__ __forceinline__ void chain_follow(const double* __restrict__ bsum, in
             __builtin_amdgcn_s_sleep(2);
         }
         if (!ok) break;
-        double q[NG][D];
+        __builtin_amdgcn_wave_barrier();  // the previous group's reads are done
 #pragma unroll
-        for (int i = 0; i < NG; ++i) {
-            const int64_t c0 = (g + i) * GS;
-#pragma unroll
-            for (int d = 0; d < D; ++d) {
-                const int64_t b = c0 + d * kWave + lane;
-                q[i][d] = i < k && b < nbf ? coherent_read(src + b) : 0.0;
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < NG; ++i) {
-            if (i < k) {
-                __builtin_amdgcn_wave_barrier();  // the previous group's reads are done
-#pragma unroll
-                for (int d = 0; d < D; ++d) sh[d * kWave + lane] = q[i][d];
-                __builtin_amdgcn_wave_barrier();
-                add_group(s, sh, need(g + i));
-            }
-        }
-        g += k;
+        for (int d = 0; d < D; ++d) sh[d * kWave + lane] = __builtin_bit_cast(double, v[d]);
+        __builtin_amdgcn_wave_barrier();
+        add_group(s, sh, len);
     }
     for (int64_t b = nbf; b < nb; ++b) s = __dadd_rn(s, coherent_read(src + b));
     if (lane == 0) {
@@ -505,9 +454,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mt_rsrc(const void* p, uint32_
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
     return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0, (int)bytes, 0x00020000);
 }
-// block_counts for the publishing launch: the workgroup's counts stored write-through, then one
-// agent-scope RELEASE add to the done counter the chain workgroup acquires.
-__device__ void block_counts_pub(Cnt c, Cnt* dst, uint32_t* done) {
+// block_counts for the publishing launch: the workgroup's counts, each word published once
+// (kUnset until then; see chain_follow).
+__device__ void block_counts_pub(Cnt c, Cnt* dst) {
     __shared__ Cnt red[kBlock / kWave];
 #pragma unroll
     for (int m = 1; m < kWave; m <<= 1) {
@@ -523,52 +472,50 @@ __device__ void block_counts_pub(Cnt c, Cnt* dst, uint32_t* done) {
         for (int w = 1; w < kBlock / kWave; ++w)
             a.mx = fmax(a.mx, red[w].mx), a.lo += red[w].lo, a.hi += red[w].hi, a.clip += red[w].clip;
         uint64_t* d = reinterpret_cast<uint64_t*>(dst);
-        __hip_atomic_store((gu64*)(d + 0), __builtin_bit_cast(uint64_t, a.mx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store((gu64*)(d + 1), (uint64_t)a.lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store((gu64*)(d + 2), (uint64_t)a.hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store((gu64*)(d + 3), (uint64_t)a.clip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add((gu32*)done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        publish_bits(d + 0, __builtin_bit_cast(uint64_t, a.mx));
+        publish_bits(d + 1, (uint64_t)a.lo);
+        publish_bits(d + 2, (uint64_t)a.hi);
+        publish_bits(d + 3, (uint64_t)a.clip);
     }
 }
 
-// metrics_final's work inside the publishing launch (its chain workgroup, after the chain): wait
-// until every streaming workgroup has added to `done` (then an agent-scope acquire), reduce the
-// nparts workgroup counts (read by returning atomics, like every handed-off word) and the chain's
-// sums, write out[0..8].  A wait past the chain's deadline writes NaN sums and out[8] = 1.
-__device__ void final_in_launch(const Cnt* parts, int nparts, uint32_t* done, uint32_t ndone, int64_t n, double* out,
-                                uint8_t* lds) {
+// metrics_final's work inside the publishing launch (its chain workgroup, after the chain): each
+// thread reads its share of the nparts workgroup counts once every word is published (the same
+// per-location hand-off as the block sums), then the reduction and the chain's sums go to
+// out[0..8].  A wait past the chain's deadline writes NaN sums and out[8] = 1.
+__device__ void final_in_launch(const Cnt* parts, int nparts, int64_t n, double* out, uint8_t* lds) {
     const int t = threadIdx.x;
     double* sums = reinterpret_cast<double*>(lds + kChainLds + 16);  // the chain's three sums
     int* flag = reinterpret_cast<int*>(lds + kChainLds + 48);
     Cnt* red = reinterpret_cast<Cnt*>(lds + kChainLds + 64);
-    __syncthreads();  // the chain's sums are in LDS
-    if (t == 0) {
-        const uint64_t dl = *reinterpret_cast<const uint64_t*>(lds + kChainLds + 56);  // chain_follow's deadline
-        bool arrived = false;
+    if (t == 0) *flag = 1;
+    __syncthreads();  // the chain's sums and deadline are in LDS
+    const uint64_t dl = *reinterpret_cast<const uint64_t*>(lds + kChainLds + 56);
+    Cnt c{0.0, 0, 0, 0};
+    bool mine = true;
+    for (int i = t; i < nparts; i += kBlock) {
+        const uint64_t* q = reinterpret_cast<const uint64_t*>(parts + i);
+        uint64_t w[4];
         for (;;) {
-            if (coherent_read(done) >= ndone) {
-                arrived = true;
+            bool done = true;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) w[k] = coherent_read_bits(q + k), done &= w[k] != kUnset;
+            if (done) break;
+            if (__builtin_amdgcn_s_memrealtime() > dl) {
+                mine = false;
                 break;
             }
-            if (__builtin_amdgcn_s_memrealtime() > dl) break;
             __builtin_amdgcn_s_sleep(2);
         }
-        if (arrived) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the workgroups' release adds were read
-        *flag = arrived;
+        if (!mine) break;
+        c.mx = fmax(c.mx, __builtin_bit_cast(double, w[0]));
+        c.lo += w[1], c.hi += w[2], c.clip += w[3];
     }
+    if (!mine) __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    red[t] = c;
     __syncthreads();
     const bool ok = *flag != 0;
     const bool chain_ok = reinterpret_cast<const int*>(lds + kChainLds + 52)[0] == 0;
-    Cnt c{0.0, 0, 0, 0};
-    for (int i = t; i < nparts && ok; i += kBlock) {
-        const double* q = reinterpret_cast<const double*>(parts + i);
-        c.mx = fmax(c.mx, coherent_read(q));
-        c.lo += __builtin_bit_cast(uint64_t, coherent_read(q + 1));
-        c.hi += __builtin_bit_cast(uint64_t, coherent_read(q + 2));
-        c.clip += __builtin_bit_cast(uint64_t, coherent_read(q + 3));
-    }
-    red[t] = c;
-    __syncthreads();
     for (int w = kBlock / 2; w > 0; w >>= 1) {
         if (t < w) {
             Cnt& a = red[t];
@@ -594,16 +541,15 @@ __global__ __launch_bounds__(kBlock, 2) void metrics_leaf_kernel(const double* _
                                                                 const uint8_t* __restrict__ fixed,
                                                                 double* __restrict__ bsum, int64_t nb, int64_t nbf,
                                                                 double* __restrict__ state, Cnt* __restrict__ parts,
-                                                                uint32_t* __restrict__ cnt, const Cnt* parts_all,
-                                                                int nparts_all, int64_t n, double* __restrict__ out) {
+                                                                const Cnt* parts_all, int nparts_all, int64_t n,
+                                                                double* __restrict__ out) {
     typedef double d2 __attribute__((ext_vector_type(2)));
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     typedef int i4 __attribute__((ext_vector_type(4)));
     __shared__ __attribute__((aligned(16))) uint8_t smem[kBlock / kWave * kLfWaveLds];
     if (blockIdx.x == 0) {
-        const int64_t nw = (int64_t)(gridDim.x - 1) * (kBlock / kWave);
-        chain_follow(bsum, nb, nbf, cnt, nw, state, smem);
-        final_in_launch(parts_all, nparts_all, cnt + nw, gridDim.x - 1, n, out, smem);
+        chain_follow(bsum, nb, nbf, state, smem);
+        final_in_launch(parts_all, nparts_all, n, out, smem);
         return;
     }
     const int wg = blockIdx.x - 1;
@@ -671,10 +617,6 @@ __global__ __launch_bounds__(kBlock, 2) void metrics_leaf_kernel(const double* _
             for (int i = 0; i < 8; ++i) *reinterpret_cast<u4*>(fl + (8 * i + lrow) * kLfRow + 16 * lcol) = fx[i];
         }
         __builtin_amdgcn_wave_barrier();
-        // the previous block's sums (stored two rounds ago, before the loads of the band just staged,
-        // so the release's vmcnt(0) finds them done): its progress word, a release
-        if (q == 1 && t > 8 && lane == 0)
-            __hip_atomic_store((gu32*)(cnt + sw), (uint32_t)(t >> 3), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         if (t + 1 < nrounds) load_band(t + 1, q == 7);  // the next band (+ the next block's fixed bytes)
         // this lane's leaf: 16 doubles and 16 fixed bytes of band q
         double idv[16];
@@ -704,21 +646,16 @@ __global__ __launch_bounds__(kBlock, 2) void metrics_leaf_kernel(const double* _
             lf = tadd2(lf, tshift<8>(lf));
             lf = tadd2(lf, tshift<16>(lf));
             lf = tadd2(lf, tshift<32>(lf));
-            if (lane == 0) {  // write-through; the progress word's release publishes them later
+            if (lane == 0) {  // published: each word is its own ready flag (chain_follow)
                 const int64_t b = b0 + (t >> 3) * nwaves;
-                __hip_atomic_store((gu64*)(bsum + b), __builtin_bit_cast(uint64_t, lf.a), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store((gu64*)(bsum + nb + b), __builtin_bit_cast(uint64_t, lf.q), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store((gu64*)(bsum + 2 * nb + b), __builtin_bit_cast(uint64_t, lf.d), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+                publish_bits(bsum + b, __builtin_bit_cast(uint64_t, lf.a));
+                publish_bits(bsum + nb + b, __builtin_bit_cast(uint64_t, lf.q));
+                publish_bits(bsum + 2 * nb + b, __builtin_bit_cast(uint64_t, lf.d));
             }
         }
     }
-    if (nrounds && lane == 0)  // the wave's last block
-        __hip_atomic_store((gu32*)(cnt + sw), (uint32_t)(nrounds >> 3), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t lo = 4 * ndw - (nz_acc - 28 * ndw), hi = ff_acc - 28 * ndw;
-    block_counts_pub(Cnt{mx, lo, hi, lane == 0 ? clip : 0ull}, parts + wg, cnt + nwaves);
+    block_counts_pub(Cnt{mx, lo, hi, lane == 0 ? clip : 0ull}, parts + wg);
 }
 
 // Fixed arrays of any other dtype (int8..int64, uint16..uint64, float16/32/64: the reference's
@@ -761,18 +698,11 @@ __global__ __launch_bounds__(kBlock) void metrics_blocks_any(const double* __res
     block_counts(Cnt{mx, lo, hi, clip}, parts + wg);
 }
 
-// The ragged last block [nbf * 8192, n) (0 < m < 8192 samples): NumPy's recursion over it, one
-// workgroup (leaves enumerated, summed one per thread, recombined in post-order).
+// The ragged last block [nbf * 8192, n) (0 < m < 8192 samples): NumPy's recursion over it, by one
+// whole workgroup (leaves enumerated, summed one per thread, recombined in post-order).
 template <typename FT>
-__global__ __launch_bounds__(kBlock) void metrics_ragged(const double* __restrict__ ideal, const FT* __restrict__ fixed,
-                                                         int64_t n, double* __restrict__ bsum, int64_t nb,
-                                                         Cnt* __restrict__ part, uint32_t* __restrict__ prog, int nprog) {
-    // prog / nprog: the publishing launch's progress words, zeroed here -- by a kernel ahead of it in
-    // the stream, not a memset node: replayed in a graph behind other kernels, a captured
-    // hipMemsetAsync left the previous replay's words in place (tests/test_gpu_graphs.py); with no
-    // ragged block only the zeroing runs
-    for (int i = threadIdx.x; i < nprog; i += kBlock) prog[i] = 0u;
-    if (n % kPwBlock == 0) return;
+__device__ void ragged_block(const double* __restrict__ ideal, const FT* __restrict__ fixed, int64_t n,
+                             double* __restrict__ bsum, int64_t nb, Cnt* __restrict__ part) {
     __shared__ int leaf_off[kPwMaxLeaves], leaf_len[kPwMaxLeaves];
     __shared__ Term lsum[kPwMaxLeaves];
     __shared__ int nleaves;
@@ -831,6 +761,33 @@ __global__ __launch_bounds__(kBlock) void metrics_ragged(const double* __restric
     block_counts(Cnt{mx, lo, hi, clip}, part);
 }
 
+template <typename FT>
+__global__ __launch_bounds__(kBlock) void metrics_ragged(const double* __restrict__ ideal, const FT* __restrict__ fixed,
+                                                         int64_t n, double* __restrict__ bsum, int64_t nb,
+                                                         Cnt* __restrict__ part) {
+    ragged_block(ideal, fixed, n, bsum, nb, part);
+}
+
+// The kernel ahead of the publishing launch: every word that launch publishes (the block sums
+// [0, nbf) of the three arrays and the streaming workgroups' nunset counts) set to kUnset,
+// grid-stride -- a kernel, not a memset node: replayed in a graph behind other kernels, a
+// captured hipMemsetAsync left the previous replay's words in place (tests/test_gpu_graphs.py) --
+// and, by workgroup 0, the ragged block (if any), whose sums the chain adds last.
+template <typename FT>
+__global__ __launch_bounds__(kBlock) void metrics_prep(const double* __restrict__ ideal, const FT* __restrict__ fixed,
+                                                       int64_t n, double* __restrict__ bsum, int64_t nb,
+                                                       Cnt* __restrict__ ragged_part, Cnt* __restrict__ unset,
+                                                       int nunset) {
+    const int64_t nbf = n / kPwBlock, tid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t nth = (int64_t)gridDim.x * kBlock;
+    uint64_t* words = reinterpret_cast<uint64_t*>(bsum);
+    for (int w = 0; w < 3; ++w)
+        for (int64_t b = tid; b < nbf; b += nth) words[w * nb + b] = kUnset;
+    uint64_t* cw = reinterpret_cast<uint64_t*>(unset);
+    for (int64_t i = tid; i < 4 * (int64_t)nunset; i += nth) cw[i] = kUnset;
+    if (blockIdx.x == 0 && n % kPwBlock) ragged_block(ideal, fixed, n, bsum, nb, ragged_part);
+}
+
 // out: [max_abs, sum_abs, sum_sq, sum_d, n_low, n_high, n_clip, n, 0]: the last part's chain
 // (and the ragged block's sum, the last in order), the counts and max of every workgroup.
 __global__ __launch_bounds__(kBlock) void metrics_final(const double* __restrict__ bsum, int64_t nb, int64_t c_lo,
@@ -881,15 +838,13 @@ constexpr int64_t kCntSlots = (int64_t)kMaxParts * kMetricBlocks + 1;
 // aligned u8 with full blocks: ONE launch (metrics_leaf_kernel) of this many streaming workgroups
 constexpr int kMetricPBlocks = 256;
 static_assert(kMetricPBlocks + 1 <= kCntSlots, "count slots");
-// the progress words of the publishing launch's streaming waves (zeroed every call by the kernel
-// ahead of it), at the start of the work buffer
-static size_t metrics_cnt_bytes(int64_t) { return (size_t)4 * kMetricPBlocks * (kBlock / kWave) + 16; }  // + done
+constexpr int kMetricPrepBlocks = 64;  // workgroups of metrics_prep (grid-stride)
 
-// Work buffer: the publish counters, Cnt per workgroup of every launch (+ the ragged block's), the
-// 3 running sums, then the block sums [3][nb].
+// Work buffer: Cnt per workgroup of every launch (+ the ragged block's), the 3 running sums, then
+// the block sums [3][nb].
 size_t metrics_work_bytes(int64_t n) {
     if (n < 0) n = 0;
-    return metrics_cnt_bytes(n) + sizeof(Cnt) * kCntSlots + 64 + 3 * sizeof(double) * (size_t)metrics_nblocks(n);
+    return sizeof(Cnt) * kCntSlots + 64 + 3 * sizeof(double) * (size_t)metrics_nblocks(n);
 }
 
 namespace {
@@ -898,22 +853,20 @@ template <typename FT>
 int launch_metrics_t(const double* ideal, const FT* fixed, int64_t n, double* out, void* work, hipStream_t stream,
                      std::string* err) {
     const int64_t nb = metrics_nblocks(n), nbf = n / kPwBlock;
-    const size_t cb = metrics_cnt_bytes(n);
-    uint32_t* cnt = (uint32_t*)work;
-    Cnt* parts = (Cnt*)((char*)work + cb);
+    Cnt* parts = (Cnt*)work;
     double* state = (double*)((char*)parts + sizeof(Cnt) * kCntSlots);
     double* bsum = state + 8;
     const bool vec = (uintptr_t)ideal % 16 == 0 && (uintptr_t)fixed % 16 == 0;
     if constexpr (std::is_same_v<FT, uint8_t>) {
         if (vec && nbf > 0) {  // one streaming launch
-            // the progress words zeroed and the ragged block (if any) summed first: the chain adds it last
+            // the published words set to kUnset and the ragged block (if any) summed first: the chain adds it last
             const int slot = nb > nbf ? 1 : 0;
-            hipLaunchKernelGGL(metrics_ragged<FT>, dim3(1), dim3(kBlock), 0, stream, ideal, fixed, n, bsum, nb, parts, cnt,
-                               (int)(cb / 4));
             const int64_t want = (nbf + kBlock / kWave - 1) / (kBlock / kWave);
             const int g = (int)(want > kMetricPBlocks ? kMetricPBlocks : want);
+            hipLaunchKernelGGL(metrics_prep<FT>, dim3(kMetricPrepBlocks), dim3(kBlock), 0, stream, ideal, fixed, n, bsum, nb,
+                               parts, parts + slot, g);
             hipLaunchKernelGGL(metrics_leaf_kernel, dim3(g + 1), dim3(kBlock), 0, stream, ideal, fixed, bsum, nb, nbf,
-                               state, parts + slot, cnt, (const Cnt*)parts, slot + g, n, out);
+                               state, parts + slot, (const Cnt*)parts, slot + g, n, out);
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return *err = std::string("metrics launch failed: ") + hipGetErrorString(e), FIR_EHIP;
             return FIR_OK;
@@ -954,8 +907,7 @@ int launch_metrics_t(const double* ideal, const FT* fixed, int64_t n, double* ou
         prev_lo = lo, prev_hi = hi;
     }
     if (nb > nbf) {  // the ragged last block (its sum is the last in order)
-        hipLaunchKernelGGL(metrics_ragged<FT>, dim3(1), dim3(kBlock), 0, stream, ideal, fixed, n, bsum, nb, parts + slot,
-                           (uint32_t*)nullptr, 0);
+        hipLaunchKernelGGL(metrics_ragged<FT>, dim3(1), dim3(kBlock), 0, stream, ideal, fixed, n, bsum, nb, parts + slot);
         ++slot;
     }
     hipLaunchKernelGGL(metrics_final, dim3(1), dim3(kBlock), 0, stream, (const double*)bsum, nb, prev_lo, state,
