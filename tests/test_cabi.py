@@ -154,3 +154,33 @@ def test_stale_library_is_refused(tmp_path):
     bad = subprocess.run([sys.executable, "-c", probe], env=env, capture_output=True, text=True)
     assert bad.returncode != 0
     assert "built from other sources" in bad.stderr
+
+
+def test_torch_runtime_shared_only_when_sonames_match(tmp_path):
+    """fir_hip loads PyTorch's bundled HIP/HSA runtime first only when its DT_SONAME majors equal
+    those of the ROCm the library was built with: the decision reads the ELF headers of
+    the real files, and a runtime of another major (here: a copy whose soname says .so.6) or a
+    missing one keeps /opt/rocm's."""
+    import shutil
+
+    import fir_hip
+
+    rocm = Path("/opt/rocm/lib")
+    if not (rocm / "libamdhip64.so").exists():
+        pytest.skip("no /opt/rocm here")
+    assert fir_hip._elf_soname(rocm / "libamdhip64.so").startswith("libamdhip64.so.")
+    same = tmp_path / "same"
+    same.mkdir()
+    for stem in ("libamdhip64.so", "libhsa-runtime64.so"):
+        shutil.copy(rocm / stem, same / stem)
+    assert fir_hip._runtime_compatible(same, rocm)
+    other = tmp_path / "other"
+    other.mkdir()
+    shutil.copy(rocm / "libhsa-runtime64.so", other / "libhsa-runtime64.so")
+    data = bytearray((rocm / "libamdhip64.so").read_bytes())
+    name = fir_hip._elf_soname(rocm / "libamdhip64.so").encode()
+    i = data.index(name + b"\0")
+    data[i:i + len(name)] = name.replace(b".so.7", b".so.6") if b".so.7" in name else name[:-1] + b"9"
+    (other / "libamdhip64.so").write_bytes(bytes(data))
+    assert not fir_hip._runtime_compatible(other, rocm)
+    assert not fir_hip._runtime_compatible(tmp_path / "empty", rocm)

@@ -22,7 +22,7 @@ def main():
     for p in args.libs:
         lib = ctypes.CDLL(p)
         lib.fir_restore_u8_dev.argtypes = [vp, i64, i32, vp, vp, vp]
-        lib.fir_compare_metrics_dev.argtypes = [vp, vp, i64, vp, vp, vp]
+        lib.fir_compare_metrics_dev.argtypes = [vp, vp, ctypes.c_int, i64, vp, vp, vp]  # ABI 4: fixed dtype
         lib.fir_metrics_work_bytes.restype = i64
         lib.fir_metrics_work_bytes.argtypes = [i64]
         libs.append(lib)
@@ -44,7 +44,7 @@ def main():
         assert libs[i].fir_restore_u8_dev(vp(a.data_ptr()), n, 0, vp(outs[i].data_ptr()), None, S) == 0
 
     def metrics(i):
-        assert libs[i].fir_compare_metrics_dev(vp(a.data_ptr()), vp(fx.data_ptr()), n, vp(mets[i].data_ptr()),
+        assert libs[i].fir_compare_metrics_dev(vp(a.data_ptr()), vp(fx.data_ptr()), 0, n, vp(mets[i].data_ptr()),  # FIR_DT_U8
                                                vp(work.data_ptr()), S) == 0
 
     ops = {"restore_clip": (restore, 9.0), "metrics": (metrics, 9.0)}

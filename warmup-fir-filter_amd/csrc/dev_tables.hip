@@ -5,8 +5,9 @@
 // are read from HBM.  The C ABI keeps taking host pointers; this cache uploads each distinct
 // table once per device and hands out its device address for one launch at a time (TableHold):
 //
-//   * a table is keyed by a 128-bit hash of its content (or of the inputs it is built from, so a
-//     large derived table is built only on a miss) and its size;
+//   * a table is keyed by the bytes it is made from (its content, or the inputs a large derived
+//     table is built from, so that one is built only on a miss) behind a kind tag: looked up by a
+//     128-bit hash and its size, confirmed by comparing those bytes (a collision is a miss);
 //   * every hold counts as in use until the launch it was taken for has been enqueued, and each
 //     use then records an event on the launch's stream; a table is freed only when it has no
 //     hold and every use event has completed, never by a device-wide sync (which would also
@@ -41,13 +42,15 @@ struct Entry {
     std::vector<hipEvent_t> uses;   // one per enqueued use, pruned when complete
 };
 
-using Key = std::tuple<uint64_t, uint64_t, size_t>;
+// (hash, size) first: the source bytes are compared only between tables whose hashes are equal
+using Key = std::tuple<uint64_t, uint64_t, size_t, std::vector<uint8_t>>;
+using TableMap = std::map<Key, Entry>;
 
 struct TableCache {
     std::mutex mu;
     hipStream_t stream = nullptr;
-    std::map<Key, Entry> tables;
-    std::map<const void*, Key> by_ptr;
+    TableMap tables;
+    std::map<const void*, TableMap::iterator> by_ptr;
     std::vector<hipEvent_t> free_events;
     size_t bytes = 0;
 };
@@ -90,6 +93,7 @@ void evict_idle(TableCache* c, size_t need) {
 
 void TableHash::add(const void* p, size_t n) {
     const uint8_t* b = (const uint8_t*)p;
+    src.insert(src.end(), b, b + n);
     for (size_t i = 0; i < n; ++i) {
         a = (a ^ b[i]) * 0x100000001b3ull;                          // FNV-1a 64
         c = (c + b[i] + 0x9E3779B97F4A7C15ull) * 0xff51afd7ed558ccdull;  // an independent mix
@@ -109,7 +113,7 @@ const void* table_acquire(const TableHash& h, size_t bytes, const std::function<
         return nullptr;
     }
     TableCache* c = cache_for(dev);
-    const Key key{h.a, h.c, bytes};
+    Key key{h.a, h.c, bytes, h.src};
     std::lock_guard<std::mutex> lk(c->mu);
     auto it = c->tables.find(key);
     if (it != c->tables.end()) {
@@ -135,11 +139,12 @@ const void* table_acquire(const TableHash& h, size_t bytes, const std::function<
         *err = std::string("table upload: ") + hipGetErrorString(e);
         return nullptr;
     }
-    Entry& en = c->tables[key];
+    const auto ins = c->tables.emplace(std::move(key), Entry{}).first;
+    Entry& en = ins->second;
     en.d = d;
     en.bytes = bytes;
     en.holds = 1;
-    c->by_ptr[d] = key;
+    c->by_ptr[d] = ins;
     c->bytes += bytes;
     return d;
 }
@@ -152,7 +157,7 @@ void table_release(const void* d, hipStream_t stream, bool launched) {
     std::lock_guard<std::mutex> lk(c->mu);
     auto pit = c->by_ptr.find(d);
     if (pit == c->by_ptr.end()) return;
-    Entry& en = c->tables[pit->second];
+    Entry& en = pit->second->second;
     if (en.holds > 0) --en.holds;
     if (!launched) return;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -181,7 +186,7 @@ const void* device_table(const void* host, size_t bytes, std::string* err) {
         *err = "device_table: empty table";
         return nullptr;
     }
-    TableHash h;
+    TableHash h(kTableRaw);
     h.add(host, bytes);
     return table_acquire(h, bytes, [&](void* dst) { std::memcpy(dst, host, bytes); }, err);
 }

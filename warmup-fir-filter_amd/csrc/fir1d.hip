@@ -307,7 +307,12 @@ int launch_fir1d_rows_multi(const void* x, int in_dtype, int64_t rows, int64_t w
     if (total == 0) return FIR_OK;
     if (!x || !y) return *err = "x and y must not be NULL", FIR_EINVAL;
     const size_t osz = stage == FIR_OUT_I32 ? 4 : 1;
-    const bool fused = in_dtype == FIR_IN_U8 && ch == 1 && (total * (int64_t)osz) % 16 == 0 &&
+    // u8 output planes start where the previous one ends, at any byte (the reference's 4499 x 2999
+    // image: plane f at f * 13492501): the fused kernel's 16-byte stores then run unaligned, which
+    // gfx950 performs in the unaligned-access mode ROCm sets for compute queues (the int32 planes
+    // keep whole-dword row staging and stay on 16-byte plane starts)
+    const bool fused = in_dtype == FIR_IN_U8 && ch == 1 &&
+                       (stage == FIR_OUT_U8_SAT || (total * (int64_t)osz) % 16 == 0) &&
                        reg_path_ok(x, y, in_dtype, rows, rowlen, total, ch, hq, F * L, L, frac, acc_bits);
     for (int f0 = 0; f0 < F;) {
         const int nf = fused ? (F - f0 < 4 ? F - f0 : 4) : 1;

@@ -490,7 +490,7 @@ __global__ __launch_bounds__(kBlock) void fir1d_mfma_long_kernel(const InT* __re
 // (keyed by the taps and the geometry: the table is built only on a cache miss)
 static const mf_i32x4* mfma_frag_table(const int32_t* hq, int L, int P, int KS, std::string* err) {
     const int c = L / 2;
-    TableHash h;
+    TableHash h(kTableMfmaFrag);
     h.add(hq, sizeof(int32_t) * (size_t)L);
     h.add_val(L), h.add_val(P), h.add_val(KS);
     const size_t bytes = (size_t)KS * 2 * kWave * 16;

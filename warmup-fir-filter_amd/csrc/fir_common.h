@@ -65,9 +65,10 @@ __device__ __forceinline__ int32_t round_acc(uint32_t acc, int shl, int frac) {
 }
 
 // 64-bit generic form (any acc_bits >= 1, any frac_bits >= 1): `acc` is the sum mod 2^64,
-// which is exact for the wrap to acc_bits < 64, and the true sum for acc_bits >= 64 (the host
-// checks |sum| < 2^63).  floor((a + 2^(f-1)) / 2^f) without overflow: (a >> f) + bit (f-1) of a;
-// for f >= 64 that is 0 for every |a| < 2^63.
+// which is exact for the wrap to acc_bits < 64, and the true sum for acc_bits >= 64 whenever the
+// launchers pick this form: only when needs_wide is false, i.e. |sum| < 2^63 is proven for the
+// taps and sample range (round128 below carries every other no-wrap sum).  floor((a + 2^(f-1)) /
+// 2^f) without overflow: (a >> f) + bit (f-1) of a; for f >= 64 that is 0 for every |a| < 2^63.
 __device__ __forceinline__ int64_t round64(int64_t acc, int frac, int acc_bits) {
     if (acc_bits < 64) {
         const int s = 64 - acc_bits;

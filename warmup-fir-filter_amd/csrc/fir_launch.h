@@ -6,19 +6,25 @@
 
 #include <functional>
 #include <string>
+#include <vector>
 
 namespace fir {
 
 // Device copies of host tables (long tap sets, matrix-core tap fragments) on the current device
-// (dev_tables.hip): cached by a 128-bit hash of their content, or of the inputs they are built
-// from (table_acquire builds the table with `fill` only on a miss), uploaded once (complete
-// before the call returns).  Every acquire is a hold on the table for ONE launch, released by
-// table_release after that launch is enqueued on `stream` (TableHold does it at scope exit): the
-// cache frees a table only when no hold is outstanding and every launch that used it has
-// completed; a table used inside a stream capture is kept for the process life.  nullptr + *err
-// on failure.  The first use of a table cannot be captured in a hipGraph (warm up before capturing).
+// (dev_tables.hip): cached by the exact bytes they are made from -- their content, or the inputs
+// a derived table is built from, behind a kind tag (table_acquire builds the table with `fill`
+// only on a miss) -- looked up by a 128-bit hash of those bytes and confirmed by comparing them
+// (a hash collision is a miss, never another table), uploaded once (complete before the call
+// returns).  Every acquire is a hold on the table for ONE launch, released by table_release after
+// that launch is enqueued on `stream` (TableHold does it at scope exit): the cache frees a table
+// only when no hold is outstanding and every launch that used it has completed; a table used
+// inside a stream capture is kept for the process life.  nullptr + *err on failure.  The first use
+// of a table cannot be captured in a hipGraph (warm up before capturing).
+enum TableKind : uint8_t { kTableRaw = 1, kTableMfmaFrag = 2 };
 struct TableHash {
     uint64_t a = 0xcbf29ce484222325ull, c = 0x84222325cbf29ce4ull;
+    std::vector<uint8_t> src;  // every byte added: the identity the cache compares on a hash hit
+    explicit TableHash(TableKind kind) { add_val(kind); }
     void add(const void* p, size_t n);
     template <typename T>
     void add_val(const T& v) { add(&v, sizeof(v)); }

@@ -91,6 +91,63 @@ _lib = None
 _lock = threading.Lock()
 
 
+def _elf_soname(path: Path) -> str | None:
+    """DT_SONAME of a 64-bit little-endian ELF shared object (None if it is not one); reads the
+    headers, the dynamic section and its string table only."""
+    import struct
+
+    try:
+        with open(path, "rb") as f:
+            hdr = f.read(64)
+            if len(hdr) < 64 or hdr[:4] != b"\x7fELF" or hdr[4] != 2 or hdr[5] != 1:
+                return None
+            shoff, = struct.unpack_from("<Q", hdr, 0x28)
+            shentsize, shnum = struct.unpack_from("<HH", hdr, 0x3A)
+            f.seek(shoff)
+            raw = f.read(shentsize * shnum)
+            secs = [struct.unpack_from("<IIQQQQIIQQ", raw, i * shentsize) for i in range(shnum)]
+            for sh in secs:
+                if sh[1] != 6:  # SHT_DYNAMIC; sh_link = its string table
+                    continue
+                f.seek(sh[4])
+                dyn = f.read(sh[5])
+                strtab = secs[sh[6]]
+                for off in range(0, len(dyn) - 15, 16):
+                    tag, val = struct.unpack_from("<qQ", dyn, off)
+                    if tag == 0:
+                        break
+                    if tag == 14:  # DT_SONAME
+                        f.seek(strtab[4] + val)
+                        return f.read(256).split(b"\0", 1)[0].decode()
+    except (OSError, struct.error, IndexError, UnicodeDecodeError):
+        return None
+    return None
+
+
+def _soname_majors(libdir: Path, stem: str) -> set[int]:
+    """Major versions in the DT_SONAME (``stem.so.<major>``) of ``stem.so*`` files in ``libdir``."""
+    majors = set()
+    for p in {q.resolve() for q in libdir.glob(stem + ".so*")}:
+        name = _elf_soname(p) if p.is_file() else None
+        if name and name.startswith(stem + ".so."):
+            head = name[len(stem) + 4:].split(".")[0]
+            if head.isdigit():
+                majors.add(int(head))
+    return majors
+
+
+def _runtime_compatible(torch_lib: Path, rocm_lib: Path = Path("/opt/rocm/lib")) -> bool:
+    """True when torch's bundled HIP / HSA runtimes carry the same soname majors as the ROCm this
+    library was built against (or that ROCm is not installed to compare with): only then may the
+    library run on torch's copies.  An older or newer major keeps /opt/rocm's runtime."""
+    for stem in ("libamdhip64", "libhsa-runtime64"):
+        mine = _soname_majors(rocm_lib, stem)
+        theirs = _soname_majors(torch_lib, stem)
+        if not theirs or (mine and not (mine & theirs)):
+            return False
+    return True
+
+
 def _share_torch_hip_runtime() -> None:
     """Make this library and PyTorch use ONE HIP runtime in a process that has both.
 
@@ -98,7 +155,8 @@ def _share_torch_hip_runtime() -> None:
     /opt/rocm's.  Loaded after torch, libfir_hip binds to torch's copies (the soname is already
     loaded); loaded first, it pulls in /opt/rocm's, torch later loads its own by path, and the
     second HSA runtime in the process finds no device ("No HIP GPUs are available").  So when
-    torch is installed, its runtime is loaded first, whichever of the two is imported first.
+    torch is installed and its runtime has the sonames of the ROCm the library was built with
+    (_runtime_compatible), its runtime is loaded first, whichever of the two is imported first.
     FIR_HIP_OWN_RUNTIME=1 keeps /opt/rocm's (a process without torch uses it anyway)."""
     if os.environ.get("FIR_HIP_OWN_RUNTIME") == "1":
         return
@@ -108,6 +166,8 @@ def _share_torch_hip_runtime() -> None:
     if spec is None or not spec.origin:
         return
     tlib = Path(spec.origin).parent / "lib"
+    if not _runtime_compatible(tlib):
+        return
     for name in ("libhsa-runtime64.so", "libamdhip64.so"):
         p = tlib / name
         if p.exists():
