@@ -271,3 +271,46 @@ def test_u8_long_filter_run_kernel_vs_oracle(L):
                 got = fir_hip.fir1d_fixed_rows(x, hq, frac, acc, stage)
                 want = co.fir1d_rows(x, hq, frac, acc, stage)
                 assert np.array_equal(got, want), (shape, frac, acc, amp, stage)
+
+
+def _hann_taps(L: int, kind: str, scale: float = 1.0) -> np.ndarray:
+    w = np.hanning(L + 2)[1:-1]
+    if kind == "smooth":
+        h = w / w.sum()
+    else:  # windowed low-pass sinc, cutoff 0.1
+        n = np.arange(L) - (L - 1) / 2
+        h = 0.2 * np.sinc(0.2 * n) * w
+        h /= h.sum()
+    return np.rint(h * 4096 * scale).astype(np.int64)
+
+
+# One-chunk u8 filters whose high byte plane is zero in some k-steps (fir1d_mfma_run_kernel HN =
+# 0 / 2 / 4: a Q4.12 filter's taps mostly fit a signed byte): all small taps, a large centre
+# (the windowed sinc), two large taps one or several k-steps apart (past 4 k-steps: both planes
+# everywhere), large taps at the filter's ends, and one large tap on the first / last k-step.
+def _mixed_plane_filters(L: int, rng) -> dict:
+    f = {"smooth": _hann_taps(L, "smooth"), "sinc": _hann_taps(L, "sinc"),
+         "sinc_x3": _hann_taps(L, "sinc", 3.0)}
+    small = rng.integers(-128, 128, L)
+    for name, pos in (("spike_mid", [L // 2]), ("spikes_near", [L // 2, L // 2 + 40]),
+                      ("spikes_far", [3, L - 4]), ("spike_first", [0]), ("spike_last", [L - 1]),
+                      ("spikes_3steps", [L // 2 - 50, L // 2 + 50])):
+        h = small.copy()
+        h[np.clip(pos, 0, L - 1)] = rng.choice([-2000, 1500, 129, -129], len(pos))
+        f[name] = h
+    f["edge_127"] = np.where(rng.random(L) < 0.5, 127, -128)
+    return f
+
+
+@pytest.mark.parametrize("L", [66, 100, 129, 162, 257, 290, 386, 450, 580, 800, 930])
+def test_u8_long_filter_high_plane_skip_vs_oracle(L):
+    rng = np.random.default_rng(1000 + L)
+    co = c_oracle()
+    for shape in [(16, 4096), (3, 3 * 1024 + 24)]:
+        x = rng.integers(0, 256, shape, dtype=np.uint8)
+        x[0, :] = 255
+        for name, hq in _mixed_plane_filters(L, rng).items():
+            for frac, acc in ((12, 32), (14, 24)):
+                got = fir_hip.fir1d_fixed_rows(x, hq, frac, acc, fir_hip.OUT_U8_SAT)
+                want = co.fir1d_rows(x, hq, frac, acc, fir_hip.OUT_U8_SAT)
+                assert np.array_equal(got, want), (shape, name, frac, acc)

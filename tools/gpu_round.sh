@@ -83,6 +83,9 @@ for s in $STEPS; do
                  run "bankab_$v" 200 python tools/lib_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so \
                      abrun/libfir_hip_bank_$v.so 10 bank; fatal $? || exit
              done ;;
+        ltab_*) kind=${s#ltab_}
+             run "ltab_$kind" 400 python tools/long_taps_ab.py ${LT_TAPS:-66,128,257,450,900} \
+                 warmup-fir-filter_amd/fir_hip/libfir_hip.so ${LT_LIBS} --kind "$kind"; fatal $? ;;
         ltab) run long_taps_ab 400 python tools/long_taps_ab.py 66,128,257,450,500,1000,4099 \
                  warmup-fir-filter_amd/fir_hip/libfir_hip.so abrun/libfir_hip_mr_v1.so abrun/libfir_hip_mr_d1.so \
                  abrun/libfir_hip_mr_d3.so abrun/libfir_hip_mr_t4w1d2.so abrun/libfir_hip_mr_old.so; fatal $? ;;

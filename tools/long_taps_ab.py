@@ -1,8 +1,11 @@
 """Dev A/B of the long-filter kernels across builds of libfir_hip.so in ONE process: u8 -> u8
 (and u8 -> int32) FIR over 2^28 samples in 4096-sample rows for each tap count, interleaved
 batches of back-to-back launches timed by HIP events; every build's output must be identical.
-Usage: python tools/long_taps_ab.py <taps,taps,...> <lib> [<lib> ...] [--no-check]
-(--no-check: experiment builds whose outputs are knowingly wrong, timed only)"""
+Usage: python tools/long_taps_ab.py <taps,taps,...> <lib> [<lib> ...] [--no-check] [--kind rand|smooth|sinc]
+(--no-check: experiment builds whose outputs are knowingly wrong, timed only; --kind: the taps --
+rand: uniform in [-2000, 2000) (every k-step needs both byte planes), smooth: a Hann window of unit
+gain in Q4.12 (every tap in [-128, 127] past ~64 taps), sinc: a Hann-windowed low-pass sinc,
+cutoff 0.1, unit gain (only the centre taps need the high byte))"""
 import ctypes
 import sys
 
@@ -10,10 +13,25 @@ import numpy as np
 import torch
 
 
+def taps_of(kind: str, L: int, rng) -> np.ndarray:
+    if kind == "rand":
+        return rng.integers(-2000, 2000, L).astype(np.int32)
+    w = np.hanning(L + 2)[1:-1]
+    if kind == "smooth":
+        h = w / w.sum()
+    else:
+        n = np.arange(L) - (L - 1) / 2
+        h = 0.2 * np.sinc(0.2 * n) * w
+        h /= h.sum()
+    return np.rint(h * 4096).astype(np.int32)
+
+
 def main():
     taps = [int(t) for t in sys.argv[1].split(",")]
     check = "--no-check" not in sys.argv
-    paths = [p for p in sys.argv[2:] if p != "--no-check"]
+    kind = sys.argv[sys.argv.index("--kind") + 1] if "--kind" in sys.argv else "rand"
+    skip = {"--no-check", "--kind", kind}
+    paths = [p for p in sys.argv[2:] if p not in skip]
     libs = [ctypes.CDLL(p) for p in paths]
     dev = torch.device("cuda", 0)
     s = torch.cuda.Stream(device=dev)
@@ -23,9 +41,10 @@ def main():
     x = torch.from_numpy(rng.integers(0, 256, n, dtype=np.uint8)).to(dev)
     ys = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in libs]
     vp, ci, i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+    print(f"kind {kind}", flush=True)
     print(f"{'taps':>5s}" + "".join(f" {p.split('/')[-1][:24]:>24s}" for p in paths), flush=True)
     for L in taps:
-        hq = rng.integers(-2000, 2000, L).astype(np.int32)
+        hq = taps_of(kind, L, rng)
         hc = hq.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
 
         def run(i, k):

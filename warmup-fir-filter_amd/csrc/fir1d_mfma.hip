@@ -600,14 +600,21 @@ template <int STAGE, int TPS_, bool MULTI, int NS>
 constexpr int mr_waves() {
     return mr_waves_of(STAGE, TPS_, MULTI, NS);
 }
-template <int STAGE, int NS, bool MULTI, int TPS_>
+// HN: the k-steps whose taps need the high byte plane.  -1: every k-step (both planes, one
+// accumulator each).  0: none (every tap in [-128, 127]: a Q4.12 filter of small taps, e.g. a long
+// smoothing window): low-plane MFMAs only, the even and odd k-steps in two accumulators (no
+// back-to-back dependent MFMA).  2 / 4: the high plane for k-steps hs0 .. hs0 + HN - 1 only (a
+// windowed filter's large centre taps), their B fragments read at that run-time offset, the low
+// plane in two accumulators as for 0.  One chunk only (the launcher picks HN from the taps).
+template <int STAGE, int NS, bool MULTI, int TPS_, int HN = -1>
 __global__ __launch_bounds__(kBlock, (mr_waves<STAGE, TPS_, MULTI, NS>())) void fir1d_mfma_run_kernel(const uint8_t* __restrict__ x,
                                                                    typename OutTraits<STAGE>::T* __restrict__ y,
                                                                    int64_t rowlen, uint32_t tiles_per_row, uint32_t ntiles,
                                                                    const mf_i32x4* __restrict__ frag, int KS, int P,
-                                                                   uint32_t bias, int mode, int shl, int frac) {
+                                                                   uint32_t bias, int mode, int shl, int frac, int hs0) {
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     constexpr int TPS = TPS_, C = NS;
+    static_assert(HN < 0 || (!MULTI && HN <= NS), "high-plane k-step ranges: one chunk");
     constexpr bool OLDS = STAGE == FIR_OUT_I32;
     constexpr int kDepth = TPS == 1 ? (OLDS ? 3 : kMrDepth1) : TPS == 4 ? kMrMDepth : kMrDepth;
     constexpr int WT = kMfTile + 32 * C - 32;  // window samples per tile and chunk
@@ -634,11 +641,19 @@ __global__ __launch_bounds__(kBlock, (mr_waves<STAGE, TPS_, MULTI, NS>())) void 
 
     // tap fragments: one set (one chunk: loaded once per wave; several: the iteration's chunk,
     // loaded at the top of each iteration)
-    mf_i32x4 a0_lo[C], a0_hi[C];
-    auto load_a = [&](mf_i32x4 (&lo)[C], mf_i32x4 (&hi)[C], int c) __attribute__((always_inline)) {
+    constexpr int NH = HN < 0 ? C : HN > 0 ? HN : 1;  // high-plane fragment registers
+    mf_i32x4 a0_lo[C], a0_hi[NH];
+    auto load_a = [&](mf_i32x4 (&lo)[C], mf_i32x4 (&hi)[NH], int c) __attribute__((always_inline)) {
         const mf_i32x4* f = frag + (int64_t)c * C * 2 * kWave + lane;
+        if constexpr (HN < 0) {
 #pragma unroll
-        for (int s = 0; s < C; ++s) lo[s] = f[(2 * s) * kWave], hi[s] = f[(2 * s + 1) * kWave];
+            for (int s = 0; s < C; ++s) lo[s] = f[(2 * s) * kWave], hi[s] = f[(2 * s + 1) * kWave];
+        } else {
+#pragma unroll
+            for (int s = 0; s < C; ++s) lo[s] = f[(2 * s) * kWave];
+#pragma unroll
+            for (int j = 0; j < HN; ++j) hi[j] = f[(2 * (hs0 + j) + 1) * kWave];
+        }
     };
     // One tile per run and one chunk (the wave's tiles t, t + S, t + 2S, ...): the tile's row and
     // column advance by constant steps (one division at the start instead of one per tile and use,
@@ -701,9 +716,11 @@ __global__ __launch_bounds__(kBlock, (mr_waves<STAGE, TPS_, MULTI, NS>())) void 
         }
     };
 
-    mf_i32x16 acc_ll[TPS], acc_mid[TPS];
+    // acc_ll: the low plane (HN >= 0: its even k-steps), acc_lo2 (HN >= 0): the odd k-steps' low
+    // plane, acc_mid: the high plane
+    mf_i32x16 acc_ll[TPS], acc_mid[TPS], acc_lo2[TPS];
 #pragma unroll
-    for (int q = 0; q < TPS; ++q) acc_ll[q] = mf_i32x16{}, acc_mid[q] = mf_i32x16{};
+    for (int q = 0; q < TPS; ++q) acc_ll[q] = mf_i32x16{}, acc_mid[q] = mf_i32x16{}, acc_lo2[q] = mf_i32x16{};
     mf_i32x16 biasv;
 #pragma unroll
     for (int i = 0; i < 16; ++i) biasv[i] = (int)bias;
@@ -732,7 +749,7 @@ __global__ __launch_bounds__(kBlock, (mr_waves<STAGE, TPS_, MULTI, NS>())) void 
         }
     }
     // one iteration (run rn, chunk c); false at the end
-    auto body = [&](mf_i32x4 (&a_lo)[C], mf_i32x4 (&a_hi)[C]) __attribute__((always_inline)) -> bool {
+    auto body = [&](mf_i32x4 (&a_lo)[C], mf_i32x4 (&a_hi)[NH]) __attribute__((always_inline)) -> bool {
         uint32_t nr = rn;
         int nc = c;
         advance(nr, nc);
@@ -771,6 +788,17 @@ __global__ __launch_bounds__(kBlock, (mr_waves<STAGE, TPS_, MULTI, NS>())) void 
             for (int q = 0; q < TPS; ++q)
                 bq[sl][q] = *reinterpret_cast<const mf_i32x4*>(&pl[q * kMrTileLds + 32 * r + 32 * sl + 16 * hf]);
         };
+        // the high plane's B fragments (HN > 0: k-steps hs0 .., a run-time offset)
+        mf_i32x4 bh[HN > 0 ? HN : 1][TPS];
+        if constexpr (HN > 0) {
+#pragma unroll
+            for (int j = 0; j < HN; ++j)
+#pragma unroll
+                for (int q = 0; q < TPS; ++q) {
+                    const mf_i32x4 v = *reinterpret_cast<const mf_i32x4*>(&pl[q * kMrTileLds + 32 * r + 32 * (hs0 + j) + 16 * hf]);
+                    bh[j][q] = XLDS ? v : v ^ (int)0x80808080;
+                }
+        }
         static_for<0, (BPD < C ? BPD : C)>([&](auto slc) { rd_b(slc); });
         static_for<0, C>([&](auto slc) {
             constexpr int sl = decltype(slc)::value;
@@ -779,7 +807,14 @@ __global__ __launch_bounds__(kBlock, (mr_waves<STAGE, TPS_, MULTI, NS>())) void 
 #pragma unroll
             for (int q = 0; q < TPS; ++q) {
                 const mf_i32x4 b = XLDS ? bq[sl][q] : bq[sl][q] ^ (int)0x80808080;
-                if constexpr (!MULTI && sl == 0) {  // a run's first k-step: the bias, and zero
+                if constexpr (HN >= 0) {  // low plane: even / odd k-steps in two accumulators
+                    mf_i32x16& la = (sl & 1) ? acc_lo2[q] : acc_ll[q];
+                    la = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_lo[sl], b,
+                                                                sl >= 2 ? la : sl == 0 && BIASV ? biasv : mf_i32x16{}, 0, 0, 0);
+                    if constexpr (sl < HN)  // high plane of k-step hs0 + sl
+                        acc_mid[q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_hi[sl], bh[sl][q], sl == 0 ? mf_i32x16{} : acc_mid[q],
+                                                                           0, 0, 0);
+                } else if constexpr (!MULTI && sl == 0) {  // a run's first k-step: the bias, and zero
                     acc_ll[q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_lo[sl], b, BIASV ? biasv : mf_i32x16{}, 0, 0, 0);
                     acc_mid[q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a_hi[sl], b, mf_i32x16{}, 0, 0, 0);
                 } else {
@@ -798,8 +833,10 @@ __global__ __launch_bounds__(kBlock, (mr_waves<STAGE, TPS_, MULTI, NS>())) void 
                 int32_t o[16];
                 uint32_t a[16];
 #pragma unroll
-                for (int i = 0; i < 16; ++i)  // (one chunk: the bias started acc_ll)
-                    a[i] = ((uint32_t)acc_mid[q][i] << 8) + (uint32_t)acc_ll[q][i] + (MULTI || !BIASV ? bias : 0u);
+                for (int i = 0; i < 16; ++i) {  // (one chunk: the bias started acc_ll)
+                    const uint32_t lo = HN >= 0 ? (uint32_t)acc_ll[q][i] + (uint32_t)acc_lo2[q][i] : (uint32_t)acc_ll[q][i];
+                    a[i] = (HN != 0 ? ((uint32_t)acc_mid[q][i] << 8) : 0u) + lo + (MULTI || !BIASV ? bias : 0u);
+                }
                 if (mode == 0) {
 #pragma unroll
                     for (int i = 0; i < 16; ++i)
@@ -897,18 +934,48 @@ static hipError_t launch_mfma_run(const void* x, void* y, int64_t rl, int64_t tp
     const uint32_t tp = (uint32_t)tpr, nt = (uint32_t)ntiles;
     const int mode = fast ? 0 : acc_bits == 32 ? 1 : 2;
     const int shl = mode == 2 ? 32 - acc_bits : 0;
+    // one chunk, u8 stage: the k-steps whose taps need the high byte plane (a tap outside
+    // [-128, 127]); k-step st multiplies taps c + P - 32 st - 31 .. c + P - 32 st + 31
+    int hn = -1, hs0 = 0;
+    if (!multi && tps == 1 && STAGE == FIR_OUT_U8_SAT) {
+        const int c = L / 2;
+        int smin = ksp, smax = -1;
+        for (int t = 0; t < L; ++t) {
+            if (hq[t] >= -128 && hq[t] <= 127) continue;
+            const int lo_st = (c + P - t - 31 + 31) / 32, hi_st = (c + P - t + 31) / 32;  // ceil / floor
+            for (int st = lo_st < 0 ? 0 : lo_st; st <= hi_st && st < ksp; ++st) smin = st < smin ? st : smin, smax = st > smax ? st : smax;
+        }
+        // a partial high plane pays a third accumulator (16 more registers and combine adds per
+        // output): worth it only when it drops at least twice the k-steps it keeps (A/B at 66 / 128
+        // / 257 / 450 / 900 taps, windowed sinc: 116 / 124 / 146 / 209 / 454 -> 138 / 137 / 149 / 191
+        // / 338 us, profiles/r05/long_taps_hn_ab.txt)
+        const int need = smax < 0 ? 0 : smax - smin + 1;
+        hn = need == 0 ? 0 : need <= 2 ? 2 : need <= 4 ? 4 : -1;
+        if (hn > 0 && ksp < 3 * hn) hn = -1;
+        if (hn > 0) hs0 = smin < ksp - hn ? smin : ksp - hn;
+    }
     auto go = [&](auto nsc, auto mc) {
         constexpr int NS = decltype(nsc)::value;
         constexpr bool M = decltype(mc)::value;
-        if constexpr (!M && NS <= kMrT1Ns)
-            hipLaunchKernelGGL((fir1d_mfma_run_kernel<STAGE, NS, M, 1>), dim3(blocks), dim3(kBlock), 0, s,
-                               (const uint8_t*)x, (OutT*)y, rl, tp, nt, fr, ksp, P, bias, mode, shl, frac);
-        else if constexpr (M && MTPS == 4)
+        if constexpr (!M && NS <= kMrT1Ns) {
+            auto one = [&](auto hnc) {
+                constexpr int H = decltype(hnc)::value;
+                hipLaunchKernelGGL((fir1d_mfma_run_kernel<STAGE, NS, M, 1, H>), dim3(blocks), dim3(kBlock), 0, s,
+                                   (const uint8_t*)x, (OutT*)y, rl, tp, nt, fr, ksp, P, bias, mode, shl, frac, hs0);
+            };
+            if constexpr (STAGE == FIR_OUT_U8_SAT) {
+                if (hn == 0) return one(std::integral_constant<int, 0>{});
+                if (hn == 2) return one(std::integral_constant<int, 2>{});
+                if (hn == 4) return one(std::integral_constant<int, 4>{});
+            }
+            one(std::integral_constant<int, -1>{});
+        } else if constexpr (M && MTPS == 4) {
             hipLaunchKernelGGL((fir1d_mfma_run_kernel<STAGE, NS, M, 4>), dim3(blocks), dim3(kBlock), 0, s,
-                               (const uint8_t*)x, (OutT*)y, rl, tp, nt, fr, ksp, P, bias, mode, shl, frac);
-        else
+                               (const uint8_t*)x, (OutT*)y, rl, tp, nt, fr, ksp, P, bias, mode, shl, frac, 0);
+        } else {
             hipLaunchKernelGGL((fir1d_mfma_run_kernel<STAGE, NS, M, kMrTps>), dim3(blocks), dim3(kBlock), 0, s,
-                               (const uint8_t*)x, (OutT*)y, rl, tp, nt, fr, ksp, P, bias, mode, shl, frac);
+                               (const uint8_t*)x, (OutT*)y, rl, tp, nt, fr, ksp, P, bias, mode, shl, frac, 0);
+        }
     };
     using std::integral_constant;
 #define FIR_MR_NS(n)                                                                       \
