@@ -89,7 +89,7 @@ GATE_MODE = os.environ.get("FIR_GATE_MODE", "serial")
 KERNELS = {"fir1d_i16": "fir1d_reg_kernel", "cplx_i16": "fir1d_reg_kernel", "fir2d_u8": "fir2d_pk16_strip_kernel",
            "fir1d_u8": "fir1d_reg_kernel", "ideal_u8": "fir1d_ideal_kernel", "bank_u8": "fir1d_reg_kernel",
            "restore_u8": "restore_map_kernel",
-           "pipeline_fixed3": "fir1d_reg_kernel (4-filter bank, one launch per image; the 7 launches as parallel nodes of one hipGraph)",
+           "pipeline_fixed3": "fir1d_reg_kernel (4-filter bank, one launch per image, 7 launches in one hipGraph)",
            "metrics_u8": "metrics_leaf_kernel (+ metrics_prep: unset markers; chain and final in the launch)"}
 NUMPY_ONLY = ("restore_u8", "metrics_u8", "pipeline_fixed3")  # no C oracle leg: the NumPy restatement is the CPU baseline
 ROOF_RAMP, ROOF_LAUNCHES = 100, 200  # roofline loop: untimed ramp, then timed launches of the dominant kernel
@@ -240,7 +240,7 @@ class Workload:
             # configs[0]: the fixed 3-tap stage of pipeline_fir_1d.py on the 7 golden images (the
             # reference's decoded u8 inputs, tests/golden/images_u8.npz) x the 4 filters of
             # h_coeff_3tap_map: one fused 4-filter launch per image, the 7 launches captured once
-            # into a hipGraph (torch.cuda.CUDAGraph) as independent nodes and replayed as one step
+            # into a hipGraph (torch.cuda.CUDAGraph) and replayed as one step
             with np.load(ROOT / "tests" / "golden" / "images_u8.npz") as d:
                 self.images = [(k, np.ascontiguousarray(d[k])) for k in sorted(d.files)]
             self.x_host = self.images[0][1]
@@ -302,38 +302,21 @@ class Workload:
         """Algorithmic bytes of one step (in + out bytes per unit x units)."""
         return int(round(self.units * self.bytes_per_unit))
 
-    def _bank_images(self, fork: bool = False):
-        """One fused 4-filter launch per image.  fork (inside the graph capture): each image's launch
-        on its own side stream, forked from and joined back into the capturing stream by events, so
-        the graph holds 7 independent kernel nodes the GPU runs side by side (the 6 small images
-        take ~4.5 us each, mostly launch latency, beside the 4499 x 2999 one)."""
-        if not fork:
-            for x, y in zip(self.xs, self.ys):
-                torch_ops.fir1d_fixed_rows_multi_dev(x, BANK3, 12, 32, fir_hip.OUT_U8_SAT, out=y)
-            return
-        main = torch.cuda.current_stream()
-        start = torch.cuda.Event()
-        start.record(main)
-        done = []
-        for (x, y), side in zip(zip(self.xs, self.ys), self.sides):
-            side.wait_event(start)
-            with torch.cuda.stream(side):
-                torch_ops.fir1d_fixed_rows_multi_dev(x, BANK3, 12, 32, fir_hip.OUT_U8_SAT, out=y)
-            ev = torch.cuda.Event()
-            ev.record(side)
-            done.append(ev)
-        for ev in done:
-            main.wait_event(ev)
+    def _bank_images(self):
+        """One fused 4-filter launch per image, in order.  (As 7 parallel graph branches on forked
+        streams the stage took 88.3 us instead of 55.8: the small launches slowed the large one they
+        shared the CUs with; gpurun_out r05f.)"""
+        for x, y in zip(self.xs, self.ys):
+            torch_ops.fir1d_fixed_rows_multi_dev(x, BANK3, 12, 32, fir_hip.OUT_U8_SAT, out=y)
 
     def bulk(self):
         if self.name == "pipeline_fixed3":
             if self.graph is None:  # capture the 7 launches once (warmed outside the capture)
                 self._bank_images()
                 torch.cuda.current_stream().synchronize()
-                self.sides = [torch.cuda.Stream(device=self.dev) for _ in self.xs]
                 self.graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(self.graph, stream=torch.cuda.current_stream()):
-                    self._bank_images(fork=True)
+                    self._bank_images()
             self.graph.replay()
         elif self.name == "fir2d_u8":
             torch_ops.fir2d_fixed_dev(self.x, self.hq2, 12, 32, fir_hip.OUT_U8_SAT, out=self.y)
@@ -721,7 +704,7 @@ def run_sub_configs(args, dev) -> tuple[dict, bool]:
                                        f"full workload ({wl.units} units), {tc:.2f} s"},
         }
         if name == "pipeline_fixed3":
-            entry["roofline"]["kernel_avg_us_is"] = "one graph replay = 7 concurrent launches (one stage)"
+            entry["roofline"]["kernel_avg_us_is"] = "one graph replay = 7 launches (one stage)"
             entry["stage_wall"] = pipeline_stage_wall()
         out[label] = entry
         del wl, ref

@@ -83,6 +83,8 @@ for s in $STEPS; do
                  run "bankab_$v" 200 python tools/lib_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so \
                      abrun/libfir_hip_bank_$v.so 10 bank; fatal $? || exit
              done ;;
+        libab_*) wl=${s#libab_}
+             run "libab_$wl" 200 python tools/lib_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so ${AB_LIB} 10 "$wl"; fatal $? ;;
         ltab_*) kind=${s#ltab_}
              run "ltab_$kind" 400 python tools/long_taps_ab.py ${LT_TAPS:-66,128,257,450,900} \
                  warmup-fir-filter_amd/fir_hip/libfir_hip.so ${LT_LIBS} --kind "$kind"; fatal $? ;;

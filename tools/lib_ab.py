@@ -1,8 +1,10 @@
 """Dev A/B: one register-kernel workload from two builds of libfir_hip.so in one process,
 interleaved batches of back-to-back launches timed by HIP events (outputs must be equal).
 Workloads: i16 = the headline (2^28 int16 -> int32, 5-tap sharpen), u8 = 2^28 u8 -> sat-u8 in
-4096-sample rows (5-tap sharpen), bank = the 4-filter 3-tap u8 bank (h_coeff_3tap_map).
-Usage: python tools/lib_ab.py <lib A> <lib B> [rounds] [i16|u8|bank]"""
+4096-sample rows (5-tap sharpen), bank = the 4-filter 3-tap u8 bank (h_coeff_3tap_map),
+bankw<W> = the same bank over rows of W samples (bankw4499: the reference's widest image's rows,
+not a whole number of 16-byte vectors).
+Usage: python tools/lib_ab.py <lib A> <lib B> [rounds] [i16|u8|bank|bankw<W>]"""
 import ctypes
 import sys
 
@@ -27,11 +29,13 @@ def main():
         ys = [torch.empty(n, dtype=torch.int32, device=dev) for _ in libs]
         in_dt, rows, width, stage, h, L, F = 1, 1, n, 1, SHARPEN5, 5, 1
     else:
+        width = int(wl[5:]) if wl.startswith("bankw") else 4096
+        n = n // width * width
         x = torch.from_numpy(rng.integers(0, 256, n, dtype=np.uint8)).to(dev)
-        F = 4 if wl == "bank" else 1
+        F = 4 if wl.startswith("bank") else 1
         ys = [torch.empty(F * n, dtype=torch.uint8, device=dev) for _ in libs]
-        in_dt, rows, width, stage = 0, n // 4096, 4096, 0
-        h, L = (BANK3, 3) if wl == "bank" else (SHARPEN5, 5)
+        in_dt, rows, stage = 0, n // width, 0
+        h, L = (BANK3, 3) if wl.startswith("bank") else (SHARPEN5, 5)
     hc = (ctypes.c_int32 * len(h))(*h)
     vp, ci = ctypes.c_void_p, ctypes.c_int
 
