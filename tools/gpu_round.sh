@@ -37,10 +37,10 @@ for s in $STEPS; do
         benchcplx) run bench_cplx 300 python bench.py --workload cplx_i16 --cpu-seconds 5; fatal $? ;;
         bench2d) run bench_2d 300 python bench.py --workload fir2d_u8 --cpu-seconds 5; fatal $? ;;
         prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-                  python bench.py --steps 200 --warmup 100 --cpu-seconds 0 --no-parity; fatal $? ;;
+                  python bench.py --steps 200 --warmup 100 --cpu-seconds 0 --no-parity --no-configs; fatal $? ;;
         pmc) for c in FETCH_SIZE WRITE_SIZE; do
                  run "pmc_$c" 300 rocprofv3 --pmc "$c" --kernel-trace -d "$OUT/pmc_$c" -o run --output-format csv -- \
-                     python bench.py --steps 10 --warmup 2 --cpu-seconds 0 --no-parity --roofline-launches 5 \
+                     python bench.py --steps 10 --warmup 2 --cpu-seconds 0 --no-parity --no-configs --roofline-launches 5 \
                      --roofline-ramp 0; fatal $? || exit
              done ;;
         bench_*) wl=${s#bench_}
@@ -116,6 +116,13 @@ for s in $STEPS; do
              run "ktrace_$wl" 150 rocprofv3 --kernel-trace -d "$OUT/ktrace_$wl" -o run --output-format csv -- \
                  python bench.py --workload "$wl" --steps 20 --warmup 10 --cpu-seconds 0 --no-parity \
                  --roofline-launches 20 --roofline-ramp 10; fatal $? ;;
+        sqlt_*) kind=${s#sqlt_}
+              run "sq_lt257_$kind" 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+                 SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_VALU --kernel-trace -d "$OUT/sq_lt257_$kind" \
+                 -o run --output-format csv -- python tools/long_taps_one.py 257 u8 6 "$kind"; fatal $? || exit
+              run "sq_lt257b_$kind" 150 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_LDS \
+                 SQ_INSTS_MFMA --kernel-trace -d "$OUT/sq_lt257b_$kind" -o run --output-format csv -- \
+                 python tools/long_taps_one.py 257 u8 6 "$kind"; fatal $? ;;
         sqlt) run sq_lt257 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
                  SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_VALU --kernel-trace -d "$OUT/sq_lt257" \
                  -o run --output-format csv -- python tools/long_taps_one.py 257 u8 6; fatal $?

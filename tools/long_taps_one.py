@@ -1,5 +1,6 @@
 """Dev driver for profiling one long-filter configuration: 2^28 samples, `reps` back-to-back
-device launches.  Usage: python tools/long_taps_one.py <taps> <i16|i16u8|u8> [reps]"""
+device launches.  Usage: python tools/long_taps_one.py <taps> <i16|i16u8|u8> [reps] [rand|smooth|sinc]
+(the tap kinds of tools/long_taps_ab.py; default rand)"""
 import sys
 from pathlib import Path
 
@@ -30,7 +31,11 @@ def main():
         x = torch.from_numpy(rng.integers(0, 256, (n // 4096, 4096), dtype=np.uint8)).to(dev)
         y = torch.empty(x.shape, dtype=torch.uint8, device=dev)
         st = fir_hip.OUT_U8_SAT
-    hq = torch_ops.Taps(rng.integers(-2000, 2000, L).tolist())
+    tap_kind = sys.argv[4] if len(sys.argv) > 4 else "rand"
+    sys.path.insert(0, str(ROOT / "tools"))
+    from long_taps_ab import taps_of
+
+    hq = torch_ops.Taps(taps_of(tap_kind, L, rng).tolist())
     for _ in range(reps):
         torch_ops.fir1d_fixed_rows_dev(x, hq, 12, 32, st, out=y)
     torch.cuda.synchronize()
