@@ -101,43 +101,6 @@ def timing(reps: int = 200) -> None:
         print(f"  {name:9s} {path:5s} {min(v):8.1f} us ({min(v) / 4:6.2f} us/frame)")
 
 
-def rows_sweep(reps: int = 200) -> None:
-    """Strip length of the MFMA kernel (FIR2D_MFMA_ROWS; unset = one resident round)."""
-    import torch
-
-    from fir_hip import torch_ops
-
-    os.environ["FIR2D_PATH"] = "mfma"
-    dev = torch.device("cuda:0")
-    frames = torch.from_numpy(np.random.default_rng(20260227).integers(0, 256, (4, 8192, 8192), dtype=np.uint8)).to(dev)
-    out = torch.empty_like(frames)
-    ref = torch.empty_like(frames)
-    st = torch.cuda.current_stream()
-    for name, sweep in (("gen5x5", ("", "28", "56", "84", "98", "112")), ("sep_lp5", ("", "56", "98")),
-                        ("q412_5x5", ("", "56", "98")), ("lap3", ("", "32", "88"))):
-        hq = KERNELS[name]
-        os.environ.pop("FIR2D_MFMA_ROWS", None)
-        torch_ops.fir2d_fixed_dev(frames, hq, out=ref)
-        line = []
-        for rows in sweep * 2:
-            if rows:
-                os.environ["FIR2D_MFMA_ROWS"] = rows
-            else:
-                os.environ.pop("FIR2D_MFMA_ROWS", None)
-            for _ in range(20):
-                torch_ops.fir2d_fixed_dev(frames, hq, out=out)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(st)
-            for _ in range(reps):
-                torch_ops.fir2d_fixed_dev(frames, hq, out=out)
-            e1.record(st)
-            torch.cuda.synchronize()
-            assert torch.equal(out, ref), (name, rows)
-            line.append(f"{rows or 'auto'}:{e0.elapsed_time(e1) * 1000 / reps:.1f}")
-        print(f"{name:9s} us per 4-frame launch by strip rows: " + "  ".join(line), flush=True)
-    os.environ.pop("FIR2D_MFMA_ROWS", None)
-
-
 if __name__ == "__main__":
     what = sys.argv[1:] or ["parity", "time"]
     t0 = time.time()
@@ -145,6 +108,4 @@ if __name__ == "__main__":
         parity()
     if "time" in what:
         timing()
-    if "rows" in what:
-        rows_sweep()
     print(f"done in {time.time() - t0:.1f} s")

@@ -32,16 +32,11 @@
 // (fir1d_mfma.hip) when its layout conditions hold, else the v_dot2 LDS kernel.  Measured at
 // 2^28 samples (profiles/r02/long_taps_*.txt): u8 samples 90-97 us on MFMA at every length vs
 // 190-425 us on LDS; int16 -> u8 152-163 vs 192-416; int16 -> int32 MFMA 289-291 us flat,
-// LDS 249-275 up to 31 taps and 298-405 from 40: int16 -> int32 below FIR_MFMA_MIN_TAPS_I32
-// stays on LDS.  Both overridable for A/B builds (65 keeps everything on LDS).
-#ifndef FIR_MFMA_MIN_TAPS
-#define FIR_MFMA_MIN_TAPS 10
-#endif
-#ifndef FIR_MFMA_MIN_TAPS_I32
-#define FIR_MFMA_MIN_TAPS_I32 40
-#endif
+// LDS 249-275 up to 31 taps and 298-405 from 40: int16 -> int32 below kMfmaMinTapsI32 stays on LDS.
 
 namespace fir {
+
+constexpr int kMfmaMinTaps = 10, kMfmaMinTapsI32 = 40;
 
 // ---------------------------------------------------------------------------------------
 // Generic LDS sliding-window kernel: any tap count, any channel count.  A workgroup owns
@@ -270,7 +265,7 @@ int launch_fir1d_rows(const void* x, int in_dtype, int64_t rows, int64_t width, 
                     ? launch_reg_taps<int16_t, FIR_OUT_U8_SAT, 2, 1>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream)
                     : launch_reg_taps<int16_t, FIR_OUT_I32, 2, 1>(L, x, y, rows, total, rowlen, hq, frac, acc_bits, stream);
         }
-    } else if (L >= (in_dtype == FIR_IN_I16 && stage == FIR_OUT_I32 ? FIR_MFMA_MIN_TAPS_I32 : FIR_MFMA_MIN_TAPS) &&
+    } else if (L >= (in_dtype == FIR_IN_I16 && stage == FIR_OUT_I32 ? kMfmaMinTapsI32 : kMfmaMinTaps) &&
                mfma_path_ok(x, y, in_dtype, rows, rowlen, total, ch, hq, L, frac, acc_bits)) {
         e = launch_fir1d_mfma(x, in_dtype, rows, rowlen, total, hq, L, frac, acc_bits, stage, y, stream);
     } else if (lds_path_ok(x, y, in_dtype, rows, rowlen, total, ch, hq, L, frac, acc_bits)) {

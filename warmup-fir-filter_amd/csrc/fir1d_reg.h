@@ -95,19 +95,13 @@ struct TapsN {
     uint32_t noclamp[F];
 };
 
-#ifndef FIR_REG_SKIP0  // 1: packed-16 filters skip their zero taps (A/B builds: make abreg)
-#define FIR_REG_SKIP0 1
-#endif
-#ifndef FIR_REG_NOCLAMP  // 0: always clamp (A/B builds: make abreg)
-#define FIR_REG_NOCLAMP 1
-#endif
 // noclamp[] for the u8 stage of the no-wrap v_dot2 form (host)
 template <int L, int F>
 inline void plan_u8_noclamp(TapsN<L, F>& t, int frac) {
     for (int f = 0; f < F; ++f) {
         int64_t vmin = frac >= 1 && frac <= 22 ? (int64_t)1 << (frac - 1) : -1, vmax = vmin;
         for (int k = 0; k < L; ++k) (t.h[f][k] > 0 ? vmax : vmin) += 255 * (int64_t)t.h[f][k];
-        t.noclamp[f] = FIR_REG_NOCLAMP && vmin >= 0 && vmax < ((int64_t)256 << frac) ? 1u : 0u;
+        t.noclamp[f] = vmin >= 0 && vmax < ((int64_t)256 << frac) ? 1u : 0u;
     }
 }
 
@@ -380,7 +374,7 @@ __device__ __forceinline__ void u8_pk16_vec(const uint32_t* P, const uint32_t* h
     for (int q = 0; q < VEC / 2; ++q) a[q] = pk_mad16(P[2 * q], hb[0], bias);
 #pragma unroll
     for (int i = 1; i < L; ++i)
-        if (!FIR_REG_SKIP0 || hb[i] != 0u)  // wave-uniform: a zero tap (the bank's edge filter) costs nothing
+        if (hb[i] != 0u)  // wave-uniform: a zero tap (the bank's edge filter) costs nothing
 #pragma unroll
             for (int q = 0; q < VEC / 2; ++q) a[q] = pk_mad16(P[2 * q + i], hb[i], a[q]);
 #pragma unroll

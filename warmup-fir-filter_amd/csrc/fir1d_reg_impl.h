@@ -24,13 +24,9 @@ namespace fir {
 // Edge dwords (kEdgeDword): one wave-wide dword load for both tile edges instead of two
 // lane-masked 16-byte loads: headline 246.6-250.6 -> 244.4-244.9 us, u8 bank 230.6 -> 224.3 us,
 // one u8 filter unchanged (profiles/r02/micro_i16_edw.txt, micro_u8_edw.txt).
-#ifndef FIR_REG_EDGE_DWORD  // overridable for A/B builds (make abreg)
-#define FIR_REG_EDGE_DWORD 1
-#endif
-constexpr int kRegFlags = kCoal | kNtStore | (FIR_REG_EDGE_DWORD ? kEdgeDword : 0);
-#ifndef FIR_REG_BANK_FLAGS  // extra flags of fused banks (F > 1; A/B builds: kXcd = 8, kPersist = 4)
-#define FIR_REG_BANK_FLAGS 0
-#endif
+// A fused bank keeps the same flags: an XCD-major block order and a persistent grid measured
+// slower or equal (profiles/r04/bank_ab.txt).
+constexpr int kRegFlags = kCoal | kNtStore | kEdgeDword;
 constexpr int kPersistBlocks = 2048;
 
 template <typename InT, int STAGE, int L, int CH, int F, int FL>
@@ -62,13 +58,6 @@ static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t
         }
     } else if (hl != nullptr || hr != nullptr) {
         return hipErrorInvalidValue;  // shards with halos are single-filter calls
-    }
-    if constexpr (F > 1 && FIR_REG_BANK_FLAGS != 0) {
-        constexpr int FB = FL | FIR_REG_BANK_FLAGS;
-        reg_launch_geometry<InT, kRegU<InT, F>, FB>(total, kPersistBlocks, &ntiles, &blocks);
-        hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, kRegU<InT, F>, FB, F>), dim3((unsigned)blocks), dim3(kBlock),
-                           0, stream, (const InT*)x, (OutT*)y, g, t, 32 - acc_bits, frac, ntiles);
-        return hipGetLastError();
     }
     hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, kRegU<InT, F>, FL, F>), dim3((unsigned)blocks), dim3(kBlock), 0,
                        stream, (const InT*)x, (OutT*)y, g, t, 32 - acc_bits, frac, ntiles);

@@ -18,11 +18,8 @@ hipError_t launch_reg_taps(int L, const void* x, void* y, int64_t rows, int64_t 
 
 // Chunks of 64 vectors per wave (the tile), by sample type and filter count (rationale and
 // measurements: fir1d_reg_impl.h).
-#ifndef FIR_REG_BANK_U  // chunks per wave of a fused u8 bank (A/B builds: make abreg)
-#define FIR_REG_BANK_U 1
-#endif
 template <typename InT, int F>
-constexpr int kRegU = sizeof(InT) == 1 && F == 1 ? 4 : (sizeof(InT) == 1 ? FIR_REG_BANK_U : 1);
+constexpr int kRegU = sizeof(InT) == 1 && F == 1 ? 4 : 1;
 
 // Samples per wave tile of the single-filter register kernel (64 lanes x U chunks x 16 bytes).
 inline int64_t reg_tile_samples(bool u8) { return u8 ? 64 * kRegU<uint8_t, 1> * 16 : 64 * kRegU<int16_t, 1> * 8; }

@@ -36,24 +36,13 @@ constexpr int kPdSep = 3;
 constexpr int kPdGen = 2;
 // packed-16 form: 32-row strips, rows 4 ahead (23.5 vs 24.3 us for 16 rows / 3 ahead; a
 // memory-only twin of the same loop takes 21.1 us, profiles/r01/micro2d_copy.txt)
-#ifndef FIR2D_PK_STRIP  // A/B builds
-#define FIR2D_PK_STRIP 32
-#endif
-constexpr int kStrip2dPk = FIR2D_PK_STRIP;
-#ifndef FIR2D_PK_PD  // A/B builds
-#define FIR2D_PK_PD 4
-#endif
-constexpr int kPdPk = FIR2D_PK_PD;
-#ifndef FIR2D_PK_MINW  // A/B builds: waves per SIMD the register allocation must allow
-#define FIR2D_PK_MINW 1
-#endif
-constexpr int kMinwPk = FIR2D_PK_MINW;
-#ifndef FIR2D_PK_ROLLED  // A/B builds: 0 = the fully unrolled 32-row strip kernel
-#define FIR2D_PK_ROLLED 1  // 0: the unrolled 32-row fir2d_reg_kernel strip
-#endif
+constexpr int kStrip2dPk = 32;
+constexpr int kPdPk = 4;
+constexpr int kMinwPk = 1;  // waves per SIMD the register allocation must allow
 
-// The separable packed-16 form on fir2d_pk16_strip_kernel: strips of about kPkRows rows (whole
-// turns of U input rows), FIR2D_PK_ROWS=n forces n (A/B).  Short strips keep the two neighbours
+// The separable packed-16 form on fir2d_pk16_strip_kernel (frames below 2^31 pixels; larger ones
+// keep the unrolled 32-row fir2d_reg_kernel strip): strips of about kPkRows rows (whole turns of U
+// input rows).  Short strips keep the two neighbours
 // that share R - 1 rows in step with each other (see the kernel's walk directions): 16-26 rows
 // measured 79.7-81.3 us per 4 frames, 6 rows 97, 36 rows 86, one resident round (56 rows) 85.5
 // (profiles/r03/ab2d_pk16_rows.txt).
@@ -64,8 +53,7 @@ static hipError_t launch_pk16_rolled(const uint8_t* x, uint8_t* y, int64_t frame
     constexpr int PD = kPdPk, U = p16_lcm(R, PD + 1);
     auto kern = fir2d_pk16_strip_kernel<R, C, PD, MODE, kMinwPk>;
     const int64_t gx = (W / 16 + kBlock - 1) / kBlock;
-    const char* env = getenv("FIR2D_PK_ROWS");
-    int64_t rows = env && atoi(env) > 0 ? atoi(env) : kPkRows;
+    int64_t rows = kPkRows;
     // whole turns of U input rows per strip (S + R - 1 a multiple of U), and at most 65535 strips
     rows = std::max<int64_t>(rows, (H + 65534) / 65535);
     const int64_t lo = rows;
@@ -79,18 +67,12 @@ static hipError_t launch_pk16_rolled(const uint8_t* x, uint8_t* y, int64_t frame
 }
 // general packed-16 form: 16-row strips (a 32-row strip's R*C MACs per row exceed the forced
 // unroll budget: the loop stays rolled and its ring spills to scratch)
-#ifndef FIR2D_PKG_VEC  // overridable for the A/B builds (tools/lib_ab2d.py)
-#define FIR2D_PKG_VEC 16
-#define FIR2D_PKG_STRIP 16
-#define FIR2D_PKG_PD 0
-#endif
-constexpr int kVec2dPkGen = FIR2D_PKG_VEC;
-constexpr int kStrip2dPkGen = FIR2D_PKG_STRIP;
-// prefetch depth (0 = by tap count): rows 2 ahead for 5x5-size kernels (0.5-3 % faster than
-// depth 3 over two A/B runs), 3 ahead for smaller ones (3x3: 21.9 vs 22.3 us at depth 2;
-// profiles/r01/ab2d_pk16_general.txt)
+constexpr int kVec2dPkGen = 16;
+constexpr int kStrip2dPkGen = 16;
+// prefetch depth: rows 2 ahead for 5x5-size kernels (0.5-3 % faster than depth 3 over two A/B
+// runs), 3 ahead for smaller ones (3x3: 21.9 vs 22.3 us at depth 2; profiles/r01/ab2d_pk16_general.txt)
 template <int R, int C>
-constexpr int pd_pk_gen() { return FIR2D_PKG_PD ? FIR2D_PKG_PD : (R * C >= 20 ? 2 : 3); }
+constexpr int pd_pk_gen() { return R * C >= 20 ? 2 : 3; }
 
 // Generic: one output per thread, exact 64-bit sum (mod 2^64, see round64), global loads (L1/L2
 // absorb the reuse), taps of any count from HBM; rows grid-strided (any height).
@@ -204,7 +186,7 @@ static hipError_t launch2d_reg(const uint8_t* x, void* y, int64_t frames, int64_
         // packed 16-bit pixel pairs when the whole sum provably fits 16 bits (u8 stage only)
         if constexpr (STAGE == FIR_OUT_U8_SAT) {
             const int pk = nowrap ? plan_pk16(t, t.col, rowt, frac) : 0;
-            if (FIR2D_PK_ROLLED && H * W < ((int64_t)1 << 31)) {
+            if (H * W < ((int64_t)1 << 31)) {
                 if (pk == (kMode2dPk16 | kMode2dPkHi8))
                     return launch_pk16_rolled<R, C, kMode2dPk16 | kMode2dPkHi8>(x, (uint8_t*)y, frames, H, W, t, s);
                 if (pk == kMode2dPk16) return launch_pk16_rolled<R, C, kMode2dPk16>(x, (uint8_t*)y, frames, H, W, t, s);

@@ -38,31 +38,15 @@ namespace fir {
 constexpr int kM2Tile = 1024;   // output pixels per wave and row (32 blocks of 32)
 constexpr int kM2MaxR = 7;
 constexpr int kM2MaxC = 5;      // horizontal halo <= 2 pixels per side
-#ifndef FIR2D_MFMA_LDS_STORE    // outputs through LDS into lane-contiguous 16-byte pieces
-#define FIR2D_MFMA_LDS_STORE 1
-#endif
-#ifndef FIR2D_MFMA_COLFAST       // wave order: column tiles fastest (1) or strips fastest (0)
-#define FIR2D_MFMA_COLFAST 1
-#endif
-#ifndef FIR2D_MFMA_ALT           // odd strips walk up (0: every strip walks down; A/B builds)
-#define FIR2D_MFMA_ALT 1
-#endif
-#ifndef FIR2D_MFMA_MINW
-#define FIR2D_MFMA_MINW 3
-#endif
+constexpr int kM2MinWaves = 3;  // waves per SIMD the one-plane kernel's registers must allow
 // Register-ring rows (R in use + 8 - R in flight).  With strips sized to one resident round an
 // 8-row ring (8-row strip granularity: 3008 waves for 3072 slots at 8192^2 x 4) beats the 7-row
 // ring (14-row granularity: 2688 waves): general 5x5 88.0 -> 87.4 us, two byte planes 109.0 ->
 // 105.1 us per 4-frame launch; deeper rings are slower (16 rows: 110-165 us)
-// (profiles/r02/ab2d_mfma_ring_*.txt).  FIR2D_MFMA_RING overrides it (A/B builds); the strip
-// length is chosen at launch (m2_rows_per_strip).
+// (profiles/r02/ab2d_mfma_ring_*.txt).  The strip length is chosen at launch (m2_rows_per_strip).
 template <int R>
 struct M2Geom {
-#ifdef FIR2D_MFMA_RING
-    static constexpr int RING = FIR2D_MFMA_RING;
-#else
     static constexpr int RING = 8;
-#endif
 };
 
 // Tap bytes by diagonal: tm[p][m][33 - d] = byte p of h'[m][C/2 + d] (0 outside the row), d = r - k
@@ -89,7 +73,7 @@ constexpr uint32_t kM2Off = 0x80000000u;   // a voffset outside every descriptor
 // (255 sum|h| + 2^(f-1)) 2^(16-f) < 2^31, so bits 16..31 of (sum + 2^(f-1)) << (16 - f) are the
 // rounded output as an int16, saturated to u8 by v_sat_pk_u8_i16.
 template <int R, int NP, bool FAST, bool ACC32>
-__global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_mfma_kernel(
+__global__ __launch_bounds__(kBlock, NP == 1 ? kM2MinWaves : 2) void fir2d_mfma_kernel(
     const uint8_t* __restrict__ x, uint8_t* __restrict__ y, int64_t H, int64_t W, uint32_t ncol, uint32_t nstrip,
     uint32_t nwaves, int rows_per_strip, Mfma2Taps taps, uint32_t bias, int sh, int shl, int frac) {
     constexpr int U = R - 1 - R / 2;  // input rows above an output row
@@ -113,12 +97,9 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
     // addressing below is scalar
     const uint32_t w = __builtin_amdgcn_readfirstlane(b * (kBlock / kWave) + (threadIdx.x >> 6));
     if (w >= nwaves) return;  // wave-uniform
-#if FIR2D_MFMA_COLFAST
-    // column tiles fastest: the 4 waves of a block read 4 KiB contiguous of each row
+    // column tiles fastest: the 4 waves of a block read 4 KiB contiguous of each row (strips fastest,
+    // each wave a different DRAM page: 99 vs 87.3 us per 4 frames, profiles/r02/ab2d_mfma_colfast.txt)
     const uint32_t col = w % ncol, strip = (w / ncol) % nstrip, frame = w / (nstrip * ncol);
-#else
-    const uint32_t strip = w % nstrip, col = (w / nstrip) % ncol, frame = w / (nstrip * ncol);
-#endif
     const int64_t fo = (int64_t)frame * H * W;
     const uint8_t* xf = x + fo;
     uint8_t* yf = y + fo;
@@ -130,7 +111,7 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
     // read hits L2 (fir2d_pk16.h measured it on the separable kernel).  Walk step q handles output
     // row orow0 + dir q; walk row s of the ring is input row wrow0 + dir s; the window position mm
     // (oldest first) multiplies tap row tap_row(mm).
-    const bool up = FIR2D_MFMA_ALT && (strip & 1);
+    const bool up = (strip & 1) != 0;
     const int64_t dir = up ? -1 : 1;
     const int64_t orow0 = up ? i0 + kM2Strip - 1 : i0;
     const int64_t wrow0 = up ? i0 + kM2Strip - 1 + D : i0 - U;
@@ -170,16 +151,8 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
     auto load_row = [&](int64_t rho, int slot) __attribute__((always_inline)) {
         const bool in = rho >= 0 && rho < H;
         const __amdgpu_buffer_rsrc_t rs = m2_rsrc(xf + (in ? rho : 0) * W, in ? wb : 0u);
-#if FIR2D_MFMA_COPYONLY >= 3  // twin with lane-contiguous loads
-        ring[slot] = __builtin_bit_cast(m2_u4, __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)j0 + 16u * lane, 0, 0));
-#else
         ring[slot] = __builtin_bit_cast(m2_u4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0));
-#endif
-#if FIR2D_MFMA_COPYONLY == 2 || FIR2D_MFMA_COPYONLY == 4
-        edge[slot] = 0u;
-#else
         edge[slot] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, eoff, 0, 0);
-#endif
     };
     // signed bytes and the halo dword [x(32n-2), x(32n-1), x(32n+32), x(32n+33)] of block n
     const int srcl = 4 * (32 + ((n + 31) & 31)), srcr = 4 * ((n + 1) & 31);
@@ -234,29 +207,23 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
         }
     };
     // lane n: bytes 32n + 0..15, lane n + 32: bytes 32n + 16..31 (two v_permlane32_swap), then
-    // (FIR2D_MFMA_LDS_STORE) through 1 KiB of wave-private LDS so that lane L stores bytes
+    // through 1 KiB of wave-private LDS so that lane L stores bytes
     // 16L..16L+15: each 16-lane pass of the store then writes 256 contiguous bytes, whole lines,
     // instead of every other 16 bytes of 512.  One non-temporal store, dropped when the row is
     // outside the strip or the frame.
-#if FIR2D_MFMA_LDS_STORE
     __shared__ __attribute__((aligned(16))) uint8_t obuf[kBlock / kWave][kM2Tile];
     uint8_t* ob = obuf[threadIdx.x >> 6];
     const uint32_t soff = (uint32_t)j0 + 16u * lane;
-#else
-    const uint32_t soff = voff;
-#endif
     auto store_row = [&](const uint32_t* g, int64_t i, bool ok) __attribute__((always_inline)) {
         const auto s02 = __builtin_amdgcn_permlane32_swap(g[0], g[2], false, false);
         const auto s13 = __builtin_amdgcn_permlane32_swap(g[1], g[3], false, false);
         m2_u4 v = m2_u4{s02[0], s02[1], s13[0], s13[1]};
-#if FIR2D_MFMA_LDS_STORE
         *reinterpret_cast<m2_u4*>(ob + 32 * n + 16 * hf) = v;
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
         v = *reinterpret_cast<const m2_u4*>(ob + 16 * lane);
         __builtin_amdgcn_wave_barrier();  // the read is done before the next row's write
         asm volatile("" ::: "memory");
-#endif
         const bool in = ok && i < H;
         const __amdgpu_buffer_rsrc_t rs = m2_rsrc(yf + (in ? i : 0) * W, in ? wb : 0u);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(m2_i32x4, v), rs, soff, 0, kM2AuxNt);
@@ -281,14 +248,6 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
             prep_row((k + R - 1) % kM2Ring);                              // walk row q + R - 1 has arrived
             load_row(wrow0 + dir * (q + R - 1 + PD), (k + R - 1 + PD) % kM2Ring);  // slot of walk row q - 1
 
-#if FIR2D_MFMA_COPYONLY  // memory-only twin (A/B builds): the same loads and stores, no arithmetic
-            {
-                const m2_u4 rv = ring[(k + U) % kM2Ring];
-                const uint32_t g[4] = {rv.x, rv.y, rv.z, rv.w};
-                store_row(g, orow0 + dir * (q - 1), q > 0);
-                continue;
-            }
-#endif
             m2_i32x16& a = acc[kk & 1];
             m2_i32x16& ah = acch[kk & 1];
             const m2_i32x16& pa = acc[(kk + 1) & 1];
@@ -331,16 +290,12 @@ __global__ __launch_bounds__(kBlock, NP == 1 ? FIR2D_MFMA_MINW : 2) void fir2d_m
 
 // Output rows per wave: 32 for one tap plane (alternating walks, below); otherwise the strips are
 // sized so that the launch is ONE round of resident waves (occupancy x CUs x 4), which removes the
-// partial last round of fixed strips; FIR2D_MFMA_ROWS=n forces n (rounded up to the unrolled
-// turn; A/B).
+// partial last round of fixed strips.
 template <int R, int NP, bool FAST, bool ACC32>
 static int m2_rows_per_strip(int64_t frames, int64_t ncol, int64_t H, hipStream_t s) {
     constexpr int UN = (M2Geom<R>::RING & 1) ? 2 * M2Geom<R>::RING : M2Geom<R>::RING;
     int64_t rows;
-    const char* env = getenv("FIR2D_MFMA_ROWS");
-    if (env && atoi(env) > 0) {
-        rows = atoi(env);
-    } else if (NP == 1 && FIR2D_MFMA_ALT) {
+    if (NP == 1) {
         // one tap plane with alternating walks: short strips keep neighbours in step (their
         // shared rows then come from L2); 32 rows: the general 5x5 85.4 -> 81.2 us per 4
         // frames, while two planes stay faster with one round (108 vs 119;

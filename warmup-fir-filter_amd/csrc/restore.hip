@@ -26,14 +26,9 @@ constexpr int kRestoreBlocks = 1024;
 // waves keep more of the read stream in flight than few long ones.  Same-process A/B over
 // 2^28 doubles (profiles/r02/ab_restore_metrics.txt): 16 loads 372-397 us, 8: 366, 4: 361-376,
 // 2: 354-363, 1: 389; the 2 GiB read-only ceiling is 301 us at 1-2 loads per lane
-// (profiles/r02/read_ceiling_2gib.txt).  FIR_RESTORE_*: A/B builds only.
-#ifndef FIR_RESTORE_LOADS
-#define FIR_RESTORE_LOADS 2
-#endif
-#ifndef FIR_RESTORE_NTSTORE
-#define FIR_RESTORE_NTSTORE 0
-#endif
-constexpr int kRestoreLoads = FIR_RESTORE_LOADS;
+// (profiles/r02/read_ceiling_2gib.txt).  The result bytes are stored plainly (non-temporal
+// stores: 394 -> 415 us, profiles/r01/nts_ab_benches.txt).
+constexpr int kRestoreLoads = 2;
 static_assert(kRestoreLoads <= 4 || kRestoreLoads % 8 == 0, "restore loads per lane");
 constexpr int kRestorePerWave = 2 * kWave * kRestoreLoads;
 
@@ -84,7 +79,7 @@ __global__ __launch_bounds__(kBlock) void restore_map_kernel(const double* __res
             for (int i = 0; i < K / 8; ++i) {  // plain stores: non-temporal ones measured 394 -> 415 us
                 u32x4* dst = reinterpret_cast<u32x4*>(out + base) + i * kWave + lane;
                 const u32x4 val = reinterpret_cast<const u32x4*>(wb)[i * kWave + lane];
-                if constexpr (FIR_RESTORE_NTSTORE) __builtin_nontemporal_store(val, dst); else *dst = val;
+                *dst = val;
             }
         } else if constexpr (K == 4) {
             typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
