@@ -89,7 +89,7 @@ GATE_MODE = os.environ.get("FIR_GATE_MODE", "serial")
 KERNELS = {"fir1d_i16": "fir1d_reg_kernel", "cplx_i16": "fir1d_reg_kernel", "fir2d_u8": "fir2d_pk16_strip_kernel",
            "fir1d_u8": "fir1d_reg_kernel", "ideal_u8": "fir1d_ideal_kernel", "bank_u8": "fir1d_reg_kernel",
            "restore_u8": "restore_map_kernel",
-           "pipeline_fixed3": "fir1d_reg_kernel (4-filter bank, one launch per image, 7 launches in one hipGraph)",
+           "pipeline_fixed3": "fir1d_reg_batch_kernel (4-filter bank, the 7 images in one launch)",
            "metrics_u8": "metrics_leaf_kernel (+ metrics_prep: unset markers; chain and final in the launch)"}
 NUMPY_ONLY = ("restore_u8", "metrics_u8", "pipeline_fixed3")  # no C oracle leg: the NumPy restatement is the CPU baseline
 ROOF_RAMP, ROOF_LAUNCHES = 100, 200  # roofline loop: untimed ramp, then timed launches of the dominant kernel
@@ -239,8 +239,8 @@ class Workload:
         elif name == "pipeline_fixed3":
             # configs[0]: the fixed 3-tap stage of pipeline_fir_1d.py on the 7 golden images (the
             # reference's decoded u8 inputs, tests/golden/images_u8.npz) x the 4 filters of
-            # h_coeff_3tap_map: one fused 4-filter launch per image, the 7 launches captured once
-            # into a hipGraph (torch.cuda.CUDAGraph) and replayed as one step
+            # h_coeff_3tap_map: the 7 images in ONE fused 4-filter launch (fir1d_fixed_images_multi_dev)
+            # per step
             with np.load(ROOT / "tests" / "golden" / "images_u8.npz") as d:
                 self.images = [(k, np.ascontiguousarray(d[k])) for k in sorted(d.files)]
             self.x_host = self.images[0][1]
@@ -268,11 +268,13 @@ class Workload:
                            "parallelism": "single GPU (replicas when N > 1)"}
         else:
             raise SystemExit(f"unknown workload {name}")
-        self.graph = None
+        self.plan = None
         if name == "pipeline_fixed3":
             self.xs = [torch.from_numpy(a).to(dev) for _, a in self.images]
-            self.ys = [torch.empty((len(BANK3),) + a.shape, dtype=torch.uint8, device=dev) for _, a in self.images]
-            self.x, self.y = self.xs[0], self.ys[0]
+            # one buffer per (image, filter) output, as the reference keeps them: each plane starts on
+            # the allocator's 512-byte boundary, so every wave stores whole 128-byte lines
+            self.ys = [[torch.empty(a.shape, dtype=torch.uint8, device=dev) for _ in BANK3] for _, a in self.images]
+            self.x, self.y = self.xs[0], self.ys[0][0]
         elif name == "fir2d_u8":  # the resident batch of frames
             self.x = torch.from_numpy(self.frames_host).to(dev)
             self.y = torch.empty(self.x.shape, dtype=torch.uint8, device=dev)
@@ -302,22 +304,14 @@ class Workload:
         """Algorithmic bytes of one step (in + out bytes per unit x units)."""
         return int(round(self.units * self.bytes_per_unit))
 
-    def _bank_images(self):
-        """One fused 4-filter launch per image, in order.  (As 7 parallel graph branches on forked
-        streams the stage took 88.3 us instead of 55.8: the small launches slowed the large one they
-        shared the CUs with; gpurun_out r05f.)"""
-        for x, y in zip(self.xs, self.ys):
-            torch_ops.fir1d_fixed_rows_multi_dev(x, BANK3, 12, 32, fir_hip.OUT_U8_SAT, out=y)
-
     def bulk(self):
         if self.name == "pipeline_fixed3":
-            if self.graph is None:  # capture the 7 launches once (warmed outside the capture)
-                self._bank_images()
-                torch.cuda.current_stream().synchronize()
-                self.graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self.graph, stream=torch.cuda.current_stream()):
-                    self._bank_images()
-            self.graph.replay()
+            # the 7 images x 4 filters in ONE launch, its arguments marshalled once (a plan).  One
+            # launch per image took 55.8 us per stage, 4.1-4.6 us for each small image; as 7
+            # parallel graph branches 88.3 us (profiles/r05/pipeline_unaligned_ab.txt)
+            if self.plan is None:
+                self.plan = torch_ops.ImagesMultiPlan(self.xs, BANK3, 12, 32, fir_hip.OUT_U8_SAT, outs=self.ys)
+            self.plan.launch()
         elif self.name == "fir2d_u8":
             torch_ops.fir2d_fixed_dev(self.x, self.hq2, 12, 32, fir_hip.OUT_U8_SAT, out=self.y)
         elif self.name == "ideal_u8":
@@ -512,17 +506,20 @@ class Workload:
         outs = json.loads((ROOT / "tests" / "golden" / "image_outputs.json").read_text())["outputs"]
         want = {(o["case_stem"], o["coeff_name"]): o["fixed_u8_sha256"] for o in outs if o["tap"] == "3tap"}
         names = list(BANK3_NAMES)
-        for (stem, _), y in zip(self.images, self.ys):
-            yh = y.cpu().numpy()
+        for (stem, _), yh in zip(self.images, self._planes_np()):
             for f, name in enumerate(names):
                 if hashlib.sha256(np.ascontiguousarray(yh[f]).tobytes()).hexdigest() != want[(stem, name)]:
                     return False
         return True
 
+    def _planes_np(self):
+        """pipeline_fixed3's outputs as one (filters, h, w) array per image."""
+        return [np.stack([p.cpu().numpy() for p in ps]) for ps in self.ys]
+
     def matches(self, ref) -> bool:
         """Full-output parity: every output, and every report metric, bit for bit."""
         if self.name == "pipeline_fixed3":
-            return all(np.array_equal(y.cpu().numpy(), r) for y, r in zip(self.ys, ref)) and self.matches_reference()
+            return all(np.array_equal(y, r) for y, r in zip(self._planes_np(), ref)) and self.matches_reference()
         got = self.y.cpu().numpy()
         if self.name != "metrics_u8":
             return bool(np.array_equal(got, ref))
@@ -704,7 +701,7 @@ def run_sub_configs(args, dev) -> tuple[dict, bool]:
                                        f"full workload ({wl.units} units), {tc:.2f} s"},
         }
         if name == "pipeline_fixed3":
-            entry["roofline"]["kernel_avg_us_is"] = "one graph replay = 7 launches (one stage)"
+            entry["roofline"]["kernel_avg_us_is"] = "one launch over the 7 images (one stage)"
             entry["stage_wall"] = pipeline_stage_wall()
         out[label] = entry
         del wl, ref

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define FIR_HIP_ABI_VERSION 4
+#define FIR_HIP_ABI_VERSION 5
 /* Tap counts: any length up to FIR_MAX_TAPS (1-D taps; 2-D tap_rows * tap_cols), like the
  * reference's Python loop (fir_1d_fixed_ref.py:83-107, fir_1d_ref.py:49-63); the bound is the
  * int taps argument and device memory (4 B per tap), not the arithmetic.  Sums are exact as the
@@ -101,6 +101,21 @@ int fir1d_fixed_rows_multi(const void* x, int in_dtype, int64_t rows, int64_t wi
 int fir1d_fixed_rows_multi_dev(const void* x_dev, int in_dtype, int64_t rows, int64_t width, int channels,
                                const int32_t* hq, int taps, int filters, int frac_bits, int acc_bits,
                                int out_stage, void* y_dev, void* stream);
+
+/* The pipeline's stage over a set of images (replaces the per-image loop of
+ * fir_1d/sim/vector/gen_fixed_output.py:88-107, which runs _run_fixed_rowwise once per image and
+ * coefficient set and keeps each output as its own array): image i is rows[i] x widths[i] x
+ * channels samples at x_devs[i]; its output for filter f (shaped like the image) at
+ * y_planes[i * filters + f], each plane its own buffer.  Results are identical to one
+ * fir1d_fixed_rows_dev call per (image, filter); every image is checked before anything launches
+ * (an error names the image).  u8 -> sat-u8 banks of one channel go out as ONE launch per 8
+ * images and 4 filters (device pointers, stream-ordered, returns after the launches).  Planes
+ * that start on 128 bytes are written in whole cache lines (16 bytes off: 18.7 vs 16.2 us for the
+ * golden images' stage, 238 vs 181 us for a 2^28-sample bank; profiles/r05/pipeline_batch_ab.txt). */
+int fir1d_fixed_images_multi_dev(int n_images, const void* const* x_devs, const int64_t* rows,
+                                 const int64_t* widths, int in_dtype, int channels, const int32_t* hq,
+                                 int taps, int filters, int frac_bits, int acc_bits, int out_stage,
+                                 void* const* y_planes, void* stream);
 
 /* Recompute the first (taps-1-taps/2)*channels and last (taps/2)*channels outputs of a
  * single-row segment of n*channels samples, reading out-of-segment samples from

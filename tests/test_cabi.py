@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.fir_abi_version() == fir_hip.ABI_VERSION == 4
+    assert lib.fir_abi_version() == fir_hip.ABI_VERSION == 5
 
 
 def test_invalid_arguments_are_rejected_without_device(lib):
@@ -55,6 +55,30 @@ def test_invalid_arguments_are_rejected_without_device(lib):
     assert rc == 1
     # empty problems are valid no-ops
     assert lib.fir1d_fixed_rows_dev(None, 0, 0, 16, 1, h, 3, 12, 32, 0, None, None) == 0
+
+
+def test_images_batch_argument_checks_without_device(lib):
+    """fir1d_fixed_images_multi_dev refuses the whole call before anything launches, naming the
+    image at fault; no images is a no-op."""
+    h = (ctypes.c_int32 * 3)(1, 2, 1)
+    i64x2 = ctypes.c_int64 * 2
+    vpx2 = ctypes.c_void_p * 2
+    xs, ys = vpx2(16, 32), vpx2(48, 64)  # never dereferenced: every call below is refused first
+    assert lib.fir1d_fixed_images_multi_dev(0, None, None, None, 0, 1, h, 3, 1, 12, 32, 0, None, None) == 0
+    assert lib.fir1d_fixed_images_multi_dev(-1, None, None, None, 0, 1, h, 3, 1, 12, 32, 0, None, None) == 1
+    assert b"images" in lib.fir_last_error()
+    assert lib.fir1d_fixed_images_multi_dev(2, None, i64x2(4, 4), i64x2(64, 64), 0, 1, h, 3, 1, 12, 32, 0, ys,
+                                            None) == 1
+    assert b"NULL" in lib.fir_last_error()
+    assert lib.fir1d_fixed_images_multi_dev(2, xs, i64x2(4, -4), i64x2(64, 64), 0, 1, h, 3, 1, 12, 32, 0, ys,
+                                            None) == 1
+    assert b"image 1" in lib.fir_last_error()
+    assert lib.fir1d_fixed_images_multi_dev(2, xs, i64x2(4, 4), i64x2(64, 64), 0, 1, h, 3, 0, 12, 32, 0, ys,
+                                            None) == 1
+    assert b"filters" in lib.fir_last_error()
+    assert lib.fir1d_fixed_images_multi_dev(2, xs, i64x2(4, 4), i64x2(64, 64), 5, 1, h, 3, 1, 12, 32, 0, ys,
+                                            None) == 1
+    assert b"image 0" in lib.fir_last_error() and b"in_dtype" in lib.fir_last_error()
 
 
 def test_errors_surface_as_firhiperror():

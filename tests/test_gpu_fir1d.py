@@ -275,6 +275,36 @@ def test_u8_rows_vs_oracle(width, L):
         assert np.array_equal(got, fo.fir1d_rows(x, hq, 12, 32, stage)), (width, L, stage)
 
 
+@pytest.mark.parametrize("L", [2, 3, 4, 5, 6, 7, 8, 9])
+def test_ragged_row_seams_vs_oracle(L):
+    """Rows that straddle 16-byte vectors, u8 stage, one channel: computed as one signal with the
+    L - 1 outputs around every row seam rewritten from their own row (kRagged, fir1d_reg.h).
+    Widths from the narrowest the register kernel takes (vector + L - 1) up, seams at every
+    vector offset, saturating pixels on both sides of each seam, banks of 1-4 filters mixing the
+    packed-16 and v_dot2 forms, and int16 samples (8-sample vectors)."""
+    rng = np.random.default_rng(L)
+    for width in (16 + L - 1, 16 + L, 33 + L, 4499):
+        rows = 48 if width < 100 else 9
+        x = rng.integers(0, 256, (rows, width), dtype=np.uint8)
+        x[:, :L] = 255
+        x[:, -L:] = 255
+        x[::3, :L] = 0
+        for F in (1, 2, 4):
+            hq = rng.integers(-3000, 3000, (F, L))
+            hq[0] = np.abs(hq[0])
+            if F > 1:
+                hq[1] = rng.integers(0, 4, L) << 10  # packed-16 form
+                hq[1, 0] |= 1 << 10
+            ys = fir_hip.fir1d_fixed_rows_multi(x, hq, 12, 32, fir_hip.OUT_U8_SAT)
+            for f in range(F):
+                want = fo.fir1d_rows(x, hq[f], 12, 32, fir_hip.OUT_U8_SAT)
+                assert np.array_equal(ys[f], want), (width, F, f)
+        x16 = rng.integers(-32768, 32768, (rows, width), dtype=np.int16)
+        hq = rng.integers(-3000, 3000, L)
+        assert np.array_equal(fir_hip.fir1d_fixed_rows(x16, hq, 12, 32, fir_hip.OUT_U8_SAT),
+                              fo.fir1d_rows(x16, hq, 12, 32, fir_hip.OUT_U8_SAT)), width
+
+
 @pytest.mark.parametrize("width", [8, 17, 1280, 4499])
 def test_i16_rows_and_complex_rows(width):
     rng = np.random.default_rng(width)

@@ -83,6 +83,7 @@ for s in $STEPS; do
                  run "bankab_$v" 200 python tools/lib_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so \
                      abrun/libfir_hip_bank_$v.so 10 bank; fatal $? || exit
              done ;;
+        probe) run probe 200 python tools/pipeline_probe.py; fatal $? ;;
         libab_*) wl=${s#libab_}
              run "libab_$wl" 200 python tools/lib_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so ${AB_LIB} 10 "$wl"; fatal $? ;;
         ltab_*) kind=${s#ltab_}

@@ -6,6 +6,7 @@ bankw<W> = the same bank over rows of W samples (bankw4499: the reference's wide
 not a whole number of 16-byte vectors).
 Usage: python tools/lib_ab.py <lib A> <lib B> [rounds] [i16|u8|bank|bankw<W>]"""
 import ctypes
+import os
 import sys
 
 import numpy as np
@@ -48,7 +49,8 @@ def main():
     for i in range(len(libs)):
         run(i, 50)
     torch.cuda.synchronize()
-    assert torch.equal(ys[0], ys[1])
+    if not os.environ.get("LIB_AB_NOCHECK"):  # timing-only variants (wrong results by design) set it
+        assert torch.equal(ys[0], ys[1])
     t = [[] for _ in libs]
     for _ in range(rounds):
         for i in range(len(libs)):

@@ -543,6 +543,23 @@ int fir1d_fixed_rows_multi_dev(const void* x_dev, int in_dtype, int64_t rows, in
     }
 }
 
+int fir1d_fixed_images_multi_dev(int n_images, const void* const* x_devs, const int64_t* rows, const int64_t* widths,
+                                 int in_dtype, int channels, const int32_t* hq, int taps, int filters, int frac_bits,
+                                 int acc_bits, int out_stage, void* const* y_planes, void* stream) {
+    try {
+        std::string err;
+        int64_t rw = 0, n = 0;
+        for (int i = 0; i < n_images && rows && widths; ++i)
+            if (!mul_ok(rows[i], widths[i], &rw) || !mul_ok(rw, channels < 1 ? 1 : channels, &n))
+                return fail(FIR_EINVAL, "image " + std::to_string(i) + ": invalid rows/width/channels");
+        int rc = fir::launch_fir1d_images_multi(n_images, x_devs, rows, widths, in_dtype, channels, hq, taps, filters,
+                                                frac_bits, acc_bits, out_stage, y_planes, (hipStream_t)stream, &err);
+        return rc ? fail(rc, err) : FIR_OK;
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
 int fir1d_fixed_edges_dev(const void* x_dev, int in_dtype, int64_t n, int channels, const int32_t* hq, int taps,
                           int frac_bits, int acc_bits, int out_stage, const void* halo_left_dev,
                           const void* halo_right_dev, void* y_dev, void* stream) {

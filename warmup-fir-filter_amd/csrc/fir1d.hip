@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <string>
 #include <type_traits>
+#include <vector>
 
 #include "fir1d_reg_launch.h"
 #include "fir_common.h"
@@ -324,6 +325,69 @@ int launch_fir1d_rows_multi(const void* x, int in_dtype, int64_t rows, int64_t w
             if (rc) return rc;
         }
         f0 += nf;
+    }
+    return FIR_OK;
+}
+
+template <int F>
+static hipError_t launch_batch_u8(int L, int n, const RegImage* im, const int32_t* hq, int frac, int acc_bits,
+                                  hipStream_t s) {
+    return launch_reg_batch_taps<uint8_t, FIR_OUT_U8_SAT, 1, F>(L, n, im, hq, frac, acc_bits, s);
+}
+
+int launch_fir1d_images_multi(int n, const void* const* xs, const int64_t* rows, const int64_t* widths, int in_dtype,
+                              int ch, const int32_t* hq, int L, int F, int frac, int acc_bits, int stage,
+                              void* const* planes, hipStream_t stream, std::string* err) {
+    if (n < 0) return *err = "images must be >= 0", FIR_EINVAL;
+    if (n == 0) return FIR_OK;
+    if (!xs || !planes || !rows || !widths) return *err = "image arrays must not be NULL", FIR_EINVAL;
+    if (F < 1) return *err = "filters must be >= 1", FIR_EINVAL;
+    for (int i = 0; i < n; ++i) {  // the whole call is refused before anything runs
+        int rc = check_common(in_dtype, rows[i], widths[i], ch, hq, L, frac, acc_bits, stage, err);
+        if (rc) return *err = "image " + std::to_string(i) + ": " + *err, rc;
+        bool null = !xs[i];
+        for (int f = 0; f < F; ++f) null |= !planes[(size_t)i * F + f];
+        if (rows[i] * widths[i] != 0 && null)
+            return *err = "image " + std::to_string(i) + ": x and its output planes must not be NULL", FIR_EINVAL;
+    }
+    std::vector<int> batch;  // images on the batch kernel
+    for (int i = 0; i < n; ++i) {
+        const int64_t total = rows[i] * widths[i] * ch;
+        if (total == 0) continue;
+        void* const* yp = planes + (size_t)i * F;
+        if (in_dtype == FIR_IN_U8 && ch == 1 && stage == FIR_OUT_U8_SAT &&
+            reg_path_ok(xs[i], yp[0], in_dtype, rows[i], widths[i], total, ch, hq, F * L, L, frac, acc_bits)) {
+            batch.push_back(i);
+            continue;
+        }
+        for (int f = 0; f < F; ++f) {
+            int rc = launch_fir1d_rows(xs[i], in_dtype, rows[i], widths[i], ch, hq + (size_t)f * L, L, frac, acc_bits,
+                                       stage, yp[f], stream, err);
+            if (rc) return rc;
+        }
+    }
+    for (size_t i0 = 0; i0 < batch.size(); i0 += kRegBatch) {
+        const int nb = (int)std::min<size_t>(kRegBatch, batch.size() - i0);
+        for (int f0 = 0; f0 < F; f0 += 4) {
+            const int nf = F - f0 < 4 ? F - f0 : 4;
+            RegImage im[kRegBatch];
+            for (int j = 0; j < nb; ++j) {
+                const int i = batch[i0 + j];
+                im[j].x = xs[i];
+                im[j].rows = rows[i];
+                im[j].rowlen = widths[i];
+                for (int f = 0; f < 4; ++f) im[j].y[f] = f < nf ? planes[(size_t)i * F + f0 + f] : nullptr;
+            }
+            const int32_t* hf = hq + (size_t)f0 * L;
+            hipError_t e;
+            switch (nf) {
+                case 1: e = launch_batch_u8<1>(L, nb, im, hf, frac, acc_bits, stream); break;
+                case 2: e = launch_batch_u8<2>(L, nb, im, hf, frac, acc_bits, stream); break;
+                case 3: e = launch_batch_u8<3>(L, nb, im, hf, frac, acc_bits, stream); break;
+                default: e = launch_batch_u8<4>(L, nb, im, hf, frac, acc_bits, stream); break;
+            }
+            if (e != hipSuccess) return *err = std::string("fir1d batch launch failed: ") + hipGetErrorString(e), FIR_EHIP;
+        }
     }
     return FIR_OK;
 }

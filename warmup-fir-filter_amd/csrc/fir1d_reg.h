@@ -15,6 +15,7 @@
 // (floor(a/2^f) + bit f-1), saturate (u8) or keep (int32; stored through LDS [kCoal]).
 #pragma once
 
+#include "fir1d_reg_launch.h"
 #include "fir_common.h"
 
 namespace fir {
@@ -47,6 +48,18 @@ enum RegFlags : int {
                         // fetches both edge dwords with ONE wave-wide dword load (lane 0: the
                         // dword before the tile, lane 63: the dword after it) instead of two
                         // lane-masked 16-byte loads in branches
+    // Rows that are not a whole number of vectors (the reference's 4499-wide image), u8 stage, one
+    // channel: every vector is computed as if the rows were one signal (no masks, the interior
+    // forms), then the lane whose vector holds a row seam rewrites the HLE + HRE outputs around it
+    // from the samples of their own row, in registers before the store (ragged_fix_*).  The masked
+    // pair it replaces ran two generic windows for every seam vector: 27.0 vs 13.5 us for the
+    // 4499 x 2999 bank (tools/pipeline_probe.py).
+    kRagged = 8192,
+    // Rows that straddle vectors, other stages / channel counts: seam vectors take the masked
+    // generic pair (fir_vector_masked).  Without kMasked or kRagged the launcher guarantees
+    // RowGeom::aligned, and the masked pair is not compiled in (it held 45 of the fused u8 bank's
+    // 90 VGPRs).
+    kMasked = 16384,
 };
 
 // One non-temporal 16-byte row-store of the coalesced path, as inline asm: the same
@@ -449,12 +462,114 @@ __device__ __forceinline__ void fir_vector_masked(const int32_t* w, int a, int b
     for (int j = 0; j < VEC; ++j) q[j] = j < b ? q1[j] : q2[j];
 }
 
-// y holds F output planes of g.total samples each (plane f at y + f * g.total).
-template <typename InT, int STAGE, int L, int CH, int U, int FLAGS, int F = 1>
-__global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict__ x,
-                                                           typename OutTraits<STAGE>::T* __restrict__ y,
-                                                           RowGeom g, TapsN<L, F> taps, int shl, int frac,
-                                                           int64_t ntiles) {
+// kRagged: the outputs p = b - HRE .. b + HLE - 1 around a row seam at vector offset b (rows start
+// at b) are recomputed from the samples of their own row and put into the vector's output
+// registers BEFORE its store, so every line is still written once and whole (a byte store after
+// the 16-byte store turned those lines into partial writes: 14.5 vs 11.4 us for the 4499- vs
+// 4496-wide image, tools/pipeline_probe.py).  s[k] = sample b - NP + k; output i (p = b - HRE + i)
+// lies in the row after the seam iff i >= HRE, sample k iff k >= NP; both tests are static.
+// ragged_samples takes the samples from the lane's own window w (w[0] = sample -HLE) by selects
+// over its NS entries: every sample an output inside the vector needs lies in it (the rest read 0
+// and feed only outputs outside the vector, which are never inserted).
+template <int L, int NS>
+__device__ __forceinline__ void ragged_samples(const int32_t (&w)[NS], int b, int32_t (&sv)[2 * (L - 1) + 1]) {
+    constexpr int C = L / 2, HLE = L - 1 - C, NP = L - 1;
+#pragma unroll
+    for (int k = 0; k < 2 * NP; ++k) {
+        const int j = b - NP + k + HLE;  // window index
+        int32_t v = 0;
+#pragma unroll
+        for (int q = 0; q < NS; ++q) v = j == q ? w[q] : v;
+        sv[k] = v;
+    }
+}
+
+// The same for u8 samples straight from the window dwords Wd[NW] (sample o of the vector is
+// byte 4 * NDL + o): the 2 * NP bytes span at most ND dwords of [PADL zero dwords, Wd..., zeros],
+// picked by selects on the dword index, then byte-aligned: about 30 VALU ops for L = 3 where
+// ragged_samples spends 144.  The pad keeps the first byte index >= 0 for every seam offset
+// b >= 1 - HLE.
+template <int L, int NW, int NDL>
+__device__ __forceinline__ void ragged_samples_u8(const uint32_t (&Wd)[NW], int b, int32_t (&sv)[2 * (L - 1) + 1]) {
+    constexpr int NP = L - 1, ND = (2 * NP + 3) / 4 + 1, HLE = L - 1 - L / 2, PADL = (HLE + NP + 3) / 4;
+    const int B0 = b - NP + 4 * (NDL + PADL);
+    const int d0 = B0 >> 2;
+    uint32_t dw[ND];
+#pragma unroll
+    for (int e = 0; e < ND; ++e) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) v = d0 + e == PADL + q ? Wd[q] : v;
+        dw[e] = v;
+    }
+    const uint32_t sh = 8u * (uint32_t)(B0 & 3);
+#pragma unroll
+    for (int k = 0; k < 2 * NP; ++k) {
+        const uint32_t lo = dw[k / 4], hi = dw[k / 4 + 1];
+        const uint32_t four = (uint32_t)(((uint64_t)hi << 32 | lo) >> sh);  // bytes k/4*4 .. +3
+        sv[k] = (int32_t)((four >> (8 * (k % 4))) & 0xFFu);
+    }
+}
+
+// Tap kk of filter f.  FROMPK (the v_dot2 kernels, int16 taps): unpacked from the pairs
+// pk[f][p] = h[L-1-2p] | h[L-2-2p] << 16, which those kernels hold anyway, instead of keeping
+// h[][] live as F * L more SGPRs across the tile (the batch kernel spilled SGPRs into VGPR lanes).
+template <int L, int F, bool FROMPK>
+__device__ __forceinline__ int32_t ragged_tap(const TapsN<L, F>& taps, int f, int kk) {
+    if constexpr (FROMPK) {
+        const uint32_t pr = taps.pk[f][(L - 1 - kk) / 2];
+        return (L - 1 - kk) % 2 == 0 ? (int32_t)(int16_t)(pr & 0xFFFFu) : (int32_t)pr >> 16;
+    } else {
+        return taps.h[f][kk];
+    }
+}
+
+// Seam output i of filter f, rounded (before the stage).
+template <int L, int F, bool ACC32, bool FROMPK>
+__device__ __forceinline__ int32_t ragged_value(const int32_t (&sv)[2 * (L - 1) + 1], const TapsN<L, F>& taps, int f,
+                                                int i, int shl, int frac) {
+    constexpr int C = L / 2, HLE = L - 1 - C, HRE = C, NP = L - 1;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int t = -HLE; t <= HRE; ++t) {
+        const int k = i + t + HLE;
+        if ((i >= HRE) == (k >= NP)) acc += (uint32_t)__mul24(ragged_tap<L, F, FROMPK>(taps, f, C - t), sv[k]);
+    }
+    return round_acc<ACC32>(acc, shl, frac);
+}
+
+// Put one filter's seam outputs pv[i] (rounded, before the stage) into the packed output bytes
+// o[VEC / 4] at vector offsets p0 + i.  The byte masks m[i][d] are plain VGPR values computed
+// once per vector (as lane-mask compares the compiler hoisted them out of the filter loop into
+// SGPR pairs and spilled SGPRs).
+template <int NP, int VEC>
+__device__ __forceinline__ void ragged_masks(int p0, uint32_t (&m)[NP][VEC / 4]) {
+#pragma unroll
+    for (int i = 0; i < NP; ++i)
+#pragma unroll
+        for (int d = 0; d < VEC / 4; ++d) {
+            const uint32_t sd = (uint32_t)(p0 + i - 4 * d);  // byte of dword d, when < 4
+            m[i][d] = sd < 4u ? 0xFFu << (8u * sd) : 0u;
+        }
+}
+
+template <int NP, int VEC>
+__device__ __forceinline__ void ragged_put_bytes(const int32_t* pv, const uint32_t (&m)[NP][VEC / 4],
+                                                 uint32_t (&o)[VEC / 4]) {
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const uint32_t v = stage_out32<FIR_OUT_U8_SAT>(pv[i]) * 0x01010101u;  // the byte in every position
+#pragma unroll
+        for (int d = 0; d < VEC / 4; ++d) o[d] = (o[d] & ~m[i][d]) | (v & m[i][d]);
+    }
+}
+
+// The tiles tile, tile + stride, ... below ntiles of one buffer (wave-uniform tile); output
+// plane f (g.total samples) at yf[f].
+template <typename InT, int STAGE, int L, int CH, int U, int FLAGS, int F>
+__device__ __forceinline__ void fir1d_reg_body(const InT* __restrict__ x, typename OutTraits<STAGE>::T* const (&yf)[F],
+                                               const RowGeom& g, const TapsN<L, F>& taps, int shl, int frac,
+                                               int64_t ntiles, int64_t tile, int64_t stride) {
     using IT = InTraits<InT>;
     constexpr int EPD = IT::kPerDword;
     constexpr int VEC = 4 * EPD;
@@ -471,7 +586,8 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
     constexpr bool U8PK = U8DOT2 && (FLAGS & kU8Pk16) && STAGE == FIR_OUT_U8_SAT;
     constexpr bool HALO = (FLAGS & kHalo) != 0;
     constexpr bool COAL = (FLAGS & kCoal) && STAGE == FIR_OUT_I32;
-    constexpr int WPB = kBlock / kWave;
+    constexpr bool RAGGED = (FLAGS & kRagged) && STAGE == FIR_OUT_U8_SAT && CH == 1;
+    constexpr bool MASKED = (FLAGS & kMasked) != 0;
     uint32_t bias = 0;
     int32_t sat_hi = 0;
     if constexpr (U8DOT2) {
@@ -482,16 +598,14 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t total = g.total;
     const int64_t nvec = total / VEC;
-    const int64_t stride = PERSIST ? (int64_t)gridDim.x * WPB : ntiles;
-    const int64_t bpos = (FLAGS & kXcd) ? xcd_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
-    int64_t tile = bpos * WPB + (threadIdx.x >> 6);  // wave-uniform
 
     uint32_t own[U][4];
     if (tile < ntiles) {
 #pragma unroll
         for (int u = 0; u < U; ++u) load_vec<InT, NTL>(x, tile * (kWave * U) + u * kWave + lane, nvec, total, own[u]);
     }
-    for (; tile < ntiles; tile += stride) {
+    // one tile per wave unless PERSIST: no loop, so nothing stays live past the tile's stores
+    for (; tile < ntiles; tile = PERSIST ? tile + stride : ntiles) {
         const int64_t vb = tile * (kWave * U);
         uint32_t hv[4] = {0, 0, 0, 0};
         constexpr bool EDW = (FLAGS & kEdgeDword) && NDL <= 1 && NDR <= 1;
@@ -553,7 +667,7 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
                     col0 = g0;
                 }
                 bool interior = col0 >= HLE && col0 + VEC + HRE <= rowlen;
-                if (g.aligned) {
+                if ((!MASKED && !RAGGED) || g.aligned) {
                     // Every vector lies inside one row, so only its halo can leave the row: zero
                     // the halo dwords (all of their samples are in the neighbouring row) and take
                     // the unmasked path.  One row: the loads already zero-fill beyond both ends.
@@ -566,6 +680,8 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
                     }
                     interior = true;
                 }
+                const bool seam = RAGGED && !interior;  // this vector holds a row seam's outputs
+                if constexpr (RAGGED) interior = true;  // computed as one signal, seams patched below
                 constexpr int64_t kFar = 1 << 24;  // beyond any window offset
                 const int ma = (int)min(col0, kFar), mb = (int)min(rowlen - col0, kFar), mr = (int)min(rowlen, kFar);
                 // samples of the window as int32 (first window sample = -HLE)
@@ -577,6 +693,29 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
                 }
                 uint32_t Pp[VEC + L - 2];  // U8PK: byte pairs of the window, shared by the filters
                 if constexpr (U8PK) BytePairs<NW, 4 * NDL - HLE, VEC + L - 2>::run(Wd, Pp);
+                // RAGGED: in a wave with a seam (a wave-uniform test, so no exec masks to hold), every
+                // lane computes its seam outputs pv once; lanes without a seam put them nowhere
+                constexpr int NPR = RAGGED && L > 1 ? L - 1 : 1;
+                int32_t pv[F][NPR];
+                uint32_t pm[NPR][VEC / 4];
+                bool anyseam = false;
+                if constexpr (RAGGED && L > 1) {
+                    anyseam = __builtin_amdgcn_ballot_w64(seam) != 0;
+                    if (anyseam) {
+                        const int sb = col0 < HLE ? -(int)col0 : (int)(rowlen - col0);  // seam's vector offset
+                        int32_t sv[2 * (L - 1) + 1];
+                        if constexpr (sizeof(InT) == 1)
+                            ragged_samples_u8<L, NW, NDL>(Wd, sb, sv);
+                        else
+                            ragged_samples<L>(w, sb, sv);
+#pragma unroll
+                        for (int f = 0; f < F; ++f)
+#pragma unroll
+                            for (int i = 0; i < L - 1; ++i)
+                                pv[f][i] = ragged_value<L, F, ACC32, U8DOT2 || DOT2>(sv, taps, f, i, shl, frac);
+                        ragged_masks<NPR, VEC>(seam ? sb - HRE : -2 * VEC, pm);
+                    }
+                }
 #pragma unroll
                 for (int f = 0; f < F; ++f) {
                     if constexpr (U8PK) {
@@ -585,7 +724,10 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
                             uint32_t o[VEC / 4];
                             u8_pk16_vec<L, VEC, FLAGS>(Pp, taps.hb[f], taps.pkbias[f], taps.pkshift[f], taps.pkmax,
                                                        md == 2, o);
-                            store_u8_dwords<VEC, NTS>(reinterpret_cast<uint8_t*>(y + f * total), g0, total, v < nvec, o);
+                            if constexpr (RAGGED && L > 1) {
+                                if (anyseam) ragged_put_bytes<NPR, VEC>(pv[f], pm, o);
+                            }
+                            store_u8_dwords<VEC, NTS>(reinterpret_cast<uint8_t*>(yf[f]), g0, total, v < nvec, o);
                             continue;
                         }
                     }
@@ -608,6 +750,20 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
                             for (int j = 0; j < VEC; ++j) q[j] = stage_out32<STAGE>(q[j]);
                         }
                     }
+                    if constexpr (RAGGED && L > 1) {  // u8 stage: pack, put the seam bytes, store
+                        uint32_t o[VEC / 4];
+#pragma unroll
+                        for (int d = 0; d < VEC / 4; ++d) {
+                            uint32_t t = 0;
+#pragma unroll
+                            for (int e = 0; e < 4; ++e)
+                                t |= (uint32_t)(U8DOT2 ? q[4 * d + e] : stage_out32<STAGE>(q[4 * d + e])) << (8 * e);
+                            o[d] = t;
+                        }
+                        if (anyseam) ragged_put_bytes<NPR, VEC>(pv[f], pm, o);
+                        store_u8_dwords<VEC, NTS>(reinterpret_cast<uint8_t*>(yf[f]), g0, total, v < nvec, o);
+                        continue;
+                    }
                     if constexpr (COAL) {
                         if (vb + (u + 1) * kWave <= nvec) {  // wave-uniform: the whole chunk is full
                             __shared__ u32x4 sbuf[kBlock * VEC / 4];
@@ -618,7 +774,7 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
                                                                  (uint32_t)q[4 * i + 2], (uint32_t)q[4 * i + 3]};
                             __builtin_amdgcn_wave_barrier();  // one wave's LDS ops complete in order
                             asm volatile("" ::: "memory");
-                            u32x4* yw = reinterpret_cast<u32x4*>(y + f * total + (vb + u * kWave) * VEC);
+                            u32x4* yw = reinterpret_cast<u32x4*>(yf[f] + (vb + u * kWave) * VEC);
 #pragma unroll
                             for (int i = 0; i < VEC / 4; ++i) {
                                 if constexpr (NTS)
@@ -630,7 +786,7 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
                             continue;
                         }
                     }
-                    store_vec<STAGE, VEC, NTS, U8DOT2>(y + f * total, g0, total, v < nvec, q);
+                    store_vec<STAGE, VEC, NTS, U8DOT2>(yf[f], g0, total, v < nvec, q);
                 }
             }
         }
@@ -641,6 +797,50 @@ __global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict
                 for (int i = 0; i < 4; ++i) own[u][i] = nxt[u][i];
         }
     }
+}
+
+template <typename InT, int STAGE, int L, int CH, int U, int FLAGS, int F = 1>
+__global__ __launch_bounds__(kBlock) void fir1d_reg_kernel(const InT* __restrict__ x,
+                                                           typename OutTraits<STAGE>::T* __restrict__ y,
+                                                           RowGeom g, TapsN<L, F> taps, int shl, int frac,
+                                                           int64_t ntiles) {
+    constexpr int WPB = kBlock / kWave;
+    const int64_t stride = (FLAGS & kPersist) ? (int64_t)gridDim.x * WPB : ntiles;
+    const int64_t bpos = (FLAGS & kXcd) ? xcd_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    typename OutTraits<STAGE>::T* yf[F];  // plane f at y + f * total
+#pragma unroll
+    for (int f = 0; f < F; ++f) yf[f] = y + f * g.total;
+    fir1d_reg_body<InT, STAGE, L, CH, U, FLAGS, F>(x, yf, g, taps, shl, frac, ntiles, bpos * WPB + (threadIdx.x >> 6),
+                                                   stride);
+}
+
+// Several images (buffers of rows) in ONE launch, the same F filters over each: the wave tiles
+// of image i are tiles tile0[i] .. tile0[i+1] - 1 of the grid, its output planes anywhere
+// (y[i][f]).  The pipeline's 7 golden images took 4.1-4.6 us per launch even at 64 x 64 (a
+// launch's load -> store latency chain, not bytes), 40-54 us for the 7 (tools/pipeline_probe.py);
+// one launch overlaps those chains.
+struct RegBatch {
+    const void* x[kRegBatch];
+    void* y[kRegBatch][4];
+    RowGeom g[kRegBatch];
+    int64_t tile0[kRegBatch + 1];  // tile0[n] = the launch's tiles
+    int n;
+};
+
+template <typename InT, int STAGE, int L, int CH, int U, int FLAGS, int F>
+__global__ __launch_bounds__(kBlock) void fir1d_reg_batch_kernel(RegBatch b, TapsN<L, F> taps, int shl, int frac) {
+    const int64_t tile = (int64_t)blockIdx.x * (kBlock / kWave) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int i = 0;
+#pragma unroll
+    for (int k = 1; k < kRegBatch; ++k) i += k < b.n && tile >= b.tile0[k] ? 1 : 0;
+    const int64_t nt = b.tile0[i + 1] - b.tile0[i], lt = tile - b.tile0[i];
+    if (lt >= nt) return;  // the last block's spare waves
+    typename OutTraits<STAGE>::T* yf[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) yf[f] = static_cast<typename OutTraits<STAGE>::T*>(b.y[i][f]);
+    const RowGeom g = b.g[i];  // one copy, loaded once
+    fir1d_reg_body<InT, STAGE, L, CH, U, FLAGS, F>(static_cast<const InT*>(b.x[i]), yf, g, taps, shl, frac, nt, lt,
+                                                   nt);
 }
 
 // Tiles and grid for a launch of fir1d_reg_kernel<.., U, FLAGS>.

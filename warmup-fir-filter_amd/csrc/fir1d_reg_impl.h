@@ -29,11 +29,8 @@ namespace fir {
 constexpr int kRegFlags = kCoal | kNtStore | kEdgeDword;
 constexpr int kPersistBlocks = 2048;
 
-template <typename InT, int STAGE, int L, int CH, int F, int FL>
-static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
-                                   const int32_t* hq, int frac, int acc_bits, hipStream_t stream, const void* hl,
-                                   const void* hr) {
-    using OutT = typename OutTraits<STAGE>::T;
+template <typename InT>
+static RowGeom make_geom(int64_t rows, int64_t total, int64_t rowlen, const void* hl, const void* hr) {
     RowGeom g;
     g.total = total;
     g.rowlen32 = (uint32_t)(rows > 1 ? rowlen : 0);
@@ -41,13 +38,29 @@ static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t
     g.aligned = rows == 1 || rowlen % (4 * InTraits<InT>::kPerDword) == 0;
     g.halo_l = hl;
     g.halo_r = hr;
-    TapsN<L, F> t;
+    return g;
+}
+
+// The kernel's tap record; false when the packed-16 plan the flags promise does not hold.
+template <int L, int F, int FL>
+static bool make_taps(TapsN<L, F>& t, const int32_t* hq, int frac) {
     for (int f = 0; f < F; ++f)
         for (int k = 0; k < L; ++k) t.h[f][k] = hq[f * L + k];
     pack_taps(t);
     plan_u8_noclamp(t, frac);
     if constexpr ((FL & kU8Pk16) != 0)
-        if (!(plan_u8_pk16(t, frac) & kU8Pk16)) return hipErrorInvalidValue;  // caller checked
+        if (!(plan_u8_pk16(t, frac) & kU8Pk16)) return false;  // caller checked
+    return true;
+}
+
+template <typename InT, int STAGE, int L, int CH, int F, int FL>
+static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
+                                   const int32_t* hq, int frac, int acc_bits, hipStream_t stream, const void* hl,
+                                   const void* hr) {
+    using OutT = typename OutTraits<STAGE>::T;
+    const RowGeom g = make_geom<InT>(rows, total, rowlen, hl, hr);
+    TapsN<L, F> t;
+    if (!make_taps<L, F, FL>(t, hq, frac)) return hipErrorInvalidValue;
     int64_t ntiles = 0, blocks = 0;
     reg_launch_geometry<InT, kRegU<InT, F>, FL>(total, kPersistBlocks, &ntiles, &blocks);
     if constexpr (F == 1) {
@@ -59,18 +72,83 @@ static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t
     } else if (hl != nullptr || hr != nullptr) {
         return hipErrorInvalidValue;  // shards with halos are single-filter calls
     }
+    if (!g.aligned) {  // rows straddle vectors: one signal with seams patched (u8 stage), else masked
+        constexpr int FX = STAGE == FIR_OUT_U8_SAT && CH == 1 ? kRagged : kMasked;
+        hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, kRegU<InT, F>, FL | FX, F>), dim3((unsigned)blocks),
+                           dim3(kBlock), 0, stream, (const InT*)x, (OutT*)y, g, t, 32 - acc_bits, frac, ntiles);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, kRegU<InT, F>, FL, F>), dim3((unsigned)blocks), dim3(kBlock), 0,
                        stream, (const InT*)x, (OutT*)y, g, t, 32 - acc_bits, frac, ntiles);
     return hipGetLastError();
 }
 
+// One launch of up to kRegBatch images (u8 stage, one channel: rows that straddle vectors take
+// the kRagged seam patch, whole-vector rows the plain form, decided per image in the kernel).
+template <typename InT, int STAGE, int L, int CH, int F, int FL>
+static hipError_t launch_reg_batch_flags(int n, const RegImage* im, const int32_t* hq, int frac, int acc_bits,
+                                         hipStream_t stream) {
+    if constexpr (STAGE != FIR_OUT_U8_SAT || CH != 1) {
+        return hipErrorInvalidValue;
+    } else {
+        if (n < 1 || n > kRegBatch) return hipErrorInvalidValue;
+        RegBatch b{};
+        TapsN<L, F> t;
+        if (!make_taps<L, F, FL>(t, hq, frac)) return hipErrorInvalidValue;
+        int64_t tiles = 0;
+        for (int i = 0; i < n; ++i) {
+            const int64_t total = im[i].rows * im[i].rowlen;
+            int64_t nt = 0, blocks = 0;
+            reg_launch_geometry<InT, kRegU<InT, F>, FL>(total, kPersistBlocks, &nt, &blocks);
+            b.x[i] = im[i].x;
+            for (int f = 0; f < F; ++f) b.y[i][f] = im[i].y[f];
+            b.g[i] = make_geom<InT>(im[i].rows, total, im[i].rowlen, nullptr, nullptr);
+            b.tile0[i] = tiles;
+            tiles += nt;
+        }
+        b.tile0[n] = tiles;
+        b.n = n;
+        const int64_t blocks = (tiles + kBlock / kWave - 1) / (kBlock / kWave);
+        if (blocks == 0) return hipSuccess;
+        hipLaunchKernelGGL((fir1d_reg_batch_kernel<InT, STAGE, L, CH, kRegU<InT, F>, FL | kRagged, F>),
+                           dim3((unsigned)blocks), dim3(kBlock), 0, stream, b, t, 32 - acc_bits, frac);
+        return hipGetLastError();
+    }
+}
+
+template <typename InT, int STAGE, int L, int CH, int F>
+struct RegOne {  // one buffer (launch_reg_flags)
+    const void *x;
+    void* y;
+    int64_t rows, total, rowlen;
+    const int32_t* hq;
+    int frac, acc_bits;
+    hipStream_t s;
+    const void *hl, *hr;
+    template <int FL>
+    hipError_t run() const {
+        return launch_reg_flags<InT, STAGE, L, CH, F, FL>(x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr);
+    }
+};
+
+template <typename InT, int STAGE, int L, int CH, int F>
+struct RegMany {  // up to kRegBatch images (launch_reg_batch_flags)
+    int n;
+    const RegImage* im;
+    const int32_t* hq;
+    int frac, acc_bits;
+    hipStream_t s;
+    template <int FL>
+    hipError_t run() const {
+        return launch_reg_batch_flags<InT, STAGE, L, CH, F, FL>(n, im, hq, frac, acc_bits, s);
+    }
+};
+
 // Picks the kernel variant: acc_bits == 32 drops the wrap shifts; int16 samples with int16
 // taps (one channel) multiply on packed v_dot2_i32_i16; so do u8 samples (byte pairs) when
 // no accumulator can wrap: 255 * sum|h| + 2^(f-1) < 2^(acc_bits-1) for every filter.
-template <typename InT, int STAGE, int L, int CH, int F>
-static hipError_t launch_reg(const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
-                             const int32_t* hq, int frac, int acc_bits, hipStream_t stream, const void* hl,
-                             const void* hr) {
+template <typename InT, int STAGE, int L, int CH, int F, typename Go>
+static hipError_t launch_reg(const Go& go, const int32_t* hq, int frac, int acc_bits) {
     bool taps16 = true;
     for (int k = 0; k < F * L; ++k) taps16 &= hq[k] >= -32768 && hq[k] <= 32767;
     const bool acc32 = acc_bits == 32;
@@ -86,35 +164,46 @@ static hipError_t launch_reg(const void* x, void* y, int64_t rows, int64_t total
             TapsN<L, F> probe;
             for (int k = 0; k < F * L; ++k) probe.h[k / L][k % L] = hq[k];
             if (taps16 && nowrap && (plan_u8_pk16(probe, frac) & kU8Pk16))
-                return launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kU8Dot2 | kU8Pk16>(x, y, rows, total, rowlen, hq,
-                                                                                          frac, acc_bits, stream, hl, hr);
+                return go.template run<kRegFlags | kU8Dot2 | kU8Pk16>();
         }
         if (taps16 && nowrap)
-            return launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kU8Dot2>(x, y, rows, total, rowlen, hq, frac, acc_bits,
-                                                                               stream, hl, hr);
+            return go.template run<kRegFlags | kU8Dot2>();
     }
     if constexpr (sizeof(InT) == 2 && CH == 1) {
         if (taps16)
-            return acc32 ? launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kDot2 | kAcc32>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream, hl, hr)
-                         : launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kDot2>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream, hl, hr);
+            return acc32 ? go.template run<kRegFlags | kDot2 | kAcc32>()
+                         : go.template run<kRegFlags | kDot2>();
     }
-    return acc32 ? launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags | kAcc32>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream, hl, hr)
-                 : launch_reg_flags<InT, STAGE, L, CH, F, kRegFlags>(x, y, rows, total, rowlen, hq, frac, acc_bits, stream, hl, hr);
+    return acc32 ? go.template run<kRegFlags | kAcc32>()
+                 : go.template run<kRegFlags>();
 }
 
 template <typename InT, int STAGE, int CH, int F>
 hipError_t launch_reg_taps(int L, const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen,
                            const int32_t* hq, int frac, int acc_bits, hipStream_t s, const void* hl, const void* hr) {
     switch (L) {
-        case 1: return launch_reg<InT, STAGE, 1, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr);
-        case 2: return launch_reg<InT, STAGE, 2, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr);
-        case 3: return launch_reg<InT, STAGE, 3, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr);
-        case 4: return launch_reg<InT, STAGE, 4, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr);
-        case 5: return launch_reg<InT, STAGE, 5, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr);
-        case 6: return launch_reg<InT, STAGE, 6, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr);
-        case 7: return launch_reg<InT, STAGE, 7, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr);
-        case 8: return launch_reg<InT, STAGE, 8, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr);
-        case 9: return launch_reg<InT, STAGE, 9, CH, F>(x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr);
+        case 1: return launch_reg<InT, STAGE, 1, CH, F>(RegOne<InT, STAGE, 1, CH, F>{x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr}, hq, frac, acc_bits);
+        case 2: return launch_reg<InT, STAGE, 2, CH, F>(RegOne<InT, STAGE, 2, CH, F>{x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr}, hq, frac, acc_bits);
+        case 3: return launch_reg<InT, STAGE, 3, CH, F>(RegOne<InT, STAGE, 3, CH, F>{x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr}, hq, frac, acc_bits);
+        case 4: return launch_reg<InT, STAGE, 4, CH, F>(RegOne<InT, STAGE, 4, CH, F>{x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr}, hq, frac, acc_bits);
+        case 5: return launch_reg<InT, STAGE, 5, CH, F>(RegOne<InT, STAGE, 5, CH, F>{x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr}, hq, frac, acc_bits);
+        case 6: return launch_reg<InT, STAGE, 6, CH, F>(RegOne<InT, STAGE, 6, CH, F>{x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr}, hq, frac, acc_bits);
+        case 7: return launch_reg<InT, STAGE, 7, CH, F>(RegOne<InT, STAGE, 7, CH, F>{x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr}, hq, frac, acc_bits);
+        case 8: return launch_reg<InT, STAGE, 8, CH, F>(RegOne<InT, STAGE, 8, CH, F>{x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr}, hq, frac, acc_bits);
+        case 9: return launch_reg<InT, STAGE, 9, CH, F>(RegOne<InT, STAGE, 9, CH, F>{x, y, rows, total, rowlen, hq, frac, acc_bits, s, hl, hr}, hq, frac, acc_bits);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <typename InT, int STAGE, int CH, int F>
+hipError_t launch_reg_batch_taps(int L, int n, const RegImage* im, const int32_t* hq, int frac, int acc_bits,
+                                 hipStream_t s) {
+    switch (L) {
+#define FIR_BATCH_L(l) \
+    case l: return launch_reg<InT, STAGE, l, CH, F>(RegMany<InT, STAGE, l, CH, F>{n, im, hq, frac, acc_bits, s}, hq, frac, acc_bits);
+        FIR_BATCH_L(1) FIR_BATCH_L(2) FIR_BATCH_L(3) FIR_BATCH_L(4) FIR_BATCH_L(5)
+        FIR_BATCH_L(6) FIR_BATCH_L(7) FIR_BATCH_L(8) FIR_BATCH_L(9)
+#undef FIR_BATCH_L
         default: return hipErrorInvalidValue;
     }
 }

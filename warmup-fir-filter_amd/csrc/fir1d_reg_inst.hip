@@ -7,4 +7,6 @@ namespace fir {
 template hipError_t launch_reg_taps<FIR_INST_T, FIR_INST_STAGE, FIR_INST_CH, FIR_INST_F>(
     int L, const void* x, void* y, int64_t rows, int64_t total, int64_t rowlen, const int32_t* hq, int frac,
     int acc_bits, hipStream_t s, const void* halo_l, const void* halo_r);
+template hipError_t launch_reg_batch_taps<FIR_INST_T, FIR_INST_STAGE, FIR_INST_CH, FIR_INST_F>(
+    int L, int n, const RegImage* im, const int32_t* hq, int frac, int acc_bits, hipStream_t s);
 }  // namespace fir

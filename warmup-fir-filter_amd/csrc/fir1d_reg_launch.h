@@ -16,6 +16,22 @@ hipError_t launch_reg_taps(int L, const void* x, void* y, int64_t rows, int64_t 
                            const int32_t* hq, int frac, int acc_bits, hipStream_t s, const void* halo_l = nullptr,
                            const void* halo_r = nullptr);
 
+constexpr int kRegBatch = 8;  // images per batch launch
+
+// One image of a batch: rows x rowlen samples at x (16-byte aligned, rowlen >= a vector + L - 1
+// when rows > 1), output plane f (f < F <= 4) at y[f], any byte.
+struct RegImage {
+    const void* x;
+    void* y[4];
+    int64_t rows, rowlen;
+};
+
+// ONE launch over n <= kRegBatch (8) images, u8 stage, one channel (other configurations:
+// hipErrorInvalidValue); picks the variant as launch_reg_taps does.
+template <typename InT, int STAGE, int CH, int F>
+hipError_t launch_reg_batch_taps(int L, int n, const RegImage* im, const int32_t* hq, int frac, int acc_bits,
+                                 hipStream_t s);
+
 // Chunks of 64 vectors per wave (the tile), by sample type and filter count (rationale and
 // measurements: fir1d_reg_impl.h).
 template <typename InT, int F>

@@ -62,6 +62,12 @@ hipError_t launch_fir1d_lds(const void* x, int in_dtype, int64_t rows, int64_t r
 int launch_fir1d_rows_multi(const void* x, int in_dtype, int64_t rows, int64_t width, int ch, const int32_t* hq,
                             int L, int F, int frac, int acc_bits, int stage, void* y, hipStream_t stream,
                             std::string* err);
+// n images, F filters each: output plane (i, f) at planes[i * F + f]; every image is checked
+// before anything launches.  u8 -> sat-u8 banks of one channel on the register kernel go out as
+// ONE launch per 8 images (and per 4 filters), the rest as launch_fir1d_rows per plane.
+int launch_fir1d_images_multi(int n, const void* const* xs, const int64_t* rows, const int64_t* widths, int in_dtype,
+                              int ch, const int32_t* hq, int L, int F, int frac, int acc_bits, int stage,
+                              void* const* planes, hipStream_t stream, std::string* err);
 
 // Recompute the halo-dependent edge outputs of a single-row segment.
 int launch_fir1d_edges(const void* x, int in_dtype, int64_t n, int ch, const int32_t* hq, int L, int frac,

@@ -33,7 +33,7 @@ OUT_U8_SAT, OUT_I32 = 0, 1
 RESTORE_CLIP, RESTORE_NORMALIZE = 0, 1
 MAX_TAPS = 1 << 30  # FIR_MAX_TAPS: any practical length (the reference has no limit)
 IPC_HANDLE_BYTES = 64
-ABI_VERSION = 4
+ABI_VERSION = 5
 GATE_TIMEOUT = 1  # FIR_GATE_TIMEOUT
 GATE_LAYOUT = 2  # FIR_GATE_LAYOUT
 
@@ -60,6 +60,8 @@ EXPORTS = {
     "fir1d_fixed_rows_dev": (_i32, [_vp, _i32, _i64, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp]),
     "fir1d_fixed_rows_multi": (_i32, [_vp, _i32, _i64, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32]),
     "fir1d_fixed_rows_multi_dev": (_i32, [_vp, _i32, _i64, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
+    "fir1d_fixed_images_multi_dev": (_i32, [_i32, _vp, _vp, _vp, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp,
+                                            _vp]),
     "fir1d_fixed_edges_dev": (_i32, [_vp, _i32, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "fir1d_fixed_segment_dev": (_i32, [_vp, _i32, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "fir2d_fixed": (_i32, [_vp, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32]),

@@ -95,6 +95,68 @@ def fir1d_fixed_rows_multi_dev(x: torch.Tensor, hq2, frac_bits: int = 12, acc_bi
     return out
 
 
+class ImagesMultiPlan:
+    """fir1d_fixed_images_multi_dev with its arguments checked and marshalled once: launch()
+    re-issues the same call (the pipeline stage replayed on resident images) for the price of
+    one C call.  outs[i] is either one (F, *xs[i].shape) tensor or a list of F tensors shaped like
+    xs[i] (one buffer per output, as the reference keeps them; planes that start on 128 bytes
+    store whole cache lines); allocated as (F, *shape) tensors when None."""
+
+    def __init__(self, xs, hq2, frac_bits: int = 12, acc_bits: int = 32, out_stage: int = OUT_U8_SAT,
+                 channels: int = 1, outs=None):
+        xs = list(xs)
+        h2 = np.asarray(hq2, dtype=np.int64)
+        if h2.ndim != 2:
+            raise FirHipError("hq2 must be a (filters, taps) array")
+        nf, L = h2.shape
+        self._h = np.ascontiguousarray(h2, dtype=np.int32).reshape(-1)
+        if outs is None:
+            outs = [torch.empty((nf,) + tuple(x.shape), dtype=_OUT_DTYPE[out_stage], device=x.device) for x in xs]
+        outs = list(outs)
+        if len(outs) != len(xs):
+            raise FirHipError("outs must hold one entry per image")
+        planes = []
+        for i, (x, o) in enumerate(zip(xs, outs)):
+            _check_dev(x, f"xs[{i}]")
+            if x.dtype not in _IN or x.dtype != xs[0].dtype:
+                raise FirHipError(f"xs[{i}]: every image must be uint8, or every image int16")
+            if isinstance(o, torch.Tensor):
+                _check_dev(o, f"outs[{i}]")
+                ps = [o[f] for f in range(o.shape[0])] if o.dim() else []
+            else:
+                ps = list(o)
+            if len(ps) != nf or any(p.shape != x.shape or p.dtype != _OUT_DTYPE[out_stage] for p in ps):
+                raise FirHipError(f"outs[{i}] must hold {nf} planes shaped like xs[{i}] of the out_stage dtype")
+            for f, p in enumerate(ps):
+                _check_dev(p, f"outs[{i}][{f}]")
+                planes.append(p.data_ptr())
+        n = len(xs)
+        rowlen = [x.shape[-1] if x.dim() else 1 for x in xs]
+        self.xs, self.outs = xs, outs  # keep the buffers alive as long as the plan
+        self._args = (n, (ctypes.c_void_p * max(n, 1))(*[x.data_ptr() for x in xs]),
+                      (ctypes.c_int64 * max(n, 1))(*[x.numel() // r if r else 0 for x, r in zip(xs, rowlen)]),
+                      (ctypes.c_int64 * max(n, 1))(*[r // channels for r in rowlen]),
+                      _IN[xs[0].dtype] if xs else 0, channels, self._h.ctypes.data_as(ctypes.c_void_p), L, nf,
+                      int(frac_bits), int(acc_bits), int(out_stage),
+                      (ctypes.c_void_p * max(len(planes), 1))(*planes))
+        self._fn = lib().fir1d_fixed_images_multi_dev
+
+    def launch(self, stream=None):
+        """Issue the call on `stream` (default: the current stream of the images' device)."""
+        sp = _stream_ptr(self.xs[0], stream) if self.xs else None
+        _check(self._fn(*self._args, sp), "fir1d_fixed_images_multi_dev")
+        return self.outs
+
+
+def fir1d_fixed_images_multi_dev(xs, hq2, frac_bits: int = 12, acc_bits: int = 32, out_stage: int = OUT_U8_SAT,
+                                 channels: int = 1, outs=None, stream=None) -> list:
+    """The same F filters (rows of hq2) over several device images at once, outputs as
+    ImagesMultiPlan describes; equal to fir1d_fixed_rows_dev per (image, filter), from one call
+    (u8 -> sat-u8 banks: one launch per 8 images and 4 filters).  Replaces the per-image loop of
+    fir_1d/sim/vector/gen_fixed_output.py:88-107 (reference root)."""
+    return ImagesMultiPlan(xs, hq2, frac_bits, acc_bits, out_stage, channels, outs).launch(stream)
+
+
 def _halo_ptrs(x: torch.Tensor, L: int, channels: int, halo_left, halo_right):
     """ctypes pointers of the two halos (a device tensor of x's dtype, None, or an int address)."""
     hl_n, hr_n = (L - 1 - L // 2) * channels, (L // 2) * channels
