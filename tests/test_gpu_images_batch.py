@@ -135,7 +135,7 @@ def test_plan_replays_and_captures_into_a_graph():
     plan.launch()
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=torch.cuda.current_stream()):
+    with torch.cuda.graph(g):  # torch's capture stream is the current stream inside
         plan.launch()
     for trial in range(2):
         for x in xs:
