@@ -58,7 +58,7 @@ enum RegFlags : int {
     // Rows that straddle vectors, other stages / channel counts: seam vectors take the masked
     // generic pair (fir_vector_masked).  Without kMasked or kRagged the launcher guarantees
     // RowGeom::aligned, and the masked pair is not compiled in (it held 45 of the fused u8 bank's
-    // 90 VGPRs).
+    // 90 VGPRs; single-filter launches keep kMasked for its code layout, fir1d_reg_impl.h).
     kMasked = 16384,
 };
 

@@ -63,9 +63,13 @@ static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t
     if (!make_taps<L, F, FL>(t, hq, frac)) return hipErrorInvalidValue;
     int64_t ntiles = 0, blocks = 0;
     reg_launch_geometry<InT, kRegU<InT, F>, FL>(total, kPersistBlocks, &ntiles, &blocks);
+    // One filter keeps the masked pair compiled in even where it cannot run: that layout measured
+    // faster in the same process (int16 headline 244.6 vs 246.0 us, u8 77.3 vs 78.3;
+    // profiles/r05/masked_layout_ab.txt).  Banks drop it (90 -> 39 VGPRs, no loss).
+    constexpr int FM = F == 1 ? kMasked : 0;
     if constexpr (F == 1) {
         if (hl != nullptr || hr != nullptr) {
-            hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, kRegU<InT, F>, FL | kHalo, F>), dim3((unsigned)blocks),
+            hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, kRegU<InT, F>, FL | kHalo | FM, F>), dim3((unsigned)blocks),
                                dim3(kBlock), 0, stream, (const InT*)x, (OutT*)y, g, t, 32 - acc_bits, frac, ntiles);
             return hipGetLastError();
         }
@@ -78,7 +82,7 @@ static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t
                            dim3(kBlock), 0, stream, (const InT*)x, (OutT*)y, g, t, 32 - acc_bits, frac, ntiles);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, kRegU<InT, F>, FL, F>), dim3((unsigned)blocks), dim3(kBlock), 0,
+    hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, kRegU<InT, F>, FL | FM, F>), dim3((unsigned)blocks), dim3(kBlock), 0,
                        stream, (const InT*)x, (OutT*)y, g, t, 32 - acc_bits, frac, ntiles);
     return hipGetLastError();
 }
