@@ -18,7 +18,7 @@ call of its own, forwards rank 0's JSON line and exits with the children's statu
 fewer GPUs than ranks rehearses over gloo (ranks share devices; config.rehearsal says so).
 Extra keys:
   roofline      dominant kernel's algorithmic bytes / its mean duration (HIP events on the
-                stream it runs on: 100 untimed ramp launches, then 200 timed back to back,
+                stream it runs on: 100 untimed ramp launches and >= 50 ms of them, then 200 timed back to back,
                 whatever --steps/--warmup are), vs the 8.0 TB/s HBM3E peak; `traffic` = PMC
                 HBM bytes per launch from the committed rocprofv3 summary in profiles/ (null if
                 absent)
@@ -526,13 +526,37 @@ class Workload:
         return fir_hip.metrics_from_sums(got, self.n) == ref
 
 
+RAMP_MS = 50.0  # the roofline loop's untimed ramp lasts at least this much GPU time
+
+
+def ramp_launches(wl: Workload, at_least: int, world: int = 1, red_dev=None) -> int:
+    """Untimed launches of the dominant kernel for a ramp of >= RAMP_MS: short kernels need more
+    than a count of launches gives them (fir_2d 4 x 8192^2 ran 94 us in its first 100 launches,
+    83 in the next 200 and 78.9 after 300; the 16 us pipeline stage 17.5 before 300, 15.8 after;
+    rocprofv3 traces in gpurun_out r05x)."""
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        wl.dominant()
+    e1.record()
+    e1.synchronize()
+    est_ms = max(e0.elapsed_time(e1) / 5, 1e-3)
+    n = max(at_least, min(20000, int(RAMP_MS / est_ms) + 1))
+    if world > 1:  # the same count on every rank
+        t = torch.tensor([float(n)], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        n = int(t.item())
+    return n
+
+
 def measure(wl: Workload, steps: int, warmup: int, ramp: int, launches: int, world: int = 1,
             barrier=lambda: None, red_dev=None):
     """Time ``steps`` steps after ``warmup`` untimed ones (barrier + synchronize on both sides, max
-    over ranks), then the dominant kernel alone: ``ramp`` untimed launches (clocks ramp over ~40),
-    then ``launches`` back to back on the stream it runs on, bracketed by two HIP events (events
-    between launches would perturb the stream: each record adds a ~11 us gap).  Leaves the full
-    step's output in place.  Returns (elapsed s, host issue s, mean dominant-kernel s)."""
+    over ranks), then the dominant kernel alone: ``ramp`` untimed launches and at least RAMP_MS of
+    them (ramp_launches), then ``launches`` back to back on the stream it runs on, bracketed by
+    two HIP events (events between launches would perturb the stream: each record adds a ~11 us
+    gap).  Leaves the full step's output in place.  Returns (elapsed s, host issue s, mean
+    dominant-kernel s)."""
     for _ in range(warmup):
         wl.step()
     barrier()
@@ -550,7 +574,7 @@ def measure(wl: Workload, steps: int, warmup: int, ramp: int, launches: int, wor
         elapsed = float(t.item())
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     n_roof = max(1, launches)
-    for _ in range(max(0, ramp)):
+    for _ in range(ramp_launches(wl, max(0, ramp), world, red_dev) if ramp > 0 else 0):
         wl.dominant()
     torch.cuda.synchronize()
     ev0.record()
@@ -888,7 +912,9 @@ def main() -> int:
                      "kernel_avg_us_ranks": {"max": round(max(kern_ranks) * 1e6, 2),
                                              "min": round(min(kern_ranks) * 1e6, 2)},
                      "timing": f"HIP events around {n_roof} back-to-back launches of the kernel after "
-                               f"{max(0, args.roofline_ramp)} untimed ones"},
+                               f"{max(0, args.roofline_ramp)} untimed ones and at least {RAMP_MS:g} ms of them"
+                               if args.roofline_ramp > 0 else
+                               f"HIP events around {n_roof} back-to-back launches of the kernel, no ramp"},
         "cpu_baseline": cpu,
         "cpu_baseline_numpy": cpu_np,
         "cpu_baseline_numpy_threads": cpu_np_mt,

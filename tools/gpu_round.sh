@@ -84,6 +84,9 @@ for s in $STEPS; do
                      abrun/libfir_hip_bank_$v.so 10 bank; fatal $? || exit
              done ;;
         probe) run probe 200 python tools/pipeline_probe.py; fatal $? ;;
+        profwl_*) wl=${s#profwl_}
+             run "profwl_$wl" 300 rocprofv3 --kernel-trace --stats -d "$OUT/profwl_$wl" -o run --output-format csv -- \
+                 python bench.py --workload "$wl" --steps 200 --warmup 100 --cpu-seconds 0 --no-parity; fatal $? ;;
         libab_*) wl=${s#libab_}
              run "libab_$wl" 200 python tools/lib_ab.py warmup-fir-filter_amd/fir_hip/libfir_hip.so ${AB_LIB} 10 "$wl"; fatal $? ;;
         ltab_*) kind=${s#ltab_}

@@ -9,9 +9,11 @@
 //     table is built from, so that one is built only on a miss) behind a kind tag: looked up by a
 //     128-bit hash and its size, confirmed by comparing those bytes (a collision is a miss);
 //   * every hold counts as in use until the launch it was taken for has been enqueued, and each
-//     use then records an event on the launch's stream; a table is freed only when it has no
-//     hold and every use event has completed, never by a device-wide sync (which would also
-//     invalidate another thread's stream capture);
+//     use then records the table's event for that stream (one event per (table, stream),
+//     re-recorded by each later use: in stream order the latest record covers every earlier use,
+//     so a table used by millions of launches still holds one event per stream); a table is
+//     freed only when it has no hold and every stream's event has completed, never by a
+//     device-wide sync (which would also invalidate another thread's stream capture);
 //   * a table used by a launch that was captured into a hipGraph is pinned for the process life
 //     (the graph keeps its address);
 //   * past kTableBudget bytes per device the cache frees idle tables; when none is idle it grows
@@ -39,7 +41,8 @@ struct Entry {
     size_t bytes = 0;
     int holds = 0;                  // acquired, launch not yet enqueued
     bool pinned = false;            // used by a captured graph
-    std::vector<hipEvent_t> uses;   // one per enqueued use, pruned when complete
+    // the latest use on each stream that used it (an event re-recorded by every use there)
+    std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
 };
 
 // (hash, size) first: the source bytes are compared only between tables whose hashes are equal
@@ -68,9 +71,9 @@ TableCache* cache_for(int dev) {
 // true when every recorded use of e has completed (completed events go back to the pool)
 bool idle(TableCache* c, Entry& e) {
     size_t k = 0;
-    for (hipEvent_t ev : e.uses) {
-        if (hipEventQuery(ev) == hipSuccess) c->free_events.push_back(ev);
-        else e.uses[k++] = ev;
+    for (const auto& u : e.uses) {
+        if (hipEventQuery(u.second) == hipSuccess) c->free_events.push_back(u.second);
+        else e.uses[k++] = u;
     }
     e.uses.resize(k);
     return e.holds == 0 && !e.pinned && e.uses.empty();
@@ -165,6 +168,12 @@ void table_release(const void* d, hipStream_t stream, bool launched) {
         en.pinned = true;  // a graph holds the address for as long as it lives
         return;
     }
+    for (auto& u : en.uses) {
+        if (u.first == stream) {  // this stream's event: the new record covers the old one
+            if (hipEventRecord(u.second, stream) != hipSuccess) en.pinned = true;
+            return;
+        }
+    }
     hipEvent_t ev = nullptr;
     if (!c->free_events.empty()) {
         ev = c->free_events.back();
@@ -178,7 +187,7 @@ void table_release(const void* d, hipStream_t stream, bool launched) {
         en.pinned = true;
         return;
     }
-    en.uses.push_back(ev);
+    en.uses.emplace_back(stream, ev);
 }
 
 const void* device_table(const void* host, size_t bytes, std::string* err) {
