@@ -13,6 +13,7 @@ no exchange).
 from __future__ import annotations
 
 import argparse
+from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 from time import perf_counter
 
@@ -126,13 +127,25 @@ def _run_bank(x_u8: np.ndarray, pending: list, *, frac_bits: int, acc_bits: int,
             ys = fir_hip.fir1d_fixed_rows_multi(np.ascontiguousarray(x_u8, dtype=np.uint8),
                                                 np.stack([t for _, t in group]), f, a, fir_hip.OUT_U8_SAT,
                                                 device=devs[0], devices=devs if len(devs) > 1 else None)
-        for (out_path, _), y in zip(group, ys):
-            np.save(out_path, y)
-            written += 1
+        written += _save_all([(out_path, y) for (out_path, _), y in zip(group, ys)])
         i = j
     if error is not None:
         raise error
     return written
+
+
+def _save_all(items) -> int:
+    """np.save of a group's outputs, the files written concurrently (np.save releases the GIL
+    while it writes); every file is attempted, then the first error (in group order) is raised."""
+    if len(items) < 2:
+        for path, y in items:
+            np.save(path, y)
+        return len(items)
+    with ThreadPoolExecutor(max_workers=len(items)) as pool:
+        futs = [pool.submit(np.save, path, y) for path, y in items]
+    for f in futs:
+        f.result()
+    return len(items)
 
 
 def generate_fixed_3tap_output_vector(input_dir: Path = DEFAULT_INPUT_DIR, output_dir: Path = DEFAULT_OUTPUT_DIR,
