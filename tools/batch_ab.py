@@ -13,6 +13,8 @@ import torch
 
 BANK3 = (1365, 1365, 1365, 1024, 2048, 1024, -4096, 0, 4096, -512, 5120, -512)
 CASES = {"golden7": ((853, 1280), (762, 640), (854, 1280), (64, 64), (64, 64), (2999, 4499), (641, 1280)),
+         "golden7_big_first": ((2999, 4499), (853, 1280), (854, 1280), (641, 1280), (762, 640), (64, 64), (64, 64)),
+         "golden7_big_last": ((64, 64), (64, 64), (762, 640), (641, 1280), (853, 1280), (854, 1280), (2999, 4499)),
          "w4499": ((2999, 4499),), "w4496": ((2999, 4496),)}
 
 
