@@ -120,6 +120,8 @@ class ImagesMultiPlan:
             _check_dev(x, f"xs[{i}]")
             if x.dtype not in _IN or x.dtype != xs[0].dtype:
                 raise FirHipError(f"xs[{i}]: every image must be uint8, or every image int16")
+            if x.device != xs[0].device:
+                raise FirHipError(f"xs[{i}]: every image must be on {xs[0].device} (one launch, one device)")
             if isinstance(o, torch.Tensor):
                 _check_dev(o, f"outs[{i}]")
                 ps = [o[f] for f in range(o.shape[0])] if o.dim() else []
@@ -129,6 +131,8 @@ class ImagesMultiPlan:
                 raise FirHipError(f"outs[{i}] must hold {nf} planes shaped like xs[{i}] of the out_stage dtype")
             for f, p in enumerate(ps):
                 _check_dev(p, f"outs[{i}][{f}]")
+                if p.device != xs[0].device:
+                    raise FirHipError(f"outs[{i}][{f}] must be on {xs[0].device}")
                 planes.append(p.data_ptr())
         n = len(xs)
         rowlen = [x.shape[-1] if x.dim() else 1 for x in xs]
