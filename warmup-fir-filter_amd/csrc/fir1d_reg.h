@@ -51,7 +51,7 @@ enum RegFlags : int {
     // Rows that are not a whole number of vectors (the reference's 4499-wide image), u8 stage, one
     // channel: every vector is computed as if the rows were one signal (no masks, the interior
     // forms), then the lane whose vector holds a row seam rewrites the HLE + HRE outputs around it
-    // from the samples of their own row, in registers before the store (ragged_fix_*).  The masked
+    // from the samples of their own row, in registers before the store (ragged_put_bytes).  The masked
     // pair it replaces ran two generic windows for every seam vector: 27.0 vs 13.5 us for the
     // 4499 x 2999 bank (tools/pipeline_probe.py).
     kRagged = 8192,
