@@ -604,8 +604,10 @@ __device__ __forceinline__ void fir1d_reg_body(const InT* __restrict__ x, typena
 #pragma unroll
         for (int u = 0; u < U; ++u) load_vec<InT, NTL>(x, tile * (kWave * U) + u * kWave + lane, nvec, total, own[u]);
     }
-    // one tile per wave unless PERSIST: no loop, so nothing stays live past the tile's stores
-    for (; tile < ntiles; tile = PERSIST ? tile + stride : ntiles) {
+    // one tile per wave unless PERSIST: no loop, so nothing stays live past the tile's stores (the
+    // batch kernel spilled SGPRs with the loop).  Multi-chunk tiles (U > 1: one u8 filter) keep the
+    // loop form (it runs once there too): 77.8 vs 78.5 us, profiles/r05/u8_loop_form_ab.txt
+    for (; tile < ntiles; tile = (PERSIST || U > 1) ? tile + stride : ntiles) {
         const int64_t vb = tile * (kWave * U);
         uint32_t hv[4] = {0, 0, 0, 0};
         constexpr bool EDW = (FLAGS & kEdgeDword) && NDL <= 1 && NDR <= 1;
