@@ -60,6 +60,11 @@ enum RegFlags : int {
     // RowGeom::aligned, and the masked pair is not compiled in (it held 45 of the fused u8 bank's
     // 90 VGPRs; single-filter launches keep kMasked for its code layout, fir1d_reg_impl.h).
     kMasked = 16384,
+    // with kRagged: every filter's output bytes are held until ONE seam fix after the filter loop,
+    // then stored (batch launches that hold a ragged image): the 7 golden images' stage 15.05-15.35
+    // vs 15.48-15.95 us, but 2^28-sample banks 4-5 % slower (the stores go out later), so the
+    // single-image kernels keep the per-filter form (profiles/r05/pipeline_batch_ab.txt, r05ae)
+    kDefer = 32768,
 };
 
 // One non-temporal 16-byte row-store of the coalesced path, as inline asm: the same
@@ -588,6 +593,7 @@ __device__ __forceinline__ void fir1d_reg_body(const InT* __restrict__ x, typena
     constexpr bool COAL = (FLAGS & kCoal) && STAGE == FIR_OUT_I32;
     constexpr bool RAGGED = (FLAGS & kRagged) && STAGE == FIR_OUT_U8_SAT && CH == 1;
     constexpr bool MASKED = (FLAGS & kMasked) != 0;
+    constexpr bool DEFER = RAGGED && (FLAGS & kDefer) && L > 1;
     uint32_t bias = 0;
     int32_t sat_hi = 0;
     if constexpr (U8DOT2) {
@@ -700,8 +706,9 @@ __device__ __forceinline__ void fir1d_reg_body(const InT* __restrict__ x, typena
                 constexpr int NPR = RAGGED && L > 1 ? L - 1 : 1;
                 int32_t pv[F][NPR];
                 uint32_t pm[NPR][VEC / 4];
+                uint32_t ob[DEFER ? F : 1][VEC / 4];  // DEFER: every filter's bytes, stored after the seam fix
                 bool anyseam = false;
-                if constexpr (RAGGED && L > 1) {
+                if constexpr (RAGGED && L > 1 && !DEFER) {
                     anyseam = __builtin_amdgcn_ballot_w64(seam) != 0;
                     if (anyseam) {
                         const int sb = col0 < HLE ? -(int)col0 : (int)(rowlen - col0);  // seam's vector offset
@@ -726,7 +733,11 @@ __device__ __forceinline__ void fir1d_reg_body(const InT* __restrict__ x, typena
                             uint32_t o[VEC / 4];
                             u8_pk16_vec<L, VEC, FLAGS>(Pp, taps.hb[f], taps.pkbias[f], taps.pkshift[f], taps.pkmax,
                                                        md == 2, o);
-                            if constexpr (RAGGED && L > 1) {
+                            if constexpr (DEFER) {
+#pragma unroll
+                                for (int d = 0; d < VEC / 4; ++d) ob[f][d] = o[d];
+                                continue;
+                            } else if constexpr (RAGGED && L > 1) {
                                 if (anyseam) ragged_put_bytes<NPR, VEC>(pv[f], pm, o);
                             }
                             store_u8_dwords<VEC, NTS>(reinterpret_cast<uint8_t*>(yf[f]), g0, total, v < nvec, o);
@@ -762,9 +773,15 @@ __device__ __forceinline__ void fir1d_reg_body(const InT* __restrict__ x, typena
                                 t |= (uint32_t)(U8DOT2 ? q[4 * d + e] : stage_out32<STAGE>(q[4 * d + e])) << (8 * e);
                             o[d] = t;
                         }
-                        if (anyseam) ragged_put_bytes<NPR, VEC>(pv[f], pm, o);
-                        store_u8_dwords<VEC, NTS>(reinterpret_cast<uint8_t*>(yf[f]), g0, total, v < nvec, o);
-                        continue;
+                        if constexpr (DEFER) {
+#pragma unroll
+                            for (int d = 0; d < VEC / 4; ++d) ob[f][d] = o[d];
+                            continue;
+                        } else {
+                            if (anyseam) ragged_put_bytes<NPR, VEC>(pv[f], pm, o);
+                            store_u8_dwords<VEC, NTS>(reinterpret_cast<uint8_t*>(yf[f]), g0, total, v < nvec, o);
+                            continue;
+                        }
                     }
                     if constexpr (COAL) {
                         if (vb + (u + 1) * kWave <= nvec) {  // wave-uniform: the whole chunk is full
@@ -789,6 +806,27 @@ __device__ __forceinline__ void fir1d_reg_body(const InT* __restrict__ x, typena
                         }
                     }
                     store_vec<STAGE, VEC, NTS, U8DOT2>(yf[f], g0, total, v < nvec, q);
+                }
+                if constexpr (DEFER) {  // one seam fix for every filter, then the stores
+                    if (__builtin_amdgcn_ballot_w64(seam) != 0) {
+                        const int sb = col0 < HLE ? -(int)col0 : (int)(rowlen - col0);  // seam's vector offset
+                        int32_t sv[2 * (L - 1) + 1];
+                        if constexpr (sizeof(InT) == 1)
+                            ragged_samples_u8<L, NW, NDL>(Wd, sb, sv);
+                        else
+                            ragged_samples<L>(w, sb, sv);
+                        ragged_masks<NPR, VEC>(seam ? sb - HRE : -2 * VEC, pm);
+#pragma unroll
+                        for (int f = 0; f < F; ++f) {
+#pragma unroll
+                            for (int i = 0; i < L - 1; ++i)
+                                pv[f][i] = ragged_value<L, F, ACC32, U8DOT2 || DOT2>(sv, taps, f, i, shl, frac);
+                            ragged_put_bytes<NPR, VEC>(pv[f], pm, ob[f]);
+                        }
+                    }
+#pragma unroll
+                    for (int f = 0; f < F; ++f)
+                        store_u8_dwords<VEC, NTS>(reinterpret_cast<uint8_t*>(yf[f]), g0, total, v < nvec, ob[f]);
                 }
             }
         }

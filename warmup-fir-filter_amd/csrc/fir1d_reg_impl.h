@@ -100,6 +100,7 @@ static hipError_t launch_reg_batch_flags(int n, const RegImage* im, const int32_
         TapsN<L, F> t;
         if (!make_taps<L, F, FL>(t, hq, frac)) return hipErrorInvalidValue;
         int64_t tiles = 0;
+        bool ragged = false;
         for (int i = 0; i < n; ++i) {
             const int64_t total = im[i].rows * im[i].rowlen;
             int64_t nt = 0, blocks = 0;
@@ -107,6 +108,7 @@ static hipError_t launch_reg_batch_flags(int n, const RegImage* im, const int32_
             b.x[i] = im[i].x;
             for (int f = 0; f < F; ++f) b.y[i][f] = im[i].y[f];
             b.g[i] = make_geom<InT>(im[i].rows, total, im[i].rowlen, nullptr, nullptr);
+            ragged |= !b.g[i].aligned;
             b.tile0[i] = tiles;
             tiles += nt;
         }
@@ -114,8 +116,12 @@ static hipError_t launch_reg_batch_flags(int n, const RegImage* im, const int32_
         b.n = n;
         const int64_t blocks = (tiles + kBlock / kWave - 1) / (kBlock / kWave);
         if (blocks == 0) return hipSuccess;
-        hipLaunchKernelGGL((fir1d_reg_batch_kernel<InT, STAGE, L, CH, kRegU<InT, F>, FL | kRagged, F>),
-                           dim3((unsigned)blocks), dim3(kBlock), 0, stream, b, t, 32 - acc_bits, frac);
+        if (ragged)  // an image whose rows straddle vectors: the deferred-store seam form (kDefer)
+            hipLaunchKernelGGL((fir1d_reg_batch_kernel<InT, STAGE, L, CH, kRegU<InT, F>, FL | kRagged | kDefer, F>),
+                               dim3((unsigned)blocks), dim3(kBlock), 0, stream, b, t, 32 - acc_bits, frac);
+        else
+            hipLaunchKernelGGL((fir1d_reg_batch_kernel<InT, STAGE, L, CH, kRegU<InT, F>, FL | kRagged, F>),
+                               dim3((unsigned)blocks), dim3(kBlock), 0, stream, b, t, 32 - acc_bits, frac);
         return hipGetLastError();
     }
 }
