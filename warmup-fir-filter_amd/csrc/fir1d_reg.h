@@ -569,6 +569,25 @@ __device__ __forceinline__ void ragged_put_bytes(const int32_t* pv, const uint32
     }
 }
 
+// A seam wave's shared part: every filter's seam outputs pv (from the lane's window: Wd for u8
+// samples, the int32 window w otherwise) and the byte masks pm that put them at vector offsets
+// sb - HRE .. (all zero in a lane without a seam).
+template <typename InT, int L, int F, int VEC, bool ACC32, bool FROMPK, int NDL, int NW, int NS>
+__device__ __forceinline__ void ragged_prepare(const uint32_t (&Wd)[NW], const int32_t (&w)[NS], bool seam, int sb,
+                                               const TapsN<L, F>& taps, int shl, int frac, int32_t (&pv)[F][L - 1],
+                                               uint32_t (&pm)[L - 1][VEC / 4]) {
+    int32_t sv[2 * (L - 1) + 1];
+    if constexpr (sizeof(InT) == 1)
+        ragged_samples_u8<L, NW, NDL>(Wd, sb, sv);
+    else
+        ragged_samples<L>(w, sb, sv);
+#pragma unroll
+    for (int f = 0; f < F; ++f)
+#pragma unroll
+        for (int i = 0; i < L - 1; ++i) pv[f][i] = ragged_value<L, F, ACC32, FROMPK>(sv, taps, f, i, shl, frac);
+    ragged_masks<L - 1, VEC>(seam ? sb - L / 2 : -2 * VEC, pm);
+}
+
 // The tiles tile, tile + stride, ... below ntiles of one buffer (wave-uniform tile); output
 // plane f (g.total samples) at yf[f].
 template <typename InT, int STAGE, int L, int CH, int U, int FLAGS, int F>
@@ -708,22 +727,11 @@ __device__ __forceinline__ void fir1d_reg_body(const InT* __restrict__ x, typena
                 uint32_t pm[NPR][VEC / 4];
                 uint32_t ob[DEFER ? F : 1][VEC / 4];  // DEFER: every filter's bytes, stored after the seam fix
                 bool anyseam = false;
+                const int sb = col0 < HLE ? -(int)col0 : (int)(rowlen - col0);  // RAGGED: the seam's vector offset
                 if constexpr (RAGGED && L > 1 && !DEFER) {
                     anyseam = __builtin_amdgcn_ballot_w64(seam) != 0;
-                    if (anyseam) {
-                        const int sb = col0 < HLE ? -(int)col0 : (int)(rowlen - col0);  // seam's vector offset
-                        int32_t sv[2 * (L - 1) + 1];
-                        if constexpr (sizeof(InT) == 1)
-                            ragged_samples_u8<L, NW, NDL>(Wd, sb, sv);
-                        else
-                            ragged_samples<L>(w, sb, sv);
-#pragma unroll
-                        for (int f = 0; f < F; ++f)
-#pragma unroll
-                            for (int i = 0; i < L - 1; ++i)
-                                pv[f][i] = ragged_value<L, F, ACC32, U8DOT2 || DOT2>(sv, taps, f, i, shl, frac);
-                        ragged_masks<NPR, VEC>(seam ? sb - HRE : -2 * VEC, pm);
-                    }
+                    if (anyseam)
+                        ragged_prepare<InT, L, F, VEC, ACC32, U8DOT2 || DOT2, NDL>(Wd, w, seam, sb, taps, shl, frac, pv, pm);
                 }
 #pragma unroll
                 for (int f = 0; f < F; ++f) {
@@ -809,20 +817,9 @@ __device__ __forceinline__ void fir1d_reg_body(const InT* __restrict__ x, typena
                 }
                 if constexpr (DEFER) {  // one seam fix for every filter, then the stores
                     if (__builtin_amdgcn_ballot_w64(seam) != 0) {
-                        const int sb = col0 < HLE ? -(int)col0 : (int)(rowlen - col0);  // seam's vector offset
-                        int32_t sv[2 * (L - 1) + 1];
-                        if constexpr (sizeof(InT) == 1)
-                            ragged_samples_u8<L, NW, NDL>(Wd, sb, sv);
-                        else
-                            ragged_samples<L>(w, sb, sv);
-                        ragged_masks<NPR, VEC>(seam ? sb - HRE : -2 * VEC, pm);
+                        ragged_prepare<InT, L, F, VEC, ACC32, U8DOT2 || DOT2, NDL>(Wd, w, seam, sb, taps, shl, frac, pv, pm);
 #pragma unroll
-                        for (int f = 0; f < F; ++f) {
-#pragma unroll
-                            for (int i = 0; i < L - 1; ++i)
-                                pv[f][i] = ragged_value<L, F, ACC32, U8DOT2 || DOT2>(sv, taps, f, i, shl, frac);
-                            ragged_put_bytes<NPR, VEC>(pv[f], pm, ob[f]);
-                        }
+                        for (int f = 0; f < F; ++f) ragged_put_bytes<NPR, VEC>(pv[f], pm, ob[f]);
                     }
 #pragma unroll
                     for (int f = 0; f < F; ++f)
