@@ -529,18 +529,26 @@ __device__ __forceinline__ int32_t ragged_tap(const TapsN<L, F>& taps, int f, in
     }
 }
 
-// Seam output i of filter f, rounded (before the stage).
-template <int L, int F, bool ACC32, bool FROMPK>
+// Seam output i of filter f, rounded (before the stage).  NOWRAP (the byte-pair kernels, chosen
+// only when no sum can wrap): the sum starts at the rounding bias 2^(f-1) and one arithmetic shift
+// rounds it, floor((a + 2^(f-1)) / 2^f) = (a >> f) + bit f-1 of a, as the main path does; the
+// wrap and the two-term rounding of round_acc are identities there.  Fewer operations, the same
+// time within noise (profiles/r05/pipeline_batch_ab.txt, r05am; without any seam values, a
+// timing-only build, the stage ran 0.6 us faster).
+template <int L, int F, bool ACC32, bool FROMPK, bool NOWRAP>
 __device__ __forceinline__ int32_t ragged_value(const int32_t (&sv)[2 * (L - 1) + 1], const TapsN<L, F>& taps, int f,
-                                                int i, int shl, int frac) {
+                                                int i, int shl, int frac, uint32_t bias) {
     constexpr int C = L / 2, HLE = L - 1 - C, HRE = C, NP = L - 1;
-    uint32_t acc = 0;
+    uint32_t acc = NOWRAP ? bias : 0u;
 #pragma unroll
     for (int t = -HLE; t <= HRE; ++t) {
         const int k = i + t + HLE;
         if ((i >= HRE) == (k >= NP)) acc += (uint32_t)__mul24(ragged_tap<L, F, FROMPK>(taps, f, C - t), sv[k]);
     }
-    return round_acc<ACC32>(acc, shl, frac);
+    if constexpr (NOWRAP)
+        return (int32_t)acc >> frac;
+    else
+        return round_acc<ACC32>(acc, shl, frac);
 }
 
 // Put one filter's seam outputs pv[i] (rounded, before the stage) into the packed output bytes
@@ -572,9 +580,10 @@ __device__ __forceinline__ void ragged_put_bytes(const int32_t* pv, const uint32
 // A seam wave's shared part: every filter's seam outputs pv (from the lane's window: Wd for u8
 // samples, the int32 window w otherwise) and the byte masks pm that put them at vector offsets
 // sb - HRE .. (all zero in a lane without a seam).
-template <typename InT, int L, int F, int VEC, bool ACC32, bool FROMPK, int NDL, int NW, int NS>
+template <typename InT, int L, int F, int VEC, bool ACC32, bool FROMPK, bool NOWRAP, int NDL, int NW, int NS>
 __device__ __forceinline__ void ragged_prepare(const uint32_t (&Wd)[NW], const int32_t (&w)[NS], bool seam, int sb,
-                                               const TapsN<L, F>& taps, int shl, int frac, int32_t (&pv)[F][L - 1],
+                                               const TapsN<L, F>& taps, int shl, int frac, uint32_t bias,
+                                               int32_t (&pv)[F][L - 1],
                                                uint32_t (&pm)[L - 1][VEC / 4]) {
     int32_t sv[2 * (L - 1) + 1];
     if constexpr (sizeof(InT) == 1)
@@ -584,7 +593,8 @@ __device__ __forceinline__ void ragged_prepare(const uint32_t (&Wd)[NW], const i
 #pragma unroll
     for (int f = 0; f < F; ++f)
 #pragma unroll
-        for (int i = 0; i < L - 1; ++i) pv[f][i] = ragged_value<L, F, ACC32, FROMPK>(sv, taps, f, i, shl, frac);
+        for (int i = 0; i < L - 1; ++i)
+            pv[f][i] = ragged_value<L, F, ACC32, FROMPK, NOWRAP>(sv, taps, f, i, shl, frac, bias);
     ragged_masks<L - 1, VEC>(seam ? sb - L / 2 : -2 * VEC, pm);
 }
 
@@ -731,7 +741,8 @@ __device__ __forceinline__ void fir1d_reg_body(const InT* __restrict__ x, typena
                 if constexpr (RAGGED && L > 1 && !DEFER) {
                     anyseam = __builtin_amdgcn_ballot_w64(seam) != 0;
                     if (anyseam)
-                        ragged_prepare<InT, L, F, VEC, ACC32, U8DOT2 || DOT2, NDL>(Wd, w, seam, sb, taps, shl, frac, pv, pm);
+                        ragged_prepare<InT, L, F, VEC, ACC32, U8DOT2 || DOT2, U8DOT2, NDL>(Wd, w, seam, sb, taps, shl, frac, bias,
+                                                                                   pv, pm);
                 }
 #pragma unroll
                 for (int f = 0; f < F; ++f) {
@@ -817,7 +828,8 @@ __device__ __forceinline__ void fir1d_reg_body(const InT* __restrict__ x, typena
                 }
                 if constexpr (DEFER) {  // one seam fix for every filter, then the stores
                     if (__builtin_amdgcn_ballot_w64(seam) != 0) {
-                        ragged_prepare<InT, L, F, VEC, ACC32, U8DOT2 || DOT2, NDL>(Wd, w, seam, sb, taps, shl, frac, pv, pm);
+                        ragged_prepare<InT, L, F, VEC, ACC32, U8DOT2 || DOT2, U8DOT2, NDL>(Wd, w, seam, sb, taps, shl, frac, bias,
+                                                                                   pv, pm);
 #pragma unroll
                         for (int f = 0; f < F; ++f) ragged_put_bytes<NPR, VEC>(pv[f], pm, ob[f]);
                     }
