@@ -19,6 +19,9 @@
  *   fir1d_fixed_rows_multi[_dev] the same for F coefficient sets over one input: the loop
  *                         over a bank's filters in gen_fixed_output.py:92-105, one read of x
  *                         for up to 4 filters.
+ *   fir1d_fixed_images_multi_dev the stage's loop over images x coefficient sets
+ *                         (gen_fixed_output.py:88-107): up to 8 images x 4 filters per launch,
+ *                         each output plane its own device buffer (ABI 5).
  *   fir1d_fixed_edges_dev recomputes the first (L-1-L/2) and last (L/2) outputs of a
  *                         segment from neighbour halo samples (multi-GPU sharding, SURVEY
  *                         §8(e)); no reference counterpart (the reference is one process).
