@@ -41,7 +41,9 @@ struct Entry {
     size_t bytes = 0;
     int holds = 0;                  // acquired, launch not yet enqueued
     bool pinned = false;            // used by a captured graph
-    // the latest use on each stream that used it (an event re-recorded by every use there)
+    // the latest use on each stream that used it (an event re-recorded by every use there).  A
+    // destroyed stream's handle can name a new stream only once its resources are released, i.e.
+    // after its pending work, so re-recording on a reused handle never hides a running use.
     std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
 };
 
