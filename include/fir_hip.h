@@ -22,6 +22,12 @@
  *   fir1d_fixed_images_multi_dev the stage's loop over images x coefficient sets
  *                         (gen_fixed_output.py:88-107): up to 8 images x 4 filters per launch,
  *                         each output plane its own device buffer (ABI 5).
+ *   fir1d_fixed_images_multi  the same stage from host memory, as generate_fixed_{3,5}tap_output_vector
+ *                         (gen_fixed_output.py:88-107) runs it: every pending image uploaded once,
+ *                         one batch launch, each output plane downloaded on its own and handed to
+ *                         the caller (np.save) while the rest are in flight (ABI 6).
+ *   fir1d_ideal_images_multi  the ideal stage's loop (gen_ideal_output.py:75-86) the same way:
+ *                         one upload per image for all of its coefficient sets (ABI 6).
  *   fir1d_fixed_edges_dev recomputes the first (L-1-L/2) and last (L/2) outputs of a
  *                         segment from neighbour halo samples (multi-GPU sharding, SURVEY
  *                         §8(e)); no reference counterpart (the reference is one process).
@@ -52,7 +58,7 @@
 extern "C" {
 #endif
 
-#define FIR_HIP_ABI_VERSION 5
+#define FIR_HIP_ABI_VERSION 6
 /* Tap counts: any length up to FIR_MAX_TAPS (1-D taps; 2-D tap_rows * tap_cols), like the
  * reference's Python loop (fir_1d_fixed_ref.py:83-107, fir_1d_ref.py:49-63); the bound is the
  * int taps argument and device memory (4 B per tap), not the arithmetic.  Sums are exact as the
@@ -119,6 +125,36 @@ int fir1d_fixed_images_multi_dev(int n_images, const void* const* x_devs, const 
                                  const int64_t* widths, int in_dtype, int channels, const int32_t* hq,
                                  int taps, int filters, int frac_bits, int acc_bits, int out_stage,
                                  void* const* y_planes, void* stream);
+
+/* ---- host-memory image batches (ABI 6) ---------------------------------------------
+ * The stage drivers' entries: the pipeline stages read every image from a .npy file and write
+ * every output plane to its own .npy file, so the device work of a stage is one upload of its
+ * images, its kernels, and one download per plane.  fir1d_fixed_images_multi runs
+ * fir1d_fixed_images_multi_dev's launches (same layout of xs / rows / widths / y_planes, host
+ * pointers) on `device`: the images are copied to the device back to back (256-byte aligned), the
+ * planes come back one D2H copy each, in y_planes order, and `ready(ready_ctx, p)` (optional) is
+ * called on the calling thread as soon as plane p is in host memory -- while the later planes are
+ * still being copied -- so the caller can write it out under the remaining copies.  `ready` must
+ * not call this library for the same device.  Synchronous: every plane is in host memory when
+ * the entry returns.  With host buffers from fir_host_alloc (page-locked) every copy is a DMA at
+ * the PCIe rate; pageable buffers also work (staged by the runtime).  timing_ms (optional, NULL
+ * to skip) receives FIR_TIMING_SLOTS values in milliseconds: [0] the uploads, [1] the kernels,
+ * [2] the downloads (HIP events on the entry's stream), [3] the whole call on the host clock.
+ * fir1d_ideal_images_multi: the float64 ideal model the same way; h holds `filters` sets of
+ * `taps` coefficients (row-major), plane i * filters + f = image i under set f.
+ * fir_host_alloc / fir_host_free: page-locked host memory usable by every device's copies
+ * (hipHostMalloc, portable); bytes == 0 gives NULL. */
+typedef void (*fir_plane_ready_fn)(void* ctx, int plane);
+#define FIR_TIMING_SLOTS 4
+int fir1d_fixed_images_multi(int n_images, const void* const* xs, const int64_t* rows, const int64_t* widths,
+                             int in_dtype, int channels, const int32_t* hq, int taps, int filters, int frac_bits,
+                             int acc_bits, int out_stage, void* const* y_planes, int device,
+                             fir_plane_ready_fn ready, void* ready_ctx, double* timing_ms);
+int fir1d_ideal_images_multi(int n_images, const uint8_t* const* xs, const int64_t* rows, const int64_t* widths,
+                             const double* h, int taps, int filters, double* const* y_planes, int device,
+                             fir_plane_ready_fn ready, void* ready_ctx, double* timing_ms);
+int fir_host_alloc(int64_t bytes, void** out);
+int fir_host_free(void* p);
 
 /* Recompute the first (taps-1-taps/2)*channels and last (taps/2)*channels outputs of a
  * single-row segment of n*channels samples, reading out-of-segment samples from

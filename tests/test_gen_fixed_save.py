@@ -1,9 +1,14 @@
-"""The fixed-output stage writes a bank's files concurrently (gen_fixed_output._save_all): every
-file is attempted, the outputs are the arrays given, and the first failure (in bank order) is
-raised after the others were written."""
+"""The stages' ordered writer (stage_io.OrderedSaver, used by gen_fixed_output._save_all and the
+batched stages): files are written concurrently but put in place in the stage's order, and the
+first failure is the reference's own np.save error, raised after the files before it, with none
+of the files after it written (the reference's one-file-at-a-time loop,
+gen_fixed_output.py:92-105, stops there)."""
+import os
+
 import numpy as np
 import pytest
 
+from fir_1d.sim.vector import stage_io
 from fir_1d.sim.vector.gen_fixed_output import _save_all
 
 
@@ -13,15 +18,67 @@ def test_saves_every_file(tmp_path):
     assert _save_all(list(zip(paths, ys))) == 4
     for p, y in zip(paths, ys):
         assert np.array_equal(np.load(p), y)
+        assert p.read_bytes() == _npy_bytes(tmp_path, y)  # byte-identical to np.save(path, y)
     assert _save_all([]) == 0
     assert _save_all([(tmp_path / "one.npy", ys[0])]) == 1
+    assert not list(tmp_path.glob(".*.part"))
 
 
-def test_first_failure_is_raised_after_the_others_are_written(tmp_path):
+def _npy_bytes(tmp_path, y):
+    p = tmp_path / "ref_np_save.npy"
+    np.save(p, y)
+    b = p.read_bytes()
+    p.unlink()
+    return b
+
+
+def test_first_failure_stops_the_group_like_the_reference(tmp_path):
     ys = [np.full((2, 2), i, np.uint8) for i in range(3)]
     bad = tmp_path / "missing_dir" / "y1.npy"  # parent does not exist
     items = [(tmp_path / "y0.npy", ys[0]), (bad, ys[1]), (tmp_path / "y2.npy", ys[2])]
-    with pytest.raises(FileNotFoundError):
+    with pytest.raises(FileNotFoundError) as ei:
         _save_all(items)
+    with pytest.raises(FileNotFoundError) as ref:  # the reference's call, for the error text
+        np.save(bad, ys[1])
+    assert str(ei.value) == str(ref.value)
     assert np.array_equal(np.load(tmp_path / "y0.npy"), ys[0])
-    assert np.array_equal(np.load(tmp_path / "y2.npy"), ys[2])
+    assert not (tmp_path / "y2.npy").exists()  # the reference never reached it
+    assert sorted(p.name for p in tmp_path.iterdir()) == ["y0.npy"]  # no temporary files left
+
+
+def test_later_existing_files_keep_their_contents(tmp_path):
+    old = np.full((2, 2), 9, np.uint8)
+    np.save(tmp_path / "y2.npy", old)
+    (tmp_path / "y1.npy").mkdir()  # np.save(dir) fails: IsADirectoryError
+    ys = [np.full((2, 2), i, np.uint8) for i in range(3)]
+    with pytest.raises(IsADirectoryError):
+        _save_all([(tmp_path / f"y{i}.npy", y) for i, y in enumerate(ys)])
+    assert np.array_equal(np.load(tmp_path / "y0.npy"), ys[0])
+    assert np.array_equal(np.load(tmp_path / "y2.npy"), old)  # not overwritten
+
+
+@pytest.mark.skipif(os.geteuid() == 0, reason="root ignores file permissions")
+def test_read_only_target_raises_the_reference_permission_error(tmp_path):
+    p = tmp_path / "y0.npy"
+    np.save(p, np.zeros(3, np.uint8))
+    p.chmod(0o444)
+    with pytest.raises(PermissionError):
+        _save_all([(p, np.ones(3, np.uint8))])
+
+
+def test_npy_header_fast_path_accepts_only_2d_c_order_u8(tmp_path):
+    a = np.arange(12, dtype=np.uint8).reshape(3, 4)
+    np.save(tmp_path / "a.npy", a)
+    r, c, off = stage_io.npy_u8_2d_shape(tmp_path / "a.npy")
+    assert (r, c) == (3, 4)
+    out = np.empty(12, np.uint8)
+    assert stage_io.read_u8_2d_into(tmp_path / "a.npy", r, c, off, out)
+    assert np.array_equal(out.reshape(3, 4), a)
+    for name, arr in (("f", np.asfortranarray(a)), ("i16", a.astype(np.int16)), ("d1", a.reshape(-1)),
+                      ("d3", a.reshape(1, 3, 4))):
+        np.save(tmp_path / f"{name}.npy", arr)
+        assert stage_io.npy_u8_2d_shape(tmp_path / f"{name}.npy") is None
+    (tmp_path / "trunc.npy").write_bytes((tmp_path / "a.npy").read_bytes()[:-2])  # short data
+    assert stage_io.npy_u8_2d_shape(tmp_path / "trunc.npy") is None
+    (tmp_path / "junk.npy").write_bytes(b"not an npy file")
+    assert stage_io.npy_u8_2d_shape(tmp_path / "junk.npy") is None

@@ -146,3 +146,15 @@ def test_plan_replays_and_captures_into_a_graph():
         for x, ps in zip(xs, outs):
             got = np.stack([p.cpu().numpy() for p in ps])
             assert np.array_equal(got, _want(x.cpu().numpy(), hq)), trial
+
+
+def test_row_length_must_be_a_multiple_of_channels():
+    """An odd-width int16 image with channels=2 is refused, as fir1d_fixed_rows_dev does,
+    instead of filtering rows*(r-1) samples at row stride r-1."""
+    x = torch.zeros((4, 9), dtype=torch.int16, device=DEV)
+    with pytest.raises(fir_hip.FirHipError, match="multiple of channels"):
+        torch_ops.fir1d_fixed_images_multi_dev([x], [[1, 2, 1]], 12, 32, fir_hip.OUT_I32, channels=2)
+    ok = torch_ops.fir1d_fixed_images_multi_dev([x[:, :8].contiguous()], [[1, 2, 1]], 12, 32, fir_hip.OUT_I32,
+                                                channels=2)
+    torch.cuda.synchronize()
+    assert ok[0].shape == (1, 4, 8)

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -54,6 +55,8 @@ struct DeviceState {
     void* pin_in = nullptr;   // small calls: pinned host staging the kernel reads / writes directly
     void* pin_out = nullptr;
     size_t pin_cap = 0;
+    std::vector<hipEvent_t> plane_ev;  // the image-batch entries: one per output plane (grow-only)
+    hipEvent_t tev[4] = {};            // ... and their timing events (H2D start / end, kernels end, D2H end)
 };
 
 std::mutex g_devs_mu;
@@ -117,6 +120,8 @@ int init_locked(DeviceState* st, int device) {
     if (!st->stream_d2h) HIP_TRY(hipStreamCreateWithFlags(&st->stream_d2h, hipStreamNonBlocking));
     for (hipEvent_t& ev : st->chunk_ev)
         if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    for (hipEvent_t& ev : st->tev)
+        if (!ev) HIP_TRY(hipEventCreate(&ev));
     st->init = true;
     return FIR_OK;
 }
@@ -348,6 +353,111 @@ bool mul_ok(int64_t a, int64_t b, int64_t* out) {
     return true;
 }
 
+// The image-batch host entries (fir1d_fixed_images_multi, fir1d_ideal_images_multi): the stage's
+// whole set of images goes to the device in one run of H2D copies (each image on a 256-byte
+// boundary of the device input buffer), `launch(dx, dy, stream, err)` runs every kernel of the
+// stage on those copies (output plane p on a 256-byte boundary of the device output buffer:
+// planes start on whole cache lines), then each plane comes back by its own D2H copy, in plane
+// order, with an event behind it.  `ready(ctx, p)` is called on this thread as soon as plane p is
+// in host memory, while the later planes are still in flight, so the caller can write plane p out
+// (np.save) under the remaining copies; with pinned host buffers (fir_host_alloc) every copy is a
+// DMA that needs no host thread.  timing_ms (optional): FIR_TIMING_SLOTS values, see fir_hip.h.
+using PlaneReady = void (*)(void*, int);
+
+size_t align256(size_t v) { return (v + 255) / 256 * 256; }
+
+template <typename F>
+int run_host_images(int device, int n, const void* const* xs, const std::vector<size_t>& in_bytes, int np,
+                    void* const* ys, const std::vector<size_t>& out_bytes, F launch, PlaneReady ready, void* ctx,
+                    double* timing_ms) {
+    const auto t_host0 = std::chrono::steady_clock::now();
+    DeviceRestore restore;
+    DeviceState* st = nullptr;
+    int rc = device_state(device, &st);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(st->mu);
+    if ((rc = init_locked(st, device))) return rc;
+    std::vector<size_t> in_off(n), out_off(np);
+    size_t in_total = 0, out_total = 0;
+    for (int i = 0; i < n; ++i) {
+        in_off[i] = in_total;
+        in_total += align256(in_bytes[i]);
+    }
+    for (int p = 0; p < np; ++p) {
+        out_off[p] = out_total;
+        out_total += align256(out_bytes[p]);
+    }
+    if ((rc = ensure(st->in, std::max<size_t>(in_total, 256))) || (rc = ensure(st->out, std::max<size_t>(out_total, 256))))
+        return rc;
+    while ((int)st->plane_ev.size() < np) {
+        hipEvent_t ev = nullptr;
+        HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        st->plane_ev.push_back(ev);
+    }
+    std::vector<const void*> dx(n);
+    std::vector<void*> dy(np);
+    for (int i = 0; i < n; ++i) dx[i] = (const char*)st->in.ptr + in_off[i];
+    for (int p = 0; p < np; ++p) dy[p] = (char*)st->out.ptr + out_off[p];
+    hipStream_t s = st->stream;
+    // every copy and kernel already queued must finish before an error return: the caller may
+    // free its buffers, and the next call reuses the device buffers
+    auto bail = [&](int code, const std::string& msg) {
+        (void)hipStreamSynchronize(s);
+        return fail(code, msg);
+    };
+    hipError_t e = hipSuccess;
+    if (timing_ms) e = hipEventRecord(st->tev[0], s);
+    for (int i = 0; i < n && e == hipSuccess; ++i)
+        if (in_bytes[i]) e = hipMemcpyAsync((void*)dx[i], xs[i], in_bytes[i], hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && timing_ms) e = hipEventRecord(st->tev[1], s);
+    if (e != hipSuccess) return bail(FIR_EHIP, std::string("image upload: ") + hipGetErrorString(e));
+    std::string err;
+    if ((rc = launch(dx.data(), dy.data(), s, &err))) return bail(rc, err);
+    if (timing_ms && (e = hipEventRecord(st->tev[2], s)) != hipSuccess)
+        return bail(FIR_EHIP, std::string("hipEventRecord: ") + hipGetErrorString(e));
+    for (int p = 0; p < np && e == hipSuccess; ++p) {
+        if (out_bytes[p]) e = hipMemcpyAsync(ys[p], dy[p], out_bytes[p], hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipEventRecord(st->plane_ev[p], s);
+    }
+    if (e == hipSuccess && timing_ms) e = hipEventRecord(st->tev[3], s);
+    if (e != hipSuccess) return bail(FIR_EHIP, std::string("plane download: ") + hipGetErrorString(e));
+    for (int p = 0; p < np && ready; ++p) {
+        if ((e = hipEventSynchronize(st->plane_ev[p])) != hipSuccess)
+            return bail(FIR_EHIP, std::string("plane download: ") + hipGetErrorString(e));
+        ready(ctx, p);
+    }
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return fail(FIR_EHIP, std::string("image batch: ") + hipGetErrorString(e));
+    if (timing_ms) {
+        float ms[3] = {0, 0, 0};
+        for (int k = 0; k < 3; ++k)
+            if ((e = hipEventElapsedTime(&ms[k], st->tev[k], st->tev[k + 1])) != hipSuccess)
+                return fail(FIR_EHIP, std::string("hipEventElapsedTime: ") + hipGetErrorString(e));
+        for (int k = 0; k < 3; ++k) timing_ms[k] = ms[k];
+        timing_ms[3] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
+    }
+    return FIR_OK;
+}
+
+// Sizes of a batch of images (rows[i] x widths[i] x ch samples), FIR_EINVAL naming the image when
+// one is impossible or a pointer it needs is NULL.
+int image_sizes(int n, const void* const* xs, const int64_t* rows, const int64_t* widths, int64_t ch, int filters,
+                void* const* ys, std::vector<int64_t>* samples) {
+    if (n < 0) return fail(FIR_EINVAL, "images must be >= 0");
+    if (filters < 1) return fail(FIR_EINVAL, "filters must be >= 1");
+    if (n > 0 && (!xs || !rows || !widths || !ys)) return fail(FIR_EINVAL, "image arrays must not be NULL");
+    samples->assign(n, 0);
+    for (int i = 0; i < n; ++i) {
+        int64_t rw = 0, s = 0;
+        if (!mul_ok(rows[i], widths[i], &rw) || !mul_ok(rw, ch, &s))
+            return fail(FIR_EINVAL, "image " + std::to_string(i) + ": invalid rows/width/channels");
+        bool null = !xs[i];
+        for (int f = 0; f < filters; ++f) null |= !ys[(size_t)i * filters + f];
+        if (s && null) return fail(FIR_EINVAL, "image " + std::to_string(i) + ": x and its output planes must not be NULL");
+        (*samples)[i] = s;
+    }
+    return FIR_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -560,6 +670,44 @@ int fir1d_fixed_images_multi_dev(int n_images, const void* const* x_devs, const 
     }
 }
 
+int fir1d_fixed_images_multi(int n_images, const void* const* xs, const int64_t* rows, const int64_t* widths,
+                             int in_dtype, int channels, const int32_t* hq, int taps, int filters, int frac_bits,
+                             int acc_bits, int out_stage, void* const* y_planes, int device, fir_plane_ready_fn ready,
+                             void* ready_ctx, double* timing_ms) {
+    try {
+        if (channels < 1) return fail(FIR_EINVAL, "channels must be >= 1");
+        std::vector<int64_t> samples;
+        int rc = image_sizes(n_images, xs, rows, widths, channels, filters, y_planes, &samples);
+        if (rc) return rc;
+        {
+            std::string err;  // the scalar arguments, before any device work
+            rc = fir::launch_fir1d_rows_multi(nullptr, in_dtype, 0, 0, channels, hq, taps, filters, frac_bits, acc_bits,
+                                              out_stage, nullptr, nullptr, &err);
+            if (rc) return fail(rc, err);
+        }
+        int64_t total = 0;
+        for (int64_t s : samples) total += s;
+        if (total == 0) return FIR_OK;
+        const size_t isz = in_size(in_dtype), osz = out_size(out_stage);
+        std::vector<size_t> ib(n_images), ob((size_t)n_images * filters);
+        for (int i = 0; i < n_images; ++i) {
+            ib[i] = (size_t)samples[i] * isz;
+            for (int f = 0; f < filters; ++f) ob[(size_t)i * filters + f] = (size_t)samples[i] * osz;
+        }
+        return run_host_images(
+            device, n_images, xs, ib, n_images * filters, y_planes, ob,
+            [&](const void* const* dx, void* const* dy, hipStream_t s, std::string* err) {
+                return fir::launch_fir1d_images_multi(n_images, dx, rows, widths, in_dtype, channels, hq, taps, filters,
+                                                      frac_bits, acc_bits, out_stage, dy, s, err);
+            },
+            ready, ready_ctx, timing_ms);
+    } catch (const std::exception& ex) {
+        return fail(FIR_EHIP, std::string("internal error: ") + ex.what());
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
 int fir1d_fixed_edges_dev(const void* x_dev, int in_dtype, int64_t n, int channels, const int32_t* hq, int taps,
                           int frac_bits, int acc_bits, int out_stage, const void* halo_left_dev,
                           const void* halo_right_dev, void* y_dev, void* stream) {
@@ -660,6 +808,72 @@ int fir1d_ideal_rows_dev(const uint8_t* x_dev, int64_t rows, int64_t width, cons
     } catch (...) {
         return fail(FIR_EHIP, "internal error");
     }
+}
+
+int fir1d_ideal_images_multi(int n_images, const uint8_t* const* xs, const int64_t* rows, const int64_t* widths,
+                             const double* h, int taps, int filters, double* const* y_planes, int device,
+                             fir_plane_ready_fn ready, void* ready_ctx, double* timing_ms) {
+    try {
+        std::vector<int64_t> samples;
+        int rc = image_sizes(n_images, (const void* const*)xs, rows, widths, 1, filters, (void* const*)y_planes,
+                             &samples);
+        if (rc) return rc;
+        for (int f = 0; f < filters; ++f) {  // every filter's taps, before any device work
+            std::string err;
+            rc = fir::launch_fir1d_ideal(nullptr, 0, 0, h ? h + (size_t)f * (taps > 0 ? taps : 0) : nullptr, taps,
+                                         nullptr, nullptr, &err);
+            if (rc) return fail(rc, "filter " + std::to_string(f) + ": " + err);
+        }
+        int64_t total = 0;
+        for (int64_t s : samples) total += s;
+        if (total == 0) return FIR_OK;
+        std::vector<size_t> ib(n_images), ob((size_t)n_images * filters);
+        for (int i = 0; i < n_images; ++i) {
+            ib[i] = (size_t)samples[i];
+            for (int f = 0; f < filters; ++f) ob[(size_t)i * filters + f] = (size_t)samples[i] * sizeof(double);
+        }
+        return run_host_images(
+            device, n_images, (const void* const*)xs, ib, n_images * filters, (void* const*)y_planes, ob,
+            [&](const void* const* dx, void* const* dy, hipStream_t s, std::string* err) {
+                for (int i = 0; i < n_images; ++i) {
+                    if (!samples[i]) continue;
+                    for (int f = 0; f < filters; ++f) {
+                        const int r = fir::launch_fir1d_ideal((const uint8_t*)dx[i], rows[i], widths[i],
+                                                              h + (size_t)f * taps, taps,
+                                                              (double*)dy[(size_t)i * filters + f], s, err);
+                        if (r) return r;
+                    }
+                }
+                return (int)FIR_OK;
+            },
+            ready, ready_ctx, timing_ms);
+    } catch (const std::exception& ex) {
+        return fail(FIR_EHIP, std::string("internal error: ") + ex.what());
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int fir_host_alloc(int64_t bytes, void** out) {
+    try {
+        if (!out || bytes < 0) return fail(FIR_EINVAL, "invalid arguments");
+        *out = nullptr;
+        if (bytes == 0) return FIR_OK;
+        hipError_t e = hipHostMalloc(out, (size_t)bytes, hipHostMallocPortable);
+        if (e != hipSuccess) {
+            *out = nullptr;
+            return fail(FIR_ENOMEM, "hipHostMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+        }
+        return FIR_OK;
+    } catch (...) {
+        return fail(FIR_EHIP, "internal error");
+    }
+}
+
+int fir_host_free(void* p) {
+    if (!p) return FIR_OK;
+    hipError_t e = hipHostFree(p);
+    return e == hipSuccess ? FIR_OK : fail(FIR_EHIP, std::string("hipHostFree: ") + hipGetErrorString(e));
 }
 
 int64_t fir_metrics_work_bytes(int64_t n) { return (int64_t)fir::metrics_work_bytes(n); }

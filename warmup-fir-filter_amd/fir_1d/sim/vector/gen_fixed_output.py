@@ -3,17 +3,19 @@
 Mirror of the reference stage ``fir_1d/sim/vector/gen_fixed_output.py``: same public
 entry points, keyword arguments, file naming (``{case}__{coeff}_fixed_{3,5}tap_y_u8.npy``
 under ``output_dir/fixed_{3,5}tap``), skip-if-exists / ``overwrite`` behaviour, return
-value (number of files generated) and CLI flags.  The difference is the row driver:
-the reference calls the golden model once per image row (:34-60); here the whole
-image goes to the GPU in one ``fir1d_fixed_rows`` launch (rows are independent and
-zero padding resets at each row edge inside the kernel).  ``devices`` / ``--devices N``
-(Config row) spreads an image's rows over several GPUs (rows are independent:
-no exchange).
+value (number of files generated), error order and CLI flags.  The difference is the driver:
+the reference calls the golden model once per image row (:34-60) inside its loop over images
+and coefficient sets (:88-107); here the whole stage is ONE device call
+(``fir_hip.fir1d_fixed_images_multi``, ``stage_io.run_image_stage``): the inputs read straight
+into page-locked staging, one upload, one batch launch over every image and coefficient set,
+each output plane downloaded on its own and written (np.save) while the later planes are still
+in flight.  ``devices`` / ``--devices N`` (Config row) instead spreads each image's
+rows over several GPUs (rows are independent: no exchange).  ``timings`` (a dict) receives the
+stage's breakdown: plan / load / H2D / kernel / D2H / save / wall, in milliseconds.
 """
 from __future__ import annotations
 
 import argparse
-from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 from time import perf_counter
 
@@ -22,6 +24,7 @@ import numpy as np
 import fir_hip
 from fir_1d.model.python.fir_1d_fixed_ref import _coeff_stage, device_bits, quantize_fixed_taps
 from fir_1d.model.python.fir_1d_ref import _prepare_rows_u8, _validate_h_coefficients
+from fir_1d.sim.vector import stage_io
 from fir_1d.sim.vector.h_coeff import h_coeff_3tap_map, h_coeff_5tap_map
 
 THIS_FILE = Path(__file__).resolve()
@@ -74,23 +77,72 @@ def _run_fixed_rowwise(x_u8: np.ndarray, h: list[float], *, frac_bits: int, acc_
 
 def _generate_fixed_outputs_for_tap_map(*, input_dir: Path, out_dir: Path, coeff_map: dict[str, list[float]],
                                         tap_label: str, frac_bits: int, acc_bits: int, coeff_bits: int,
-                                        overwrite: bool = False, devices=None) -> int:
+                                        overwrite: bool = False, devices=None, timings: dict | None = None) -> int:
     inputs = _iter_input_npy_files(input_dir)
     if not inputs:
         raise FileNotFoundError(f"No input .npy files found in {input_dir}")
     out_dir.mkdir(parents=True, exist_ok=True)
-    generated = 0
-    for in_path in inputs:
-        x_u8 = _load_input_image_u8(in_path)
-        stem = _case_stem_from_input(in_path)
-        pending = []
-        for coeff_name, h in coeff_map.items():
-            out_path = out_dir / f"{stem}__{coeff_name}_fixed_{tap_label}_y_u8.npy"
-            if not out_path.exists() or overwrite:
-                pending.append((out_path, h))
-        generated += _run_bank(x_u8, pending, frac_bits=frac_bits, acc_bits=acc_bits, coeff_bits=coeff_bits,
-                               devices=devices)
-    return generated
+    devs = fir_hip.parse_devices(devices)
+    if len(devs) > 1:  # each image's rows over several devices, image by image
+        generated = 0
+        for in_path in inputs:
+            x_u8 = _load_input_image_u8(in_path)
+            stem = _case_stem_from_input(in_path)
+            pending = []
+            for coeff_name, h in coeff_map.items():
+                out_path = out_dir / f"{stem}__{coeff_name}_fixed_{tap_label}_y_u8.npy"
+                if not out_path.exists() or overwrite:
+                    pending.append((out_path, h))
+            generated += _run_bank(x_u8, pending, frac_bits=frac_bits, acc_bits=acc_bits, coeff_bits=coeff_bits,
+                                   devices=devs)
+        return generated
+    taps: dict = {}  # coefficient set -> quantized taps, or the exception its validation raised
+
+    def quantized(name):
+        if name not in taps:
+            try:
+                taps[name] = quantize_fixed_taps(coeff_map[name], frac_bits, acc_bits, coeff_bits)
+            except ValueError as exc:
+                taps[name] = exc
+        return taps[name]
+
+    def plan_items(stem, shape):
+        """The reference's inner loop (gen_fixed_output.py:92-105) without the compute: skipped
+        files, then each pending set's checks in bank order (none for an image with no rows: its
+        row loop never calls the model).  A failing set ends the stage there."""
+        items = []
+        for name in coeff_map:
+            out_path = out_dir / f"{stem}__{name}_fixed_{tap_label}_y_u8.npy"
+            if out_path.exists() and not overwrite:
+                continue
+            if shape[0] > 0:
+                q = quantized(name)
+                if isinstance(q, Exception):
+                    return items, q
+            items.append((out_path, name))
+        return items, None
+
+    f, a = device_bits(frac_bits, acc_bits)
+
+    def compute(xs, keys, outs, ready, timing):
+        """Every image under the sets ``keys``: one device call per tap length (the reference's
+        banks have one), each a single batch launch."""
+        calls, i = 0, 0
+        while i < len(keys):
+            j = i
+            while j < len(keys) and len(taps[keys[j]]) == len(taps[keys[i]]):
+                j += 1
+            t: dict = {}
+            fir_hip.fir1d_fixed_images_multi(xs, np.stack([taps[k] for k in keys[i:j]]), f, a, fir_hip.OUT_U8_SAT,
+                                             device=devs[0], outs=[o[i:j] for o in outs],
+                                             ready=lambda im, g, i=i: ready(im, i + g), timing=t)
+            for k, v in t.items():
+                timing[k] = timing.get(k, 0.0) + v
+            calls += 1
+            i = j
+        timing["calls"] = calls
+
+    return stage_io.run_image_stage(inputs, _case_stem_from_input, plan_items, compute, np.uint8, timings)
 
 
 def _run_bank(x_u8: np.ndarray, pending: list, *, frac_bits: int, acc_bits: int, coeff_bits: int,
@@ -135,35 +187,34 @@ def _run_bank(x_u8: np.ndarray, pending: list, *, frac_bits: int, acc_bits: int,
 
 
 def _save_all(items) -> int:
-    """np.save of a group's outputs, the files written concurrently (np.save releases the GIL
-    while it writes); every file is attempted, then the first error (in group order) is raised."""
-    if len(items) < 2:
-        for path, y in items:
-            np.save(path, y)
-        return len(items)
-    with ThreadPoolExecutor(max_workers=len(items)) as pool:
-        futs = [pool.submit(np.save, path, y) for path, y in items]
-    for f in futs:
-        f.result()
-    return len(items)
+    """np.save of a group's outputs (stage_io.OrderedSaver): written concurrently, put in place in
+    group order; the first failure is raised after the files before it, and none after it exists,
+    as the reference's one-file-at-a-time loop (gen_fixed_output.py:92-105) leaves them."""
+    saver = stage_io.OrderedSaver(workers=max(1, min(len(items), stage_io.SAVE_WORKERS)))
+    try:
+        for i, (path, y) in enumerate(items):
+            saver.submit(i, path, y)
+        return saver.commit()
+    finally:
+        saver.close()
 
 
 def generate_fixed_3tap_output_vector(input_dir: Path = DEFAULT_INPUT_DIR, output_dir: Path = DEFAULT_OUTPUT_DIR,
                                       *, frac_bits: int = 12, acc_bits: int = 32, coeff_bits: int = 16,
-                                      overwrite: bool = False, devices=None) -> int:
+                                      overwrite: bool = False, devices=None, timings: dict | None = None) -> int:
     return _generate_fixed_outputs_for_tap_map(
         input_dir=Path(input_dir).resolve(), out_dir=Path(output_dir).resolve() / "fixed_3tap",
         coeff_map=h_coeff_3tap_map, tap_label="3tap", frac_bits=frac_bits, acc_bits=acc_bits,
-        coeff_bits=coeff_bits, overwrite=overwrite, devices=devices)
+        coeff_bits=coeff_bits, overwrite=overwrite, devices=devices, timings=timings)
 
 
 def generate_fixed_5tap_output_vector(input_dir: Path = DEFAULT_INPUT_DIR, output_dir: Path = DEFAULT_OUTPUT_DIR,
                                       *, frac_bits: int = 12, acc_bits: int = 32, coeff_bits: int = 16,
-                                      overwrite: bool = False, devices=None) -> int:
+                                      overwrite: bool = False, devices=None, timings: dict | None = None) -> int:
     return _generate_fixed_outputs_for_tap_map(
         input_dir=Path(input_dir).resolve(), out_dir=Path(output_dir).resolve() / "fixed_5tap",
         coeff_map=h_coeff_5tap_map, tap_label="5tap", frac_bits=frac_bits, acc_bits=acc_bits,
-        coeff_bits=coeff_bits, overwrite=overwrite, devices=devices)
+        coeff_bits=coeff_bits, overwrite=overwrite, devices=devices, timings=timings)
 
 
 def _build_argparser() -> argparse.ArgumentParser:

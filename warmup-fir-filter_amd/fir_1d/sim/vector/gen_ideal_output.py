@@ -2,9 +2,12 @@
 
 Mirror of the reference stage ``fir_1d/sim/vector/gen_ideal_output.py`` (entry points,
 naming ``{case}__{coeff}_ideal_{3,5}tap_y_f64.npy`` under ``output_dir/ideal_{3,5}tap``,
-skip-if-exists, return count, CLI flags).  The per-row loop of the reference
-(:37-50) becomes one ``fir1d_ideal_rows`` launch per image, bit-exact in float64
-(``devices`` / ``--devices N``: the image's rows spread over several GPUs, no exchange).
+skip-if-exists, return count, error order, CLI flags).  The reference's loops over images,
+coefficient sets (:75-86) and rows (:37-50) become ONE device call per stage
+(``fir_hip.fir1d_ideal_images_multi`` through ``stage_io.run_image_stage``: each image uploaded
+once for all four sets, every plane bit-exact in float64, downloaded and written while the later
+planes are in flight); ``devices`` / ``--devices N`` instead spreads each image's rows over several
+GPUs (no exchange).  ``timings`` (a dict) receives the stage's breakdown in milliseconds.
 """
 from __future__ import annotations
 
@@ -16,6 +19,7 @@ import numpy as np
 
 import fir_hip
 from fir_1d.model.python.fir_1d_ref import _prepare_rows_u8, _validate_h_coefficients
+from fir_1d.sim.vector import stage_io
 from fir_1d.sim.vector.gen_fixed_output import _case_stem_from_input, _iter_input_npy_files, _load_input_image_u8
 from fir_1d.sim.vector.h_coeff import h_coeff_3tap_map, h_coeff_5tap_map
 
@@ -42,36 +46,77 @@ def _run_ideal_rowwise(x_u8: np.ndarray, h: list[float], devices=None) -> np.nda
 
 
 def _generate_ideal_outputs_for_tap_map(*, input_dir: Path, out_dir: Path, coeff_map: dict[str, list[float]],
-                                        tap_label: str, overwrite: bool = False, devices=None) -> int:
+                                        tap_label: str, overwrite: bool = False, devices=None,
+                                        timings: dict | None = None) -> int:
     inputs = _iter_input_npy_files(input_dir)
     if not inputs:
         raise FileNotFoundError(f"No input .npy files found in {input_dir}")
     out_dir.mkdir(parents=True, exist_ok=True)
-    generated = 0
-    for in_path in inputs:
-        x_u8 = _load_input_image_u8(in_path)
-        stem = _case_stem_from_input(in_path)
-        for coeff_name, h in coeff_map.items():
-            out_path = out_dir / f"{stem}__{coeff_name}_ideal_{tap_label}_y_f64.npy"
+    devs = fir_hip.parse_devices(devices)
+    if len(devs) > 1:  # each image's rows over several devices, one (image, set) at a time
+        generated = 0
+        for in_path in inputs:
+            x_u8 = _load_input_image_u8(in_path)
+            stem = _case_stem_from_input(in_path)
+            for coeff_name, h in coeff_map.items():
+                out_path = out_dir / f"{stem}__{coeff_name}_ideal_{tap_label}_y_f64.npy"
+                if out_path.exists() and not overwrite:
+                    continue
+                np.save(out_path, _run_ideal_rowwise(x_u8, h, devs))
+                generated += 1
+        return generated
+
+    def plan_items(stem, shape):
+        """The reference's inner loop (gen_ideal_output.py:79-86) without the compute: skipped
+        files, then each pending set's check (fir_1d_ref.py:9-24; none for an image with no rows,
+        whose row loop never calls the model).  A failing set ends the stage there."""
+        items = []
+        for name, h in coeff_map.items():
+            out_path = out_dir / f"{stem}__{name}_ideal_{tap_label}_y_f64.npy"
             if out_path.exists() and not overwrite:
                 continue
-            np.save(out_path, _run_ideal_rowwise(x_u8, h, devices))
-            generated += 1
-    return generated
+            if shape[0] > 0:
+                try:
+                    _validate_h_coefficients(h)
+                except ValueError as exc:
+                    return items, exc
+            items.append((out_path, name))
+        return items, None
+
+    def compute(xs, keys, outs, ready, timing):
+        """Every image under the sets ``keys``: one device call per tap length."""
+        calls, i = 0, 0
+        while i < len(keys):
+            j = i
+            while j < len(keys) and len(coeff_map[keys[j]]) == len(coeff_map[keys[i]]):
+                j += 1
+            t: dict = {}
+            fir_hip.fir1d_ideal_images_multi(xs, [[float(v) for v in coeff_map[k]] for k in keys[i:j]],
+                                             device=devs[0], outs=[o[i:j] for o in outs],
+                                             ready=lambda im, g, i=i: ready(im, i + g), timing=t)
+            for k, v in t.items():
+                timing[k] = timing.get(k, 0.0) + v
+            calls += 1
+            i = j
+        timing["calls"] = calls
+
+    return stage_io.run_image_stage(inputs, _case_stem_from_input, plan_items, compute, np.float64, timings)
 
 
 def generate_ideal_3tap_output_vector(input_dir: Path = DEFAULT_INPUT_DIR, output_dir: Path = DEFAULT_OUTPUT_DIR,
-                                      *, overwrite: bool = False, devices=None) -> int:
+                                      *, overwrite: bool = False, devices=None, timings: dict | None = None) -> int:
     return _generate_ideal_outputs_for_tap_map(
         input_dir=Path(input_dir).resolve(), out_dir=Path(output_dir).resolve() / "ideal_3tap",
-        coeff_map=h_coeff_3tap_map, tap_label="3tap", overwrite=overwrite, devices=devices)
+        coeff_map=h_coeff_3tap_map, tap_label="3tap", overwrite=overwrite, devices=devices,
+        timings=timings)
 
 
 def generate_ideal_5tap_output_vector(input_dir: Path = DEFAULT_INPUT_DIR, output_dir: Path = DEFAULT_OUTPUT_DIR,
-                                      *, overwrite: bool = False, devices=None) -> int:
+                                      *, overwrite: bool = False, devices=None, timings: dict | None = None) -> int:
     return _generate_ideal_outputs_for_tap_map(
         input_dir=Path(input_dir).resolve(), out_dir=Path(output_dir).resolve() / "ideal_5tap",
-        coeff_map=h_coeff_5tap_map, tap_label="5tap", overwrite=overwrite, devices=devices)
+        coeff_map=h_coeff_5tap_map, tap_label="5tap", overwrite=overwrite, devices=devices,
+        timings=timings)
 
 
 def main(argv=None) -> int:

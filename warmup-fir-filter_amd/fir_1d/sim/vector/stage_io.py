@@ -1,0 +1,336 @@
+"""Host side of the pipeline's vector stages on the GPU: one device call per stage.
+
+The reference's stages (fir_1d/sim/vector/gen_fixed_output.py:88-107, gen_ideal_output.py:75-86)
+loop over the input images and, per image, over the coefficient sets: np.load, the row-wise model,
+np.save of one .npy file per (image, set).  Here a stage is planned first -- every input's header
+read, its pending outputs found (skip-if-exists / overwrite) and its coefficient sets checked in
+the reference's order -- then run as ONE device call (fir_hip.fir1d_{fixed,ideal}_images_multi):
+
+* the inputs are read straight from their .npy files into one page-locked staging buffer (no
+  np.load copy, every upload a DMA), all images uploaded by one run of copies;
+* one batch launch computes every (image, set) plane;
+* each plane comes back into page-locked memory by its own copy, and is handed to a pool of
+  writer threads as soon as it lands, so the np.save of plane p overlaps the copies of the later
+  planes; the files are written under temporary names and renamed into place in the
+  reference's order.
+
+Error behaviour is the reference's: a stage stops at the first failing item in its order (an
+input that np.load refuses, a coefficient set that fails validation, a file np.save cannot
+write) with that item's own exception, after writing every output before it and none after it.
+A write that fails in the pool is redone as the reference's own np.save(path, y) call, which
+raises the reference's error (or succeeds, and the stage goes on).
+"""
+from __future__ import annotations
+
+import os
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+import numpy as np
+
+import fir_hip
+
+# One device call takes at most this many bytes of input + output planes (page-locked staging);
+# a larger stage runs as several calls, image-aligned (an image larger than this runs alone).
+BATCH_BYTES = int(os.environ.get("FIR_STAGE_BATCH_BYTES", str(1 << 30)))
+SAVE_WORKERS = 8  # np.save releases the GIL while it writes; the box's page cache takes parallel writes
+
+
+def _align(n: int, a: int = 256) -> int:
+    return (n + a - 1) // a * a
+
+
+class _Arena:
+    """Grow-only page-locked buffers of one thread (fir_hip.host_empty): allocating pinned memory
+    costs far more than a stage's copies, so the stages of a pipeline run share it."""
+
+    def __init__(self):
+        self.bufs: dict[str, np.ndarray] = {}
+
+    def take(self, slot: str, nbytes: int) -> np.ndarray:
+        buf = self.bufs.get(slot)
+        if buf is None or buf.size < nbytes:
+            self.bufs.pop(slot, None)
+            want = max(nbytes, 0 if buf is None else buf.size + buf.size // 4)
+            try:
+                buf = fir_hip.host_empty(want)
+            except fir_hip.FirHipError:  # no page-locked memory to be had: pageable works, slower
+                buf = np.empty(want, dtype=np.uint8)
+            self.bufs[slot] = buf
+        return buf
+
+
+_tls = threading.local()
+
+
+def arena() -> _Arena:
+    if not hasattr(_tls, "arena"):
+        _tls.arena = _Arena()
+    return _tls.arena
+
+
+def npy_u8_2d_shape(path: Path):
+    """(rows, cols, data offset) of a .npy file holding a 2-D C-order uint8 array, else None (the
+    caller then uses np.load, which reads -- or refuses -- the file as the reference does)."""
+    try:
+        with open(path, "rb") as f:
+            version = np.lib.format.read_magic(f)
+            if version == (1, 0):
+                shape, fortran, dtype = np.lib.format.read_array_header_1_0(f)
+            elif version == (2, 0):
+                shape, fortran, dtype = np.lib.format.read_array_header_2_0(f)
+            else:
+                return None
+            off = f.tell()
+            size = os.fstat(f.fileno()).st_size
+    except Exception:  # noqa: BLE001 - anything np.load would judge: leave it to np.load
+        return None
+    if dtype != np.dtype(np.uint8) or fortran or len(shape) != 2:
+        return None
+    if size - off < shape[0] * shape[1]:
+        return None
+    return int(shape[0]), int(shape[1]), off
+
+
+def read_u8_2d_into(path: Path, rows: int, cols: int, off: int, out: np.ndarray) -> bool:
+    """Read the array of a file npy_u8_2d_shape accepted into ``out`` (rows * cols bytes)."""
+    n = rows * cols
+    if n == 0:
+        return True
+    try:
+        with open(path, "rb", buffering=0) as f:
+            f.seek(off)
+            mv = memoryview(out)[:n]
+            got = 0
+            while got < n:
+                k = f.readinto(mv[got:])
+                if not k:
+                    return False
+                got += k
+    except OSError:
+        return False
+    return True
+
+
+def load_input_image_u8(path: Path) -> np.ndarray:
+    """The reference's _load_input_image_u8 (gen_fixed_output.py:25-31): np.load, 2-D check, astype."""
+    x = np.load(path)
+    if x.ndim != 2:
+        raise ValueError(f"{path.name}: expected 2D array, got shape={x.shape}")
+    return x if x.dtype == np.uint8 else x.astype(np.uint8)
+
+
+class OrderedSaver:
+    """np.save of a stage's outputs on a thread pool, committed in the stage's order.
+
+    submit(i, path, y) starts writing y (which must stay untouched until commit) to a temporary
+    file beside ``path``; commit() renames them into place in index order.  The first item whose
+    write failed, or whose existing target the reference's open(path, "wb") would refuse, is
+    redone as np.save(path, y) -- the reference's own call, which raises its error -- and every
+    later temporary file is removed, so the directory holds what the reference's sequential loop
+    would have left."""
+
+    def __init__(self, workers: int = SAVE_WORKERS):
+        self.pool = ThreadPoolExecutor(max_workers=workers)
+        self.items: dict[int, tuple] = {}
+        self.write_s = 0.0
+        self._mu = threading.Lock()
+
+    def _write(self, tmp: Path, y: np.ndarray) -> None:
+        t0 = time.perf_counter()
+        with open(tmp, "wb") as f:
+            np.save(f, y)
+        with self._mu:
+            self.write_s += time.perf_counter() - t0
+
+    def submit(self, index: int, path: Path, y: np.ndarray) -> None:
+        tmp = path.with_name(f".{path.name}.{os.getpid()}.{threading.get_ident()}.{index}.part")
+        self.items[index] = (path, y, tmp, self.pool.submit(self._write, tmp, y))
+
+    def commit(self) -> int:
+        """Rename every submitted file into place in index order; returns how many were written.
+        Raises the first failing item's error (the reference's np.save), after the items before it."""
+        done = 0
+        try:
+            for i in sorted(self.items):
+                path, y, tmp, fut = self.items[i]
+                ok = fut.exception() is None
+                if ok and path.exists():
+                    try:  # the access check open(path, "wb") makes, without truncating the file
+                        os.close(os.open(path, os.O_WRONLY))
+                    except OSError:
+                        ok = False
+                if ok:
+                    os.replace(tmp, path)
+                else:
+                    np.save(path, y)  # the reference's call: raises its error (or writes the file)
+                done += 1
+        finally:
+            self.discard()  # the temporary files of the items after a failure
+        return done
+
+    def discard(self) -> None:
+        """Drop every uncommitted item (a device error ended the stage): wait, remove its file."""
+        for path, y, tmp, fut in self.items.values():
+            fut.exception()
+            try:
+                tmp.unlink()
+            except FileNotFoundError:
+                pass
+        self.items.clear()
+
+    def close(self) -> None:
+        self.discard()
+        self.pool.shutdown(wait=True)
+
+
+class PlannedImage:
+    """One input of a stage: its file, shape (known from the header, or from np.load), the array
+    when np.load had to read it, and its pending outputs [(order, out_path, key)]."""
+
+    def __init__(self, path: Path, stem: str):
+        self.path, self.stem = path, stem
+        self.shape = None
+        self.off = None
+        self.array = None
+        self.items: list = []
+
+
+def run_image_stage(inputs: list[Path], stem_of, plan_items, compute, out_dtype, timings: dict | None = None) -> int:
+    """Run one pipeline stage over ``inputs`` (the sorted input files) as device calls.
+
+    stem_of(path) -> case stem.  plan_items(stem, shape) -> (items, error): the pending outputs
+    [(out_path, key)] of an image in the reference's order -- keys name coefficient sets, every
+    key of a non-empty image already validated -- and the exception that stops the stage at that
+    point (None).  compute(xs, keys, outs, ready, timing): the device work for non-empty images
+    ``xs`` under the coefficient sets ``keys``, into outs[i][j]; ready(i, j) once a plane is in
+    host memory.  Returns the number of files written; raises the stage's first error after
+    writing everything before it.  ``timings`` receives the stage's breakdown (ms)."""
+    t_start = time.perf_counter()
+    tm = {"plan_ms": 0.0, "load_ms": 0.0, "h2d_ms": 0.0, "kernel_ms": 0.0, "d2h_ms": 0.0, "call_ms": 0.0,
+          "save_write_ms": 0.0, "save_tail_ms": 0.0, "device_calls": 0, "files": 0}
+    # ---- plan: the reference's order of loads, skips, checks -----------------------------
+    planned: list[PlannedImage] = []
+    error = None
+    order = 0
+    for path in inputs:
+        im = PlannedImage(path, stem_of(path))
+        hdr = npy_u8_2d_shape(path)
+        if hdr is not None:
+            im.shape, im.off = (hdr[0], hdr[1]), hdr[2]
+        else:
+            try:
+                im.array = load_input_image_u8(path)
+            except Exception as exc:  # noqa: BLE001 - the stage stops here, as the reference's loop
+                error = exc
+                break
+            im.shape = im.array.shape
+        items, err = plan_items(im.stem, im.shape)
+        for out_path, key in items:
+            im.items.append((order, out_path, key))
+            order += 1
+        planned.append(im)
+        if err is not None:
+            error = err
+            break
+    tm["plan_ms"] = (time.perf_counter() - t_start) * 1e3
+    saver = OrderedSaver()
+    written = 0
+    try:
+        i0 = 0
+        while i0 < len(planned):
+            # one device call's window of images: image-aligned, <= BATCH_BYTES of staging
+            i1, nbytes = i0, 0
+            while i1 < len(planned):
+                im = planned[i1]
+                keys = {k for _, _, k in im.items}
+                b = _align(im.shape[0] * im.shape[1]) * (1 + 8 * len(keys))
+                if i1 > i0 and nbytes + b > BATCH_BYTES:
+                    break
+                nbytes += b
+                i1 += 1
+            window = planned[i0:i1]
+            stop = _run_window(window, compute, out_dtype, saver, tm)
+            written += saver.commit()
+            if stop is not None:  # an input np.load refuses, found at its turn
+                error = stop
+                break
+            i0 = i1
+    finally:
+        saver.close()
+        tm["files"] = written
+        tm["save_write_ms"] = saver.write_s * 1e3
+        tm["wall_ms"] = (time.perf_counter() - t_start) * 1e3
+        if timings is not None:
+            timings.update({k: round(v, 3) if isinstance(v, float) else v for k, v in tm.items()})
+    if error is not None:
+        raise error
+    return written
+
+
+def _run_window(window: list, compute, out_dtype, saver: OrderedSaver, tm: dict):
+    """Load, compute and submit one window of planned images; returns the load error that cuts
+    the window short (the images before it are still computed and saved), else None."""
+    ar = arena()
+    t0 = time.perf_counter()
+    fast = [im for im in window if im.array is None]
+    in_buf = ar.take("in", sum(_align(im.shape[0] * im.shape[1]) for im in fast))
+    off, stop, cut = 0, None, len(window)
+    xs_all = []
+    for k, im in enumerate(window):
+        if im.array is not None:
+            xs_all.append(im.array)
+            continue
+        n = im.shape[0] * im.shape[1]
+        view = in_buf[off:off + n].reshape(im.shape)
+        off += _align(n)
+        if not read_u8_2d_into(im.path, im.shape[0], im.shape[1], im.off, view):
+            try:  # the header looked fine but the data did not come: np.load judges the file
+                view = load_input_image_u8(im.path)
+            except Exception as exc:  # noqa: BLE001
+                stop, cut = exc, k
+                break
+        xs_all.append(view)
+    tm["load_ms"] += (time.perf_counter() - t0) * 1e3
+    window, xs_all = window[:cut], xs_all[:cut]
+    gpu = [(im, x) for im, x in zip(window, xs_all) if im.items and x.size]
+    for im, x in zip(window, xs_all):  # empty images: the reference writes empty arrays, no compute
+        if im.items and not x.size:
+            for order, out_path, _ in im.items:
+                saver.submit(order, out_path, np.zeros(x.shape, dtype=out_dtype))
+    # the coefficient sets the device call needs, in first-use order (the reference's bank order)
+    keys: list = []
+    for im, _ in gpu:
+        for _, _, k in im.items:
+            if k not in keys:
+                keys.append(k)
+    if not gpu or not keys:
+        return stop
+    isz = np.dtype(out_dtype).itemsize
+    out_buf = ar.take("out", sum(_align(x.size * isz) * len(keys) for _, x in gpu))
+    outs, off = [], 0
+    for _, x in gpu:
+        planes = []
+        for _ in keys:
+            planes.append(out_buf[off:off + x.size * isz].view(out_dtype).reshape(x.shape))
+            off += _align(x.size * isz)
+        outs.append(planes)
+    where = [{k: (order, out_path) for order, out_path, k in im.items} for im, _ in gpu]
+
+    def ready(i, j):
+        hit = where[i].get(keys[j])
+        if hit is not None:
+            saver.submit(hit[0], hit[1], outs[i][j])
+
+    timing: dict = {}
+    compute([x for _, x in gpu], keys, outs, ready, timing)
+    for k in ("h2d_ms", "kernel_ms", "d2h_ms", "call_ms"):
+        tm[k] += timing.get(k, 0.0)
+    tm["device_calls"] += timing.get("calls", 1)
+    t1 = time.perf_counter()
+    for *_, fut in saver.items.values():
+        fut.exception()
+    tm["save_tail_ms"] += (time.perf_counter() - t1) * 1e3
+    return stop

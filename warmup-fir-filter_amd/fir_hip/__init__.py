@@ -7,7 +7,8 @@ CPU fallback: the product path fails loudly rather than computing elsewhere.
 
 Host-array entry points (NumPy in, NumPy out, synchronous):
     fir1d_fixed_rows, fir1d_fixed_rows_multi, fir1d_fixed_rows_sharded, fir2d_fixed,
-    fir1d_ideal_rows, compare_metrics, restore_u8
+    fir1d_ideal_rows, compare_metrics, restore_u8, and the stage drivers' image batches
+    fir1d_fixed_images_multi / fir1d_ideal_images_multi (page-locked staging: host_empty)
 Device entry points (torch tensors on a HIP device, enqueued on the current stream):
     see :mod:`fir_hip.torch_ops`.
 """
@@ -25,7 +26,8 @@ __all__ = [
     "fir1d_fixed_rows_sharded", "fir2d_fixed", "fir1d_ideal_rows", "compare_metrics", "restore_u8", "IN_U8", "IN_I16",
     "OUT_U8_SAT", "OUT_I32", "RESTORE_CLIP", "RESTORE_NORMALIZE", "MAX_TAPS", "EXPORTS", "ipc_export", "ipc_import",
     "ipc_close", "peek", "IPC_HANDLE_BYTES", "device_bus_id", "peer_access", "peer_atomics", "halo_mailbox_bytes",
-    "GATE_TIMEOUT", "GATE_LAYOUT", "build_id", "parse_devices", "METRIC_DTYPES",
+    "GATE_TIMEOUT", "GATE_LAYOUT", "build_id", "parse_devices", "METRIC_DTYPES", "fir1d_fixed_images_multi",
+    "fir1d_ideal_images_multi", "host_empty", "TIMING_KEYS",
 ]
 
 IN_U8, IN_I16 = 0, 1
@@ -33,7 +35,7 @@ OUT_U8_SAT, OUT_I32 = 0, 1
 RESTORE_CLIP, RESTORE_NORMALIZE = 0, 1
 MAX_TAPS = 1 << 30  # FIR_MAX_TAPS: any practical length (the reference has no limit)
 IPC_HANDLE_BYTES = 64
-ABI_VERSION = 5
+ABI_VERSION = 6
 GATE_TIMEOUT = 1  # FIR_GATE_TIMEOUT
 GATE_LAYOUT = 2  # FIR_GATE_LAYOUT
 
@@ -62,6 +64,11 @@ EXPORTS = {
     "fir1d_fixed_rows_multi_dev": (_i32, [_vp, _i32, _i64, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
     "fir1d_fixed_images_multi_dev": (_i32, [_i32, _vp, _vp, _vp, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp,
                                             _vp]),
+    "fir1d_fixed_images_multi": (_i32, [_i32, _vp, _vp, _vp, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32,
+                                        _vp, _vp, _vp]),
+    "fir1d_ideal_images_multi": (_i32, [_i32, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _i32, _vp, _vp, _vp]),
+    "fir_host_alloc": (_i32, [_i64, ctypes.POINTER(_vp)]),
+    "fir_host_free": (_i32, [_vp]),
     "fir1d_fixed_edges_dev": (_i32, [_vp, _i32, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "fir1d_fixed_segment_dev": (_i32, [_vp, _i32, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "fir2d_fixed": (_i32, [_vp, _i64, _i64, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32]),
@@ -416,6 +423,135 @@ def fir1d_fixed_rows_multi(x: np.ndarray, hq2, frac_bits: int = 12, acc_bits: in
                                         int(frac_bits), int(acc_bits), int(out_stage), _ptr(y), int(device)),
            "fir1d_fixed_rows_multi")
     return y
+
+
+# ---- host image batches (the stage drivers' entries, fir_hip.h ABI 6) -------------------
+_PLANE_READY = ctypes.CFUNCTYPE(None, _vp, ctypes.c_int)  # fir_plane_ready_fn
+TIMING_KEYS = ("h2d_ms", "kernel_ms", "d2h_ms", "call_ms")  # FIR_TIMING_SLOTS, in order
+
+
+class _Pinned:
+    """One fir_host_alloc block; freed when the last array over it is gone."""
+
+    def __init__(self, nbytes: int):
+        p = _vp(0)
+        _check(lib().fir_host_alloc(int(nbytes), ctypes.byref(p)), "fir_host_alloc")
+        self.ptr, self.nbytes = p.value, int(nbytes)
+
+    def __del__(self):
+        if getattr(self, "ptr", None) and _lib is not None:
+            _lib.fir_host_free(_vp(self.ptr))
+            self.ptr = None
+
+
+def host_empty(nbytes: int) -> np.ndarray:
+    """A uint8 array of ``nbytes`` in page-locked host memory (fir_host_alloc): the copies of the
+    image-batch entries run as DMA straight from / into it.  The block is released when the array
+    (and every view of it) is garbage."""
+    if nbytes <= 0:
+        return np.empty(0, dtype=np.uint8)
+    owner = _Pinned(nbytes)
+    raw = (ctypes.c_uint8 * owner.nbytes).from_address(owner.ptr)
+    raw._owner = owner  # the ctypes array keeps the block alive; NumPy's base chain keeps the array
+    return np.frombuffer(raw, dtype=np.uint8)
+
+
+def _host_planes(xs: list, nf: int, dtype, outs):
+    """The output planes of an image batch: the caller's ``outs`` (per image, F arrays shaped like
+    the image, C-contiguous, writeable, of ``dtype``) or fresh arrays."""
+    if outs is None:
+        return [[np.empty(x.shape, dtype=dtype) for _ in range(nf)] for x in xs]
+    outs = [list(o) for o in outs]
+    if len(outs) != len(xs):
+        raise FirHipError("outs must hold one entry per image")
+    for i, (x, ps) in enumerate(zip(xs, outs)):
+        if len(ps) != nf:
+            raise FirHipError(f"outs[{i}] must hold {nf} planes")
+        for f, p in enumerate(ps):
+            if not isinstance(p, np.ndarray) or p.dtype != np.dtype(dtype) or p.shape != x.shape:
+                raise FirHipError(f"outs[{i}][{f}] must be a {np.dtype(dtype)} array of shape {x.shape}")
+            if not p.flags.c_contiguous or not p.flags.writeable:
+                raise FirHipError(f"outs[{i}][{f}] must be C-contiguous and writeable")
+    return outs
+
+
+def _run_images(fn, what: str, args_head: list, planes: list, device: int, ready, timing):
+    """Call an image-batch entry: planes flattened image-major, ``ready(i, f)`` per landed plane
+    (exceptions it raises are re-raised after the call), ``timing`` (dict) filled from the
+    entry's FIR_TIMING_SLOTS."""
+    nf = len(planes[0]) if planes else 1
+    flat = [p for ps in planes for p in ps]
+    yp = (_vp * max(1, len(flat)))(*[p.ctypes.data for p in flat])
+    errors = []
+
+    def on_ready(_ctx, p):
+        try:
+            ready(p // nf, p % nf)
+        except BaseException as exc:  # noqa: BLE001 - re-raised after the C call returns
+            errors.append(exc)
+
+    cb = _PLANE_READY(on_ready) if ready is not None else None
+    t = (ctypes.c_double * 4)() if timing is not None else None
+    _check(fn(*args_head, yp, int(device), ctypes.cast(cb, _vp) if cb is not None else None, None, t), what)
+    if timing is not None:
+        timing.update({k: float(v) for k, v in zip(TIMING_KEYS, t)})
+    if errors:
+        raise errors[0]
+    return planes
+
+
+def _image_geometry(xs: list, dtype_ok) -> tuple:
+    xs = [np.ascontiguousarray(x) for x in xs]
+    for i, x in enumerate(xs):
+        if x.ndim != 2:
+            raise FirHipError(f"xs[{i}] must be a 2-D (rows, width) image, got shape {x.shape}")
+        if not dtype_ok(x.dtype):
+            raise FirHipError(f"xs[{i}] has dtype {x.dtype}")
+    n = len(xs)
+    ptrs = (_vp * max(1, n))(*[x.ctypes.data for x in xs])
+    rows = (_i64 * max(1, n))(*[x.shape[0] for x in xs])
+    return xs, ptrs, rows
+
+
+def fir1d_fixed_images_multi(xs, hq2, frac_bits: int = 12, acc_bits: int = 32, out_stage: int = OUT_U8_SAT,
+                             channels: int = 1, device: int = 0, outs=None, ready=None, timing: dict | None = None):
+    """The F filters (rows of hq2) over every 2-D image of ``xs`` (all uint8 or all int16; row =
+    width*channels interleaved samples) in one device call: the images uploaded once, one batch
+    launch, each plane downloaded into ``outs[i][f]`` (fresh arrays when None; page-locked ones from
+    host_empty make every copy a DMA).  ``ready(i, f)`` runs on this thread as soon as plane (i, f)
+    is in host memory, while later planes are still in flight.  Returns outs.  Replaces the loop
+    over images x coefficient sets of fir_1d/sim/vector/gen_fixed_output.py:88-107 (reference root)."""
+    xs = list(xs)
+    dt = xs[0].dtype if xs else np.dtype(np.uint8)
+    xs, ptrs, rows = _image_geometry(xs, lambda d: d == dt and d in (np.uint8, np.int16))
+    h2 = np.asarray(hq2, dtype=np.int64)
+    if h2.ndim != 2 or h2.shape[0] < 1:
+        raise FirHipError("hq2 must be a non-empty (filters, taps) array")
+    nf, L = h2.shape
+    h = np.concatenate([_taps_i32(row) for row in h2])
+    for i, x in enumerate(xs):
+        if x.shape[1] % channels:
+            raise FirHipError(f"xs[{i}]: row length must be a multiple of channels")
+    widths = (_i64 * max(1, len(xs)))(*[x.shape[1] // channels for x in xs])
+    planes = _host_planes(xs, nf, np.uint8 if out_stage == OUT_U8_SAT else np.int32, outs)
+    head = [len(xs), ptrs, rows, widths, IN_U8 if dt == np.uint8 else IN_I16, int(channels), _ptr(h), L, nf,
+            int(frac_bits), int(acc_bits), int(out_stage)]
+    return _run_images(lib().fir1d_fixed_images_multi, "fir1d_fixed_images_multi", head, planes, device, ready, timing)
+
+
+def fir1d_ideal_images_multi(xs, hs, device: int = 0, outs=None, ready=None, timing: dict | None = None):
+    """The float64 ideal model with each coefficient set of ``hs`` (F x taps floats) over every 2-D
+    uint8 image of ``xs``, one upload per image for all F sets; planes, ``ready`` and ``timing`` as
+    fir1d_fixed_images_multi.  Replaces the loop of fir_1d/sim/vector/gen_ideal_output.py:75-86."""
+    xs, ptrs, rows = _image_geometry(list(xs), lambda d: d == np.uint8)
+    h2 = np.ascontiguousarray(np.asarray(hs, dtype=np.float64))
+    if h2.ndim != 2 or h2.shape[0] < 1 or h2.shape[1] < 1 or h2.shape[1] > MAX_TAPS:
+        raise FirHipError(f"hs must be a (filters, taps) array with 1 <= taps <= {MAX_TAPS}")
+    nf, L = h2.shape
+    widths = (_i64 * max(1, len(xs)))(*[x.shape[1] for x in xs])
+    planes = _host_planes(xs, nf, np.float64, outs)
+    head = [len(xs), ptrs, rows, widths, _ptr(h2), L, nf]
+    return _run_images(lib().fir1d_ideal_images_multi, "fir1d_ideal_images_multi", head, planes, device, ready, timing)
 
 
 def fir2d_fixed(x: np.ndarray, hq2, frac_bits: int = 12, acc_bits: int = 32, out_stage: int = OUT_U8_SAT,

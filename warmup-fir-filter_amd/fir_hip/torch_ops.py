@@ -122,6 +122,8 @@ class ImagesMultiPlan:
                 raise FirHipError(f"xs[{i}]: every image must be uint8, or every image int16")
             if x.device != xs[0].device:
                 raise FirHipError(f"xs[{i}]: every image must be on {xs[0].device} (one launch, one device)")
+            if (x.shape[-1] if x.dim() else 1) % channels:
+                raise FirHipError(f"xs[{i}]: row length must be a multiple of channels")
             if isinstance(o, torch.Tensor):
                 _check_dev(o, f"outs[{i}]")
                 ps = [o[f] for f in range(o.shape[0])] if o.dim() else []
