@@ -132,9 +132,10 @@ int fir1d_fixed_images_multi_dev(int n_images, const void* const* x_devs, const 
  * images, its kernels, and one download per plane.  fir1d_fixed_images_multi runs
  * fir1d_fixed_images_multi_dev's launches (same layout of xs / rows / widths / y_planes, host
  * pointers) on `device`: the images are copied to the device back to back (256-byte aligned), the
- * planes come back one D2H copy each, in y_planes order, and `ready(ready_ctx, p)` (optional) is
- * called on the calling thread as soon as plane p is in host memory -- while the later planes are
- * still being copied -- so the caller can write it out under the remaining copies.  `ready` must
+ * planes come back one D2H copy each, largest first (ties in y_planes order), and
+ * `ready(ready_ctx, p)` (optional) is called once per plane p, on the calling thread, as soon as it
+ * is in host memory -- while the later planes are still being copied -- so the caller can write it
+ * out under the remaining copies (the largest writes start first).  `ready` must
  * not call this library for the same device.  Synchronous: every plane is in host memory when
  * the entry returns.  With host buffers from fir_host_alloc (page-locked) every copy is a DMA at
  * the PCIe rate; pageable buffers also work (staged by the runtime).  timing_ms (optional, NULL

@@ -20,6 +20,7 @@ for p in (ROOT, ROOT / "warmup-fir-filter_amd"):
         sys.path.insert(0, str(p))
 
 GOLDEN = ROOT / "tests" / "golden"
+IMAGES = ROOT / "warmup-fir-filter_amd" / "fir_1d" / "sim" / "img_u8.npz"  # decoded golden inputs (package data)
 
 
 def pytest_configure(config):
@@ -63,7 +64,7 @@ def iter_ragged(name: str):
 
 
 def load_images() -> dict[str, np.ndarray]:
-    d = np.load(GOLDEN / "images_u8.npz")
+    d = np.load(IMAGES)
     return {k: d[k] for k in d.files}
 
 

@@ -19,7 +19,8 @@ Reference entry points exercised (paths relative to the reference root):
 Files written:
   kat_fixed.json, kat_ideal.json     known-answer + error cases (reference tests' vectors)
   random_fixed.npz, random_ideal.npz randomized (x, h, frac, acc, coeff) sweeps
-  images_u8.npz                      the 7 decoded golden input images (u8, H x W)
+  ../../warmup-fir-filter_amd/fir_1d/sim/img_u8.npz
+                                     the 7 decoded golden input images (u8, H x W)
   image_outputs.json                 sha256 of all 56 fixed + 56 ideal outputs + report metrics
   small_image_outputs.npz            full fixed/ideal outputs of the two 64x64 cases
   restore_u8.npz                     restore conversions (clip / normalize) of the 16 small
@@ -54,6 +55,8 @@ import numpy as np
 
 REF = Path(os.environ.get("FIR_REFERENCE", "/root/reference"))
 OUT = Path(__file__).resolve().parent
+# the decoded golden inputs live with the package (the pipeline CLI's default image source)
+IMAGES = OUT.parents[1] / "warmup-fir-filter_amd" / "fir_1d" / "sim" / "img_u8.npz"
 
 
 def _ref_imports():
@@ -269,7 +272,7 @@ def _sha(a: np.ndarray) -> str:
 def _image_job(args):
     stem, tap, name, h = args
     fixed_ref, ideal_ref, gfo, gio, _, rep, _ = _ref_imports()
-    x = np.load(OUT / "images_u8.npz")[stem]
+    x = np.load(IMAGES)[stem]
     yf = gfo._run_fixed_rowwise(x, h, frac_bits=12, acc_bits=32, coeff_bits=16)
     yi = gio._run_ideal_rowwise(x, h)
     metrics = rep._compute_metrics(yi, yf)
@@ -283,7 +286,7 @@ def gen_images(jobs):
     imgs = {}
     for idx, p in enumerate(files):
         imgs[f"case_{idx:03d}_{p.stem}"] = giv._load_image_gray_u8(p)
-    np.savez_compressed(OUT / "images_u8.npz", **imgs)
+    np.savez_compressed(IMAGES, **imgs)
     inputs = {k: {"shape": list(v.shape), "sha256": _sha(v)} for k, v in imgs.items()}
 
     work = []

@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 import fir_hip
-from conftest import GOLDEN
+from conftest import GOLDEN, IMAGES
 from oracle import c_oracle, fir_oracle as fo
 from pipeline_fir_1d import run_pipeline
 
@@ -114,8 +114,7 @@ def test_pipeline_end_to_end_on_golden_images(tmp_path, image_outputs):
     res = run_pipeline(tap="all", overwrite_vectors=False, skip_input=False, skip_ideal=False, skip_fixed=False,
                        skip_report=False, skip_restore=True, restore_kind="all", ideal_policy="clip",
                        overwrite_images=False, strict_report=True, strict_restore=False, top_k=5,
-                       image_dir=GOLDEN / "images_u8.npz", vector_dir=tmp_path / "vector",
-                       image_out_dir=tmp_path / "img")
+                       vector_dir=tmp_path / "vector", image_out_dir=tmp_path / "img")  # default image source
     assert res["ideal_counts"] == {"ideal_3tap": 28, "ideal_5tap": 28}
     assert res["fixed_counts"] == {"fixed_3tap": 28, "fixed_5tap": 28}
     out = tmp_path / "vector" / "output"
@@ -140,7 +139,7 @@ def test_pipeline_end_to_end_on_golden_images(tmp_path, image_outputs):
     res2 = run_pipeline(tap="3", overwrite_vectors=False, skip_input=False, skip_ideal=False, skip_fixed=False,
                         skip_report=True, skip_restore=True, restore_kind="all", ideal_policy="clip",
                         overwrite_images=False, strict_report=False, strict_restore=False, top_k=5,
-                        image_dir=GOLDEN / "images_u8.npz", vector_dir=tmp_path / "vector",
+                        image_dir=IMAGES, vector_dir=tmp_path / "vector",
                         image_out_dir=tmp_path / "img")
     assert res2["ideal_counts"] == {"ideal_3tap": 0} and res2["fixed_counts"] == {"fixed_3tap": 0}
     assert res2["input_manifest"]["skipped_cases"] == 7
@@ -153,7 +152,7 @@ def test_pipeline_devices_reproduces_all_112_outputs(tmp_path, image_outputs):
     res = run_pipeline(tap="all", overwrite_vectors=False, skip_input=False, skip_ideal=False, skip_fixed=False,
                        skip_report=True, skip_restore=True, restore_kind="all", ideal_policy="clip",
                        overwrite_images=False, strict_report=False, strict_restore=False, top_k=5,
-                       image_dir=GOLDEN / "images_u8.npz", vector_dir=tmp_path / "vector",
+                       image_dir=IMAGES, vector_dir=tmp_path / "vector",
                        image_out_dir=tmp_path / "img", devices=[0, 0, 0])
     assert res["ideal_counts"] == {"ideal_3tap": 28, "ideal_5tap": 28}
     assert res["fixed_counts"] == {"fixed_3tap": 28, "fixed_5tap": 28}

@@ -73,7 +73,9 @@ def test_fixed_images_multi_host_entry_vs_oracle(pinned):
     seen = []
     got = fir_hip.fir1d_fixed_images_multi(xs, bank, 12, 32, fir_hip.OUT_U8_SAT, outs=outs,
                                            ready=lambda i, f: seen.append((i, f)))
-    assert seen == [(i, f) for i in range(len(xs)) for f in range(len(bank))]
+    sizes = [xs[i].size for i, _ in seen]
+    assert sorted(seen) == [(i, f) for i in range(len(xs)) for f in range(len(bank))]  # each plane once
+    assert sizes == sorted(sizes, reverse=True)  # largest planes first
     for x, planes in zip(xs, got):
         for h, y in zip(bank, planes):
             ref = co.fir1d_rows(x, h, 12, 32, co.OUT_U8_SAT) if x.size else np.zeros(x.shape, np.uint8)

@@ -147,3 +147,20 @@ def test_rows_over_devices_blocks_cover_every_row_once():
             seen = []
             _over_devices(nrows, devs, lambda r0, r1, d: seen.extend(range(r0, r1)))
             assert sorted(seen) == list(range(nrows)), (nrows, devs)
+
+
+def test_pipeline_default_image_source_is_package_data(image_outputs):
+    """The CLI's default inputs (pipeline_fir_1d.default_image_source) are the package's own decoded
+    copy of the reference images, not a test fixture; every image has the reference decode's
+    SHA-256."""
+    import hashlib
+    from pathlib import Path
+
+    import pipeline_fir_1d
+
+    src = pipeline_fir_1d.default_image_source()
+    pkg = Path(pipeline_fir_1d.__file__).resolve().parent
+    assert src.is_relative_to(pkg) and "tests" not in src.relative_to(pkg).parts
+    with np.load(src) as d:
+        got = {k: hashlib.sha256(np.ascontiguousarray(d[k]).tobytes()).hexdigest() for k in d.files}
+    assert got == {k: v["sha256"] for k, v in image_outputs["inputs"].items()}

@@ -37,7 +37,7 @@ def main():
     t = best(lambda: fir_hip.fir1d_fixed_rows(x, [-256, -1024, 6656, -1024, -256], 12, 32, fir_hip.OUT_I32))
     out["fir1d_fixed_rows int16->int32 2^28 (512 MiB in, 1 GiB out)"] = {
         "seconds": round(t, 4), "gsamples_per_s": round(x.size / t / 1e9, 3), "pcie_gb_per_s": round(6 * x.size / t / 1e9, 2)}
-    imgs = np.load(ROOT / "tests" / "golden" / "images_u8.npz")
+    imgs = np.load(ROOT / "warmup-fir-filter_amd" / "fir_1d" / "sim" / "img_u8.npz")
     ims = [imgs[k] for k in sorted(imgs.files)]
     n = sum(a.size for a in ims)
     hq = [-256, -1024, 6656, -1024, -256]

@@ -45,7 +45,7 @@ def main():
         vec = Path(tmp) / "vector"
         inp, out = vec / "input", vec / "output"
         res = {}
-        _, res["input_vectors_s"] = timed(generate_input_vector_jsons, ROOT / "tests" / "golden" / "images_u8.npz", inp,
+        _, res["input_vectors_s"] = timed(generate_input_vector_jsons, ROOT / "warmup-fir-filter_amd" / "fir_1d" / "sim" / "img_u8.npz", inp,
                                           overwrite=True)
         for tap, ideal, fixed, report in (("3tap", generate_ideal_3tap_output_vector, generate_fixed_3tap_output_vector,
                                            generate_3tap_compare_report),

@@ -35,7 +35,7 @@ def per_call_us(fn, reps):
 
 
 def main():
-    img = np.load(ROOT / "tests" / "golden" / "images_u8.npz")["case_005_img_006_4499x2999_gray"]
+    img = np.load(ROOT / "warmup-fir-filter_amd" / "fir_1d" / "sim" / "img_u8.npz")["case_005_img_006_4499x2999_gray"]
     row = np.ascontiguousarray(img[1500])
     row_list = row.tolist()
     hq = np.array([-256, -1024, 6656, -1024, -256], np.int32)

@@ -357,8 +357,8 @@ bool mul_ok(int64_t a, int64_t b, int64_t* out) {
 // whole set of images goes to the device in one run of H2D copies (each image on a 256-byte
 // boundary of the device input buffer), `launch(dx, dy, stream, err)` runs every kernel of the
 // stage on those copies (output plane p on a 256-byte boundary of the device output buffer:
-// planes start on whole cache lines), then each plane comes back by its own D2H copy, in plane
-// order, with an event behind it.  `ready(ctx, p)` is called on this thread as soon as plane p is
+// planes start on whole cache lines), then each plane comes back by its own D2H copy, largest
+// first, with an event behind it.  `ready(ctx, p)` is called on this thread as soon as plane p is
 // in host memory, while the later planes are still in flight, so the caller can write plane p out
 // (np.save) under the remaining copies; with pinned host buffers (fir_host_alloc) every copy is a
 // DMA that needs no host thread.  timing_ms (optional): FIR_TIMING_SLOTS values, see fir_hip.h.
@@ -415,16 +415,22 @@ int run_host_images(int device, int n, const void* const* xs, const std::vector<
     if ((rc = launch(dx.data(), dy.data(), s, &err))) return bail(rc, err);
     if (timing_ms && (e = hipEventRecord(st->tev[2], s)) != hipSuccess)
         return bail(FIR_EHIP, std::string("hipEventRecord: ") + hipGetErrorString(e));
-    for (int p = 0; p < np && e == hipSuccess; ++p) {
+    // largest planes first: their writes (the caller's longest) start earliest, under the copies
+    // of the small ones
+    std::vector<int> order(np);
+    for (int p = 0; p < np; ++p) order[p] = p;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return out_bytes[a] > out_bytes[b]; });
+    for (int k = 0; k < np && e == hipSuccess; ++k) {
+        const int p = order[k];
         if (out_bytes[p]) e = hipMemcpyAsync(ys[p], dy[p], out_bytes[p], hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipEventRecord(st->plane_ev[p], s);
+        if (e == hipSuccess) e = hipEventRecord(st->plane_ev[k], s);
     }
     if (e == hipSuccess && timing_ms) e = hipEventRecord(st->tev[3], s);
     if (e != hipSuccess) return bail(FIR_EHIP, std::string("plane download: ") + hipGetErrorString(e));
-    for (int p = 0; p < np && ready; ++p) {
-        if ((e = hipEventSynchronize(st->plane_ev[p])) != hipSuccess)
+    for (int k = 0; k < np && ready; ++k) {
+        if ((e = hipEventSynchronize(st->plane_ev[k])) != hipSuccess)
             return bail(FIR_EHIP, std::string("plane download: ") + hipGetErrorString(e));
-        ready(ctx, p);
+        ready(ctx, order[k]);
     }
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return fail(FIR_EHIP, std::string("image batch: ") + hipGetErrorString(e));
     if (timing_ms) {

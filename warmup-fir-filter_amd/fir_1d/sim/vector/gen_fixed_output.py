@@ -190,7 +190,7 @@ def _save_all(items) -> int:
     """np.save of a group's outputs (stage_io.OrderedSaver): written concurrently, put in place in
     group order; the first failure is raised after the files before it, and none after it exists,
     as the reference's one-file-at-a-time loop (gen_fixed_output.py:92-105) leaves them."""
-    saver = stage_io.OrderedSaver(workers=max(1, min(len(items), stage_io.SAVE_WORKERS)))
+    saver = stage_io.OrderedSaver(workers=max(1, min(len(items), stage_io.save_workers())))
     try:
         for i, (path, y) in enumerate(items):
             saver.submit(i, path, y)

@@ -5,7 +5,7 @@ preview / manifest fields, skip-if-exists).  Image decoding is host I/O and out 
 path's scope; it uses Pillow like the reference (``convert("L")``, :19-33).  Two
 differences: the output directory is created before the first ``np.save`` (the reference
 saves first and fails on a fresh checkout, :130 vs :42), and ``image_dir`` may also be an
-``.npz`` archive of already-decoded uint8 images (``tests/golden/images_u8.npz``), so the
+``.npz`` archive of already-decoded uint8 images (``fir_1d/sim/img_u8.npz``), so the
 pipeline runs without re-decoding JPEGs (libjpeg versions can differ).
 """
 from __future__ import annotations

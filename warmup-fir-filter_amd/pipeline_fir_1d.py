@@ -6,8 +6,10 @@ dict.  Stages 2-4 run on the GPU (ideal and fixed models one launch per image --
 bank fused into one read of each image -- and the report metrics as one reduction per
 case); input decoding and PNG restore stay host I/O.  Extra keyword arguments (``image_dir``,
 ``vector_dir``, ``image_out_dir``) relocate the reference's fixed directories; by default
-the golden inputs come from ``fir_1d/sim/img`` next to this package if present, else from
-the committed decoded images ``tests/golden/images_u8.npz``.
+the golden inputs come from ``fir_1d/sim/img`` next to this package if present (the reference's
+image files, ``pipeline_fir_1d.py:204-205``), else from the package's own decoded copy of them,
+``fir_1d/sim/img_u8.npz`` (the 7 images as the reference's Pillow decode gives them; SHA-256s in
+SURVEY Appendix A).
 
     python warmup-fir-filter_amd/pipeline_fir_1d.py --tap all --overwrite-vectors
 """
@@ -41,7 +43,7 @@ def default_image_source() -> Path:
     img = SIM_DIR / "img"
     if img.exists():
         return img
-    return _HERE.parent / "tests" / "golden" / "images_u8.npz"
+    return SIM_DIR / "img_u8.npz"
 
 
 def _selected_taps(tap: str) -> list[str]:
