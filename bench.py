@@ -156,12 +156,15 @@ def emit_result(line: str) -> None:
 class Workload:
     """One bench workload: host input, device buffers, one step, the oracle check."""
 
-    def __init__(self, name: str, rank: int, world: int, dev: torch.device, log2n: int):
+    def __init__(self, name: str, rank: int, world: int, dev: torch.device, log2n: int, n_total: int | None = None):
+        """n_total (1-D workloads): the signal's total length split over the ranks (strong scaling)
+        instead of 2^log2n samples per rank (weak scaling)."""
         self.name, self.rank, self.world, self.dev = name, rank, world, dev
         self.gen2d = False
         rng = np.random.default_rng(SEED + rank)
         if name == "fir1d_i16":
-            self.n = 1 << log2n
+            lo, hi = sharded.segment_bounds(n_total, world, rank) if n_total else (0, 1 << log2n)
+            self.n = hi - lo
             self.taps = torch_ops.Taps(SHARPEN5)
             self.channels = 1
             self.x_host = rng.integers(-32768, 32768, self.n, dtype=np.int16)
@@ -173,7 +176,8 @@ class Workload:
                            "total_samples": self.n * world, "taps": 5, "frac_bits": 12, "acc_bits": 32,
                            "parallelism": "single GPU"}  # sharded runs: set by the first step
         elif name == "cplx_i16":
-            self.n = 1 << (log2n - 1)  # complex samples
+            lo, hi = sharded.segment_bounds(n_total // 2, world, rank) if n_total else (0, 1 << (log2n - 1))
+            self.n = hi - lo  # complex samples
             self.taps = torch_ops.Taps(SIMPLE_LP3)
             self.channels = 2
             self.x_host = rng.integers(-32768, 32768, 2 * self.n, dtype=np.int16)
@@ -363,7 +367,17 @@ class Workload:
             else:
                 self.halo_kind, self.halo_src = sharded.make_halo_source(self.x, self.taps.n, self.channels,
                                                                          prefer=HALO_PREF)
-            self.config["parallelism"] = (
+            self.describe_parallelism()
+        self._step_sharded()
+
+    def set_halo(self, kind, src) -> None:
+        """Use ``src`` (an XgmiHalo or HaloExchange over this rank's segment) from the next step on."""
+        self.halo_kind, self.halo_src = kind, src
+        self.left = self.right = None
+        self.describe_parallelism()
+
+    def describe_parallelism(self) -> None:
+        self.config["parallelism"] = (
                 f"contiguous shards x{self.world}, " + (
                     "halo handed over through the neighbours' HBM over xGMI, ordered per step: a one-wave gate "
                     "kernel publishes this rank's edge samples with the step's epoch, waits for both neighbours' "
@@ -373,6 +387,8 @@ class Workload:
                         "then one FIR launch reads them") if self.halo_kind == "xgmi"
                     else "halo exchanged by RCCL send/recv every step (ordered by the messages), overlapped with "
                          "the bulk kernel, then an edge kernel"))
+
+    def _step_sharded(self):
         if self.halo_kind == "xgmi" and GATE_MODE == "overlap":  # gate || bulk, then the edge kernel
             self.halo_src.gate_async()
             self.bulk()
@@ -792,6 +808,66 @@ def run_sub_configs(args, dev) -> tuple[dict, bool]:
     return out, all_ok
 
 
+class LegFailed(Exception):
+    """A halo source's leg of an N > 1 run could not produce a number (no xGMI path, a timed-out
+    gate, a parity mismatch); the run goes on with the next source."""
+
+
+def run_halo_legs(kinds, run_one) -> tuple[dict, str | None]:
+    """Each halo source's leg in turn (collective: every rank runs the same legs in the same
+    order).  ``run_one(kind)`` returns the leg's record or raises LegFailed, which is recorded as
+    the leg's ``error`` while the next leg still runs.  Returns (legs, headline kind): the first
+    leg in ``kinds`` order that measured with bit-exact parity, or None."""
+    legs = {}
+    for kind in kinds:
+        try:
+            legs[kind] = run_one(kind)
+        except LegFailed as exc:
+            legs[kind] = {"error": str(exc)}
+    ok = [k for k in kinds if "error" not in legs[k] and legs[k].get("parity") != "MISMATCH"]
+    return legs, (ok[0] if ok else None)
+
+
+def halo_leg(wl: Workload, kind: str, args, world: int, barrier, red_dev, parity_check: bool = True) -> dict:
+    """One N > 1 leg: set up ``kind``'s halo source over the resident segments (xGMI: mapped
+    mailboxes, probed collectively; rccl: the send/recv exchange), time the steps and the dominant
+    kernel, report the hand-off's own cost, check every rank's full output against the oracle,
+    and release the source.  Raises LegFailed when the source cannot run."""
+    if kind == "xgmi":
+        got, src = sharded.make_halo_source(wl.x, wl.taps.n, wl.channels, prefer="xgmi")
+        if got != "xgmi":
+            raise LegFailed(f"xGMI halo path unavailable: {src.fallback_reason}")
+    else:
+        src = sharded.HaloExchange(wl.x, wl.taps.n, wl.channels)
+    wl.set_halo(kind, src)
+    try:
+        barrier()
+        elapsed, t_issue, kern = measure(wl, args.steps, args.warmup, args.roofline_ramp, args.roofline_launches,
+                                         world, barrier, red_dev)
+        kern_ranks = gather_floats(kern, world, red_dev)
+        failed = gate_failures(wl, world, red_dev)
+        if failed:
+            raise LegFailed(f"halo gate timed out (a neighbour's epoch did not arrive within {src.timeout_s} s) on "
+                            f"rank(s) {failed}")
+        halo = halo_report(wl, world, barrier, red_dev)
+        parity = "skipped"
+        if parity_check:
+            ok = wl.matches(wl.oracle(_cpu_threads()))
+            f = torch.tensor([0 if ok else 1], device=red_dev)
+            dist.all_reduce(f, op=dist.ReduceOp.MAX)
+            parity = "bit-exact vs oracle (full output, every rank)" if int(f.item()) == 0 else "MISMATCH"
+        units = gather_floats(float(wl.units), world, red_dev)
+        return {"value": round(sum(units) * args.steps / elapsed / 1e9, 3), "unit": wl.unit,
+                "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+                "kernel_avg_us_ranks": {"max": round(max(kern_ranks) * 1e6, 2), "min": round(min(kern_ranks) * 1e6, 2)},
+                "halo": halo, "parity": parity, "parallelism": wl.config["parallelism"],
+                "_elapsed": elapsed, "_t_issue": t_issue, "_kern": max(kern_ranks)}
+    finally:
+        barrier()  # no rank unmaps or frees while a neighbour may still read its mailbox
+        if isinstance(src, sharded.XgmiHalo):
+            src.close()
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -866,32 +942,69 @@ def main() -> int:
                 dist.barrier()
 
     barrier()  # every rank's segment is resident and its communicator up before the first step
-    elapsed, t_issue, kern_avg_s = measure(wl, args.steps, args.warmup, args.roofline_ramp, args.roofline_launches,
-                                           world, barrier, red_dev)
-    n_roof = max(1, args.roofline_launches)
-    kern_ranks = gather_floats(kern_avg_s, world, red_dev)
-    halo = halo_report(wl, world, barrier, red_dev) if wl.sharded_1d and world > 1 else None
-    failed = gate_failures(wl, world, red_dev) if wl.sharded_1d else []
-    if failed:
-        if rank == 0:
-            timeout = wl.halo_src.timeout_s
-            emit_result(json.dumps({"metric": METRIC, "value": None, "unit": wl.unit, "n_gpus": world,
-                                    "error": f"halo gate timed out (a neighbour's epoch did not arrive within "
-                                             f"{timeout} s) on rank(s) {failed}", "config": wl.config}))
-        print(f"bench.py: halo gate timed out on rank(s) {failed}", file=sys.stderr)
-        if dist.is_initialized():
+    legs = strong = None
+    if wl.sharded_1d and world > 1:
+        # both halo sources, each its own leg with its own numbers (the first real multi-GPU run
+        # then yields a value whichever source works); the headline is the first that worked
+        kinds = ["xgmi", "rccl"] if HALO_PREF == "xgmi" else [HALO_PREF]
+        legs, head = run_halo_legs(kinds, lambda k: halo_leg(wl, k, args, world, barrier, red_dev,
+                                                             not args.no_parity))
+        if head is None:
+            if rank == 0:
+                emit_result(json.dumps({"metric": METRIC, "value": None, "unit": wl.unit, "n_gpus": world,
+                                        "error": "no halo source produced a result",
+                                        "legs": legs, "config": wl.config}))
+            print(f"bench.py: every halo leg failed: {legs}", file=sys.stderr)
             dist.destroy_process_group()
-        return 3
-
-    # parity: full output vs the C oracle (every rank, its own segment with the received halos)
-    parity = "skipped"
-    if not args.no_parity:
-        ok = wl.matches(wl.oracle(_cpu_threads()))
-        if world > 1:
-            f = torch.tensor([0 if ok else 1], device=red_dev)
-            dist.all_reduce(f, op=dist.ReduceOp.MAX)
-            ok = int(f.item()) == 0
-        parity = "bit-exact vs oracle (full output, every rank)" if ok else "MISMATCH"
+            return 3
+        lead = legs[head]
+        elapsed, t_issue, kern_avg_s = lead["_elapsed"], lead["_t_issue"], lead["_kern"]
+        kern_ranks = [lead["kernel_avg_us_ranks"]["max"] / 1e6, lead["kernel_avg_us_ranks"]["min"] / 1e6]
+        halo, parity = lead["halo"], lead["parity"]
+        wl.config["parallelism"] = lead["parallelism"]
+        # strong scaling beside the weak headline: the same total as one GPU's headline (2^log2n
+        # samples) split over the N ranks, through the headline's halo source
+        swl = Workload(args.workload, rank, world, dev, args.log2n, n_total=1 << args.log2n)
+        torch.cuda.synchronize()
+        try:
+            srec = halo_leg(swl, head, args, world, barrier, red_dev, not args.no_parity)
+            spans = gather_floats(float(swl.n), world, red_dev)
+            strong = {"total_samples": 1 << args.log2n, "samples_per_rank": {"max": int(max(spans)),
+                                                                              "min": int(min(spans))},
+                      **{k: v for k, v in srec.items() if not k.startswith("_") and k != "parallelism"},
+                      "scaling": "strong", "halo_source": head}
+        except LegFailed as exc:
+            strong = {"total_samples": 1 << args.log2n, "error": str(exc), "halo_source": head}
+        del swl
+        for rec in legs.values():
+            for k in [k for k in rec if k.startswith("_")]:
+                del rec[k]
+    else:
+        elapsed, t_issue, kern_avg_s = measure(wl, args.steps, args.warmup, args.roofline_ramp,
+                                               args.roofline_launches, world, barrier, red_dev)
+        kern_ranks = gather_floats(kern_avg_s, world, red_dev)
+        halo = None
+        failed = gate_failures(wl, world, red_dev) if wl.sharded_1d else []
+        if failed:
+            if rank == 0:
+                timeout = wl.halo_src.timeout_s
+                emit_result(json.dumps({"metric": METRIC, "value": None, "unit": wl.unit, "n_gpus": world,
+                                        "error": f"halo gate timed out (a neighbour's epoch did not arrive within "
+                                                 f"{timeout} s) on rank(s) {failed}", "config": wl.config}))
+            print(f"bench.py: halo gate timed out on rank(s) {failed}", file=sys.stderr)
+            if dist.is_initialized():
+                dist.destroy_process_group()
+            return 3
+        # parity: full output vs the C oracle (every rank, its own segment with the received halos)
+        parity = "skipped"
+        if not args.no_parity:
+            ok = wl.matches(wl.oracle(_cpu_threads()))
+            if world > 1:
+                f = torch.tensor([0 if ok else 1], device=red_dev)
+                dist.all_reduce(f, op=dist.ReduceOp.MAX)
+                ok = int(f.item()) == 0
+            parity = "bit-exact vs oracle (full output, every rank)" if ok else "MISMATCH"
+    n_roof = max(1, args.roofline_launches)
 
     # CPU legs: rank 0 only, at every N, after the GPU legs (the other ranks wait at the barrier below)
     cpu = cpu_np = cpu_np_mt = cpu_loop = None
@@ -987,6 +1100,9 @@ def main() -> int:
             "scaling number"))
     if halo is not None:
         line["config"] = dict(line["config"], halo=halo)
+    if legs is not None:
+        line["legs"] = legs
+        line["strong_scaling"] = strong
     if wl.sharded_1d and world == 1:
         line["config"] = dict(wl.config, rehearsal=f"FIR_SELF_HALO=1: {wl.halo_kind} halo hand-off with itself every "
                                                     f"step (ring of one), gate mode {GATE_MODE}")
@@ -998,7 +1114,7 @@ def main() -> int:
     if dist.is_initialized():
         torch.cuda.synchronize()
         barrier()  # no rank unmaps or frees its segment while a neighbour may still read it
-        if isinstance(wl.halo_src, sharded.XgmiHalo):
+        if isinstance(wl.halo_src, sharded.XgmiHalo) and legs is None:
             wl.halo_src.close()
         dist.destroy_process_group()
     return 0 if parity != "MISMATCH" and subs_ok else 1

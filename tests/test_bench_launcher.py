@@ -163,3 +163,106 @@ def test_halo_report_and_gate_failures_over_gloo():
         assert info["exchange_us_per_step"]["max"] >= info["exchange_us_per_step"]["min"] > 0
         assert failed == [1]
         assert ranks == [0.5, 1.5]
+
+
+def _legs_worker(rank, world, port, q):
+    """bench.halo_leg / run_halo_legs over gloo with the GPU parts stubbed: the xGMI leg's gate
+    times out on rank 1 (an injected status word), the RCCL leg runs the real send/recv exchange."""
+    import os
+    import sys
+    import types
+
+    sys.path[:0] = [str(ROOT), str(ROOT / "warmup-fir-filter_amd")]
+    import torch
+    import torch.distributed as dist
+
+    import bench as b
+    from fir_hip import sharded
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        class StuckGate(sharded.XgmiHalo):  # mapped and probed fine, but a later gate times out on rank 1
+            def __init__(self):
+                self.status = torch.tensor([1 if rank == 1 else 0], dtype=torch.int32)
+                self.timeout_s = 10.0
+                self.closed = False
+
+            def gate(self, stream=None):
+                pass
+
+            def close(self):
+                self.closed = True
+
+        stuck = StuckGate()
+        real = sharded.make_halo_source
+        sharded.make_halo_source = lambda *a, **k: ("xgmi", stuck) if k.get("prefer") == "xgmi" else real(*a, **k)
+        b.measure = lambda wl, *a, **k: (0.01, 0.001, 1e-4)  # the GPU timing loops
+
+        class WL:  # the fields halo_leg reads
+            x = torch.arange(rank * 100, rank * 100 + 40, dtype=torch.int16)
+            taps = types.SimpleNamespace(n=5)
+            channels, units, unit, config = 1, 40, "Gsamples/s", {}
+            halo_kind = halo_src = None
+
+            def set_halo(self, kind, src):
+                self.halo_kind, self.halo_src = kind, src
+                self.config["parallelism"] = kind
+
+            def oracle(self, nthreads):
+                return None
+
+            def matches(self, ref):
+                return True
+
+        args = types.SimpleNamespace(steps=10, warmup=0, roofline_ramp=0, roofline_launches=1)
+        wl = WL()
+        legs, head = b.run_halo_legs(["xgmi", "rccl"],
+                                     lambda k: b.halo_leg(wl, k, args, world, dist.barrier, torch.device("cpu")))
+        q.put((rank, legs, head, stuck.closed))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gate_failure_leaves_the_rccl_leg_reported_over_gloo():
+    """At N > 1 the bench times both halo sources; an xGMI gate that times out on one rank marks
+    only that leg failed (its error names the rank) and the RCCL leg still yields the run's
+    value, with bit-exact parity, so the first real multi-GPU run has a number either way."""
+    import multiprocessing as mp
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_legs_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    got = dict((r, (legs, head, closed)) for r, legs, head, closed in (q.get(timeout=5) for _ in range(2)))
+    for r in (0, 1):
+        legs, head, closed = got[r]
+        assert head == "rccl" and closed
+        assert "timed out" in legs["xgmi"]["error"] and "[1]" in legs["xgmi"]["error"]
+        rccl = legs["rccl"]
+        assert rccl["value"] == round(80 * 10 / 0.01 / 1e9, 3) and rccl["parity"].startswith("bit-exact")
+        assert rccl["halo"]["source"] == "rccl" and rccl["halo"]["exchange_us_per_step"]["max"] > 0
+
+
+def test_run_halo_legs_headline_order():
+    import bench as b
+
+    def one(kind):
+        if kind == "xgmi":
+            raise b.LegFailed("xGMI halo path unavailable: rank 0: no peer access")
+        return {"value": 1.0, "parity": "bit-exact"}
+
+    legs, head = b.run_halo_legs(["xgmi", "rccl"], one)
+    assert head == "rccl" and legs["xgmi"] == {"error": "xGMI halo path unavailable: rank 0: no peer access"}
+    legs, head = b.run_halo_legs(["xgmi", "rccl"], lambda k: {"value": 2.0, "parity": "MISMATCH"})
+    assert head is None
+    legs, head = b.run_halo_legs(["xgmi", "rccl"], lambda k: {"value": 3.0, "parity": "bit-exact"})
+    assert head == "xgmi"
