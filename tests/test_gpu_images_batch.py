@@ -92,8 +92,9 @@ def test_unaligned_image_pointer_takes_the_per_image_path():
 
 
 def test_planes_in_their_own_buffers_at_any_byte():
-    """outs[i] as a list of per-filter planes: 128-byte, 16-byte and odd plane starts (an image whose
-    first plane is not on 16 bytes goes through the per-image path)."""
+    """outs[i] as a list of per-filter planes: 128-byte, 16-byte and odd plane starts, plane 0
+    included (u8 planes may start at any byte, every one of them: the batch launch stores through
+    byte-aligned vector types in gfx950's unaligned-access mode)."""
     rng = np.random.default_rng(9)
     shapes = [(31, 4499), (17, 1280), (1, 5000)]
     xs = [rng.integers(0, 256, sh, dtype=np.uint8) for sh in shapes]
@@ -101,7 +102,7 @@ def test_planes_in_their_own_buffers_at_any_byte():
     keep, outs = [], []
     for n, sh in enumerate(shapes):
         ps = []
-        for off in ((0, 16, 1, 7), (3, 0, 16, 5), (0, 0, 0, 0))[n]:  # image 1: plane 0 off 16 B -> per image
+        for off in ((0, 16, 1, 7), (3, 0, 16, 5), (0, 0, 0, 0))[n]:  # image 1: plane 0 at an odd byte
             buf = torch.empty(sh[0] * sh[1] + off, dtype=torch.uint8, device=DEV)
             keep.append(buf)
             ps.append(buf[off:].view(sh))

@@ -314,3 +314,54 @@ def test_u8_long_filter_high_plane_skip_vs_oracle(L):
                 got = fir_hip.fir1d_fixed_rows(x, hq, frac, acc, fir_hip.OUT_U8_SAT)
                 want = co.fir1d_rows(x, hq, frac, acc, fir_hip.OUT_U8_SAT)
                 assert np.array_equal(got, want), (shape, name, frac, acc)
+
+
+def test_table_survives_its_stream_destroyed_mid_launch():
+    """A tap table still read by launches on a stream that is destroyed while they run: a new
+    stream (which may reuse the destroyed one's handle) uses the same table, then more distinct
+    tables than the cache budget force eviction.  The cache keeps one event per use and never
+    re-records a pending one (dev_tables.hip), so the table outlives every launch that reads it
+    and all outputs equal the oracle (the old per-(table, stream) re-record trusted
+    a reused handle)."""
+    import ctypes
+    from types import SimpleNamespace
+
+    hip = ctypes.CDLL("libamdhip64.so")  # the HIP runtime already in the process (torch's / the library's)
+    co = c_oracle()
+    rng = np.random.default_rng(31)
+    x = rng.integers(0, 256, 8192, dtype=np.uint8)
+    L = 1 << 20  # generic kernel, taps read from a 4 MiB device table
+    hq = np.zeros(L, dtype=np.int32)
+    hq[rng.integers(0, L, 256)] = rng.integers(-4096, 4096, 256)
+    hq[L // 2 - 1:L // 2 + 2] += np.array([1024, 2048, 1024], dtype=np.int32)
+    want = co.fir1d_rows(x.reshape(1, -1), hq, 12, 32, co.OUT_U8_SAT).reshape(-1)
+    torch.cuda.set_device(0)
+    xd = torch.from_numpy(x).to(DEV)
+    ys = [torch.full(x.shape, 7, dtype=torch.uint8, device=DEV) for _ in range(4)]
+    torch.cuda.synchronize()
+
+    def new_stream():
+        h = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(h)) == 0
+        return SimpleNamespace(cuda_stream=h.value)
+
+    sa = new_stream()
+    for y in ys[:3]:  # queued work that reads the table for a while
+        torch_ops.fir1d_fixed_rows_dev(xd, hq, 12, 32, fir_hip.OUT_U8_SAT, out=y, stream=sa)
+    assert hip.hipStreamDestroy(ctypes.c_void_p(sa.cuda_stream)) == 0  # may return with the launches in flight
+    sb = new_stream()
+    torch_ops.fir1d_fixed_rows_dev(xd, hq, 12, 32, fir_hip.OUT_U8_SAT, out=ys[3], stream=sb)
+    small = torch.from_numpy(rng.integers(0, 256, 96, dtype=np.uint8)).to(DEV)
+    big = 1 << 22  # 16 MiB tables: 20 of them pass the 256 MiB budget, so idle tables are evicted
+    outs = []
+    for k in range(20):
+        h2 = np.zeros(big, dtype=np.int32)
+        h2[big // 2] = 4096 + k
+        outs.append((h2, torch_ops.fir1d_fixed_rows_dev(small, h2, 12, 32, fir_hip.OUT_U8_SAT, stream=sb)))
+    torch.cuda.synchronize()
+    assert hip.hipStreamDestroy(ctypes.c_void_p(sb.cuda_stream)) == 0
+    for y in ys:
+        assert np.array_equal(y.cpu().numpy(), want)
+    s = small.cpu().numpy().reshape(1, -1)
+    for h2, y in outs[::5]:
+        assert np.array_equal(y.cpu().numpy(), co.fir1d_rows(s, h2, 12, 32, co.OUT_U8_SAT).reshape(-1))

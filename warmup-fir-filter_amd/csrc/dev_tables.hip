@@ -9,11 +9,14 @@
 //     table is built from, so that one is built only on a miss) behind a kind tag: looked up by a
 //     128-bit hash and its size, confirmed by comparing those bytes (a collision is a miss);
 //   * every hold counts as in use until the launch it was taken for has been enqueued, and each
-//     use then records the table's event for that stream (one event per (table, stream),
-//     re-recorded by each later use: in stream order the latest record covers every earlier use,
-//     so a table used by millions of launches still holds one event per stream); a table is
-//     freed only when it has no hold and every stream's event has completed, never by a
-//     device-wide sync (which would also invalidate another thread's stream capture);
+//     use then records an event of its own behind that launch, kept until it has completed
+//     (completed ones go back to a pool, oldest first, so the events held stay bounded by the
+//     launches in flight).  No event is ever re-recorded while its record is pending: that would
+//     assume the stream handle still names the stream that made the record, and a destroyed
+//     stream's handle may be handed to a new stream while the old one's launches still run
+//     (hipStreamDestroy may return with work in flight).  A table is freed only when it has no
+//     hold and every use's event has completed, never by a device-wide sync (which would also
+//     invalidate another thread's stream capture);
 //   * a table used by a launch that was captured into a hipGraph is pinned for the process life
 //     (the graph keeps its address);
 //   * past kTableBudget bytes per device the cache frees idle tables; when none is idle it grows
@@ -21,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -41,10 +45,8 @@ struct Entry {
     size_t bytes = 0;
     int holds = 0;                  // acquired, launch not yet enqueued
     bool pinned = false;            // used by a captured graph
-    // the latest use on each stream that used it (an event re-recorded by every use there).  A
-    // destroyed stream's handle can name a new stream only once its resources are released, i.e.
-    // after its pending work, so re-recording on a reused handle never hides a running use.
-    std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
+    // one event per use whose completion has not been seen yet, in record order
+    std::deque<hipEvent_t> uses;
 };
 
 // (hash, size) first: the source bytes are compared only between tables whose hashes are equal
@@ -70,14 +72,23 @@ TableCache* cache_for(int dev) {
     return c.get();
 }
 
+// return the completed events at the front of e's uses to the pool (oldest first: amortised
+// O(1) per use; a completed event behind a pending one waits for that one)
+void prune(TableCache* c, Entry& e) {
+    while (!e.uses.empty() && hipEventQuery(e.uses.front()) == hipSuccess) {
+        c->free_events.push_back(e.uses.front());
+        e.uses.pop_front();
+    }
+}
+
 // true when every recorded use of e has completed (completed events go back to the pool)
 bool idle(TableCache* c, Entry& e) {
-    size_t k = 0;
-    for (const auto& u : e.uses) {
-        if (hipEventQuery(u.second) == hipSuccess) c->free_events.push_back(u.second);
-        else e.uses[k++] = u;
+    std::deque<hipEvent_t> pending;
+    for (hipEvent_t ev : e.uses) {
+        if (hipEventQuery(ev) == hipSuccess) c->free_events.push_back(ev);
+        else pending.push_back(ev);
     }
-    e.uses.resize(k);
+    e.uses.swap(pending);
     return e.holds == 0 && !e.pinned && e.uses.empty();
 }
 
@@ -106,7 +117,7 @@ void TableHash::add(const void* p, size_t n) {
     }
 }
 
-const void* table_acquire(const TableHash& h, size_t bytes, const std::function<void(void*)>& fill, std::string* err) {
+const void* table_acquire(TableHash&& h, size_t bytes, const std::function<void(void*)>& fill, std::string* err) {
     if (bytes == 0) {
         *err = "device_table: empty table";
         return nullptr;
@@ -118,7 +129,7 @@ const void* table_acquire(const TableHash& h, size_t bytes, const std::function<
         return nullptr;
     }
     TableCache* c = cache_for(dev);
-    Key key{h.a, h.c, bytes, h.src};
+    Key key{h.a, h.c, bytes, std::move(h.src)};  // the identity bytes move, once: no copy on a hit
     std::lock_guard<std::mutex> lk(c->mu);
     auto it = c->tables.find(key);
     if (it != c->tables.end()) {
@@ -170,12 +181,7 @@ void table_release(const void* d, hipStream_t stream, bool launched) {
         en.pinned = true;  // a graph holds the address for as long as it lives
         return;
     }
-    for (auto& u : en.uses) {
-        if (u.first == stream) {  // this stream's event: the new record covers the old one
-            if (hipEventRecord(u.second, stream) != hipSuccess) en.pinned = true;
-            return;
-        }
-    }
+    prune(c, en);
     hipEvent_t ev = nullptr;
     if (!c->free_events.empty()) {
         ev = c->free_events.back();
@@ -189,7 +195,7 @@ void table_release(const void* d, hipStream_t stream, bool launched) {
         en.pinned = true;
         return;
     }
-    en.uses.emplace_back(stream, ev);
+    en.uses.push_back(ev);
 }
 
 const void* device_table(const void* host, size_t bytes, std::string* err) {
@@ -199,7 +205,7 @@ const void* device_table(const void* host, size_t bytes, std::string* err) {
     }
     TableHash h(kTableRaw);
     h.add(host, bytes);
-    return table_acquire(h, bytes, [&](void* dst) { std::memcpy(dst, host, bytes); }, err);
+    return table_acquire(std::move(h), bytes, [&](void* dst) { std::memcpy(dst, host, bytes); }, err);
 }
 
 }  // namespace fir

@@ -305,11 +305,12 @@ int launch_fir1d_rows_multi(const void* x, int in_dtype, int64_t rows, int64_t w
     const size_t osz = stage == FIR_OUT_I32 ? 4 : 1;
     // u8 output planes start where the previous one ends, at any byte (the reference's 4499 x 2999
     // image: plane f at f * 13492501): the fused kernel's 16-byte stores then run unaligned, which
-    // gfx950 performs in the unaligned-access mode ROCm sets for compute queues (the int32 planes
-    // keep whole-dword row staging and stay on 16-byte plane starts)
-    const bool fused = in_dtype == FIR_IN_U8 && ch == 1 &&
-                       (stage == FIR_OUT_U8_SAT || (total * (int64_t)osz) % 16 == 0) &&
-                       reg_path_ok(x, y, in_dtype, rows, rowlen, total, ch, hq, F * L, L, frac, acc_bits);
+    // gfx950 performs in the unaligned-access mode ROCm sets for compute queues (byte-aligned store
+    // types, fir1d_reg.h), so for the u8 stage no plane's alignment is a condition, plane 0's
+    // included; the int32 planes keep whole-dword row staging and stay on 16-byte plane starts
+    const bool u8out = stage == FIR_OUT_U8_SAT;
+    const bool fused = in_dtype == FIR_IN_U8 && ch == 1 && (u8out || (total * (int64_t)osz) % 16 == 0) &&
+                       reg_path_ok(x, u8out ? x : y, in_dtype, rows, rowlen, total, ch, hq, F * L, L, frac, acc_bits);
     for (int f0 = 0; f0 < F;) {
         const int nf = fused ? (F - f0 < 4 ? F - f0 : 4) : 1;
         void* yf = (char*)y + (size_t)f0 * (size_t)total * osz;
@@ -355,8 +356,10 @@ int launch_fir1d_images_multi(int n, const void* const* xs, const int64_t* rows,
         const int64_t total = rows[i] * widths[i] * ch;
         if (total == 0) continue;
         void* const* yp = planes + (size_t)i * F;
+        // u8 planes may start at any byte, each of them (see launch_fir1d_rows_multi): only the
+        // image's own alignment and shape decide
         if (in_dtype == FIR_IN_U8 && ch == 1 && stage == FIR_OUT_U8_SAT &&
-            reg_path_ok(xs[i], yp[0], in_dtype, rows[i], widths[i], total, ch, hq, F * L, L, frac, acc_bits)) {
+            reg_path_ok(xs[i], xs[i], in_dtype, rows[i], widths[i], total, ch, hq, F * L, L, frac, acc_bits)) {
             batch.push_back(i);
             continue;
         }

@@ -494,7 +494,7 @@ static const mf_i32x4* mfma_frag_table(const int32_t* hq, int L, int P, int KS, 
     h.add(hq, sizeof(int32_t) * (size_t)L);
     h.add_val(L), h.add_val(P), h.add_val(KS);
     const size_t bytes = (size_t)KS * 2 * kWave * 16;
-    return (const mf_i32x4*)table_acquire(h, bytes, [&](void* dst) {
+    return (const mf_i32x4*)table_acquire(std::move(h), bytes, [&](void* dst) {
         int8_t* tab = (int8_t*)dst;
         for (int st = 0; st < KS; ++st)
             for (int lane = 0; lane < kWave; ++lane)

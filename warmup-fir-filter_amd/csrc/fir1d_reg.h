@@ -22,6 +22,12 @@ namespace fir {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+// u8 output planes may start at any byte (a fused bank's planes follow each other, and the
+// reference's 4499 x 2999 image puts plane f at f * 13492501): their 16- / 8-byte stores go
+// through these byte-aligned types, so the code states the alignment it has; gfx950 runs compute
+// queues in unaligned-access mode, and the same global_store_dwordx4 / dwordx2 is emitted.
+typedef uint32_t u32x4_u8a __attribute__((ext_vector_type(4), aligned(1)));
+typedef uint32_t u32x2_u8a __attribute__((ext_vector_type(2), aligned(1)));
 typedef short fir_short2v __attribute__((ext_vector_type(2)));
 
 enum RegFlags : int {
@@ -73,7 +79,7 @@ enum RegFlags : int {
 // profiles/r01/micro_i16_sc.txt; the sc0 / sc1 policy bits add nothing).  The s_nop covers the
 // VMEM-store-data hazard (a VALU write of the data VGPRs right after a >64-bit store), which the
 // compiler cannot see through inline asm.
-__device__ __forceinline__ void store16_nt(u32x4* p, u32x4 v) {
+__device__ __forceinline__ void store16_nt(void* p, u32x4 v) {
     asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
@@ -249,15 +255,15 @@ __device__ __forceinline__ void store_vec(typename OutTraits<STAGE>::T* __restri
                            ((uint32_t)stage_out32<STAGE>(q[4 * i + 3]) << 24);
             }
             if constexpr (VEC == 16) {
-                const u32x4 val = {o[0], o[1], o[2], o[3]};
-                u32x4* p = reinterpret_cast<u32x4*>(y + g0);
+                const u32x4_u8a val = {o[0], o[1], o[2], o[3]};
+                u32x4_u8a* p = reinterpret_cast<u32x4_u8a*>(y + g0);
                 if constexpr (NT)
                     store16_nt(p, val);  // u8 path: 79.2 -> 78.0 us vs the builtin (micro_u8_asm.txt)
                 else
                     *p = val;
             } else {
-                const u32x2 val = {o[0], o[1]};
-                u32x2* p = reinterpret_cast<u32x2*>(y + g0);
+                const u32x2_u8a val = {o[0], o[1]};
+                u32x2_u8a* p = reinterpret_cast<u32x2_u8a*>(y + g0);
                 if (NT) __builtin_nontemporal_store(val, p); else *p = val;
             }
         } else {
@@ -283,15 +289,15 @@ __device__ __forceinline__ void store_u8_dwords(uint8_t* __restrict__ y, int64_t
                                                 const uint32_t (&o)[VEC / 4]) {
     if (full) {
         if constexpr (VEC == 16) {
-            const u32x4 val = {o[0], o[1], o[2], o[3]};
-            u32x4* p = reinterpret_cast<u32x4*>(y + g0);
+            const u32x4_u8a val = {o[0], o[1], o[2], o[3]};
+            u32x4_u8a* p = reinterpret_cast<u32x4_u8a*>(y + g0);
             if constexpr (NT)
                 store16_nt(p, val);
             else
                 *p = val;
         } else {
-            const u32x2 val = {o[0], o[1]};
-            u32x2* p = reinterpret_cast<u32x2*>(y + g0);
+            const u32x2_u8a val = {o[0], o[1]};
+            u32x2_u8a* p = reinterpret_cast<u32x2_u8a*>(y + g0);
             if (NT) __builtin_nontemporal_store(val, p); else *p = val;
         }
     } else if (g0 < total) {

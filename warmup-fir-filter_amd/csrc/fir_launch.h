@@ -29,7 +29,7 @@ struct TableHash {
     template <typename T>
     void add_val(const T& v) { add(&v, sizeof(v)); }
 };
-const void* table_acquire(const TableHash& h, size_t bytes, const std::function<void(void*)>& fill, std::string* err);
+const void* table_acquire(TableHash&& h, size_t bytes, const std::function<void(void*)>& fill, std::string* err);
 void table_release(const void* d, hipStream_t stream, bool launched = true);
 const void* device_table(const void* host, size_t bytes, std::string* err);  // table_acquire by content
 struct TableHold {  // one launch's hold: released (its use recorded on `s`) when the scope ends
