@@ -20,8 +20,8 @@ Extra keys:
   roofline      dominant kernel's algorithmic bytes / its mean duration (HIP events on the
                 stream it runs on: 100 untimed ramp launches and >= 50 ms of them, then 200 timed back to back,
                 whatever --steps/--warmup are), vs the 8.0 TB/s HBM3E peak; `traffic` = PMC
-                HBM bytes per launch from the committed rocprofv3 summary in profiles/ (null if
-                absent)
+                HBM bytes per launch from the committed rocprofv3 summary in profiles/, null if
+                absent or taken on another build (its build_id must equal fir_build_id())
   cpu_baseline  the C oracle (oracle/fir_oracle.c, OpenMP) on this host's cores, same input;
                 timed by rank 0 at every N, after the GPU legs, while the other ranks wait
   parity        every rank's full output compared bit-exactly with the C oracle
@@ -685,19 +685,23 @@ def gate_failures(wl: Workload, world: int, red_dev) -> list[int]:
     return [r for r, f in enumerate(flags) if f]
 
 
-def pmc_traffic(wl: Workload):
+def pmc_traffic(wl: Workload, root: Path = ROOT):
     """HBM bytes per launch (per step for pipeline_fixed3) from the committed rocprofv3 PMC summary
-    profiles/pmc_<workload>.json, when it was taken at this workload's size; else None."""
-    pmc = ROOT / "profiles" / f"pmc_{wl.name}{'_gen5x5' if wl.gen2d else ''}.json"
+    profiles/pmc_<workload>.json -- only when it was taken at this workload's size AND on the build
+    that is running (its build_id, written by tools/pmc_summary.py from fir_build_id() on the box,
+    equals the loaded library's): a summary of another build describes other kernels.  Else None."""
+    pmc = root / "profiles" / f"pmc_{wl.name}{'_gen5x5' if wl.gen2d else ''}.json"
     if not pmc.exists():
         return None
     try:
         summary = json.loads(pmc.read_text())
     except (ValueError, OSError):
         return None
-    if summary.get("algorithmic_bytes_per_launch") == wl.alg_bytes:
-        return summary.get("hbm_bytes_per_launch")
-    return None
+    if summary.get("algorithmic_bytes_per_launch") != wl.alg_bytes:
+        return None
+    if summary.get("build_id") != fir_hip.build_id():
+        return None
+    return summary.get("hbm_bytes_per_launch")
 
 
 # The other single-GPU BASELINE configs, timed after the headline when bench.py runs without

@@ -266,3 +266,28 @@ def test_run_halo_legs_headline_order():
     assert head is None
     legs, head = b.run_halo_legs(["xgmi", "rccl"], lambda k: {"value": 3.0, "parity": "bit-exact"})
     assert head == "xgmi"
+
+
+def test_pmc_traffic_only_for_the_running_build(tmp_path):
+    """roofline.traffic comes from a committed PMC summary only when that summary was taken on the
+    build that is running (build_id == fir_build_id()) at this workload's size; a summary of
+    another build, an old one without an id, or another size gives null."""
+    import json
+    import types
+
+    import bench as b
+    import fir_hip
+
+    wl = types.SimpleNamespace(name="fir1d_i16", gen2d=False, alg_bytes=1610612736)
+    (tmp_path / "profiles").mkdir()
+    path = tmp_path / "profiles" / "pmc_fir1d_i16.json"
+    assert b.pmc_traffic(wl, tmp_path) is None  # no summary
+    base = {"algorithmic_bytes_per_launch": wl.alg_bytes, "hbm_bytes_per_launch": 1644000000}
+    path.write_text(json.dumps(dict(base, build_id=fir_hip.build_id())))
+    assert b.pmc_traffic(wl, tmp_path) == 1644000000
+    path.write_text(json.dumps(dict(base, build_id="0" * 32)))
+    assert b.pmc_traffic(wl, tmp_path) is None  # another build
+    path.write_text(json.dumps(base))
+    assert b.pmc_traffic(wl, tmp_path) is None  # no build id: taken before round 6
+    path.write_text(json.dumps(dict(base, build_id=fir_hip.build_id(), algorithmic_bytes_per_launch=5)))
+    assert b.pmc_traffic(wl, tmp_path) is None  # another size

@@ -7,6 +7,10 @@ run_counter_collection.csv.  Per MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_S
 on gfx950 FETCH_SIZE reports exactly half of the bytes of a wide (16 B/lane) coalesced
 streaming read, so it is doubled; WRITE_SIZE is exact for 16-B/lane streaming stores.
 
+The summary records the build id of the library the passes ran (fir_hip.build_id(), i.e. the
+source hash the .so was built from): bench.py attaches a summary's traffic only to runs of that
+same build.  Run it on the box, in the same call as the passes.
+
 Usage: tools/pmc_summary.py <dir with pmc_FETCH_SIZE/ and pmc_WRITE_SIZE/> <kernel substring>
                             <algorithmic bytes per launch> <out.json> [dir prefix, default pmc_]
 """
@@ -30,6 +34,14 @@ def per_launch(path: Path, counter: str, kernel: str) -> list[float]:
     return vals
 
 
+def build_id() -> str:
+    repo = Path(__file__).resolve().parents[1]
+    sys.path.insert(0, str(repo / "warmup-fir-filter_amd"))
+    import fir_hip
+
+    return fir_hip.build_id()
+
+
 def main() -> None:
     root, kernel, alg, out = Path(sys.argv[1]), sys.argv[2], int(sys.argv[3]), Path(sys.argv[4])
     pre = sys.argv[5] if len(sys.argv) > 5 else "pmc_"
@@ -49,6 +61,7 @@ def main() -> None:
         "traffic_over_algorithmic": round((fetch_b + write_b) / alg, 4),
         "correction": "FETCH_SIZE x2 (gfx950 reports half of wide coalesced streaming reads), WRITE_SIZE x1",
         "source": str(root),
+        "build_id": build_id(),
     }
     out.write_text(json.dumps(summary, indent=1) + "\n")
     print(json.dumps(summary))
