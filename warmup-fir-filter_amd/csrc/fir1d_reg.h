@@ -64,7 +64,7 @@ enum RegFlags : int {
     // Rows that straddle vectors, other stages / channel counts: seam vectors take the masked
     // generic pair (fir_vector_masked).  Without kMasked or kRagged the launcher guarantees
     // RowGeom::aligned, and the masked pair is not compiled in (it held 45 of the fused u8 bank's
-    // 90 VGPRs; single-filter launches keep kMasked for its code layout, fir1d_reg_impl.h).
+    // 90 VGPRs; single int16 filters keep kMasked for its code layout, fir1d_reg_impl.h).
     kMasked = 16384,
     // with kRagged: every filter's output bytes are held until ONE seam fix after the filter loop,
     // then stored (batch launches that hold a ragged image): the 7 golden images' stage 15.05-15.35

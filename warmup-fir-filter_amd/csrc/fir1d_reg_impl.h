@@ -63,10 +63,12 @@ static hipError_t launch_reg_flags(const void* x, void* y, int64_t rows, int64_t
     if (!make_taps<L, F, FL>(t, hq, frac)) return hipErrorInvalidValue;
     int64_t ntiles = 0, blocks = 0;
     reg_launch_geometry<InT, kRegU<InT, F>, FL>(total, kPersistBlocks, &ntiles, &blocks);
-    // One filter keeps the masked pair compiled in even where it cannot run: that layout measured
-    // faster in the same process (int16 headline 244.6 vs 246.0 us, u8 77.3 vs 78.3;
-    // profiles/r05/masked_layout_ab.txt).  Banks drop it (90 -> 39 VGPRs, no loss).
-    constexpr int FM = F == 1 ? kMasked : 0;
+    // One int16 filter keeps the masked pair compiled in even where it cannot run: that code
+    // layout is faster in every one of 12 interleaved pairs in one process (headline 244.98 vs
+    // 246.02 us median, profiles/r06/ab_pairs_single_filter.txt).  u8 filters and banks drop it:
+    // for one u8 filter the pairs tie (78.86 vs 79.01 us, 6 of 12 each way) and the kernel halves
+    // (4321 -> 2037 instructions, 66 -> 62 VGPRs); a bank's VGPRs go 90 -> 39.
+    constexpr int FM = F == 1 && sizeof(InT) == 2 ? kMasked : 0;
     if constexpr (F == 1) {
         if (hl != nullptr || hr != nullptr) {
             hipLaunchKernelGGL((fir1d_reg_kernel<InT, STAGE, L, CH, kRegU<InT, F>, FL | kHalo | FM, F>), dim3((unsigned)blocks),
