@@ -27,8 +27,13 @@ CONTRACT = json.loads((Path(__file__).resolve().parent / "golden" / "stage_contr
 BY_NAME = {r["name"]: r for r in CONTRACT["scenarios"]}
 
 
+@pytest.mark.parametrize("batch_bytes", [1 << 30, 4096])
 @pytest.mark.parametrize("scn", S.SCENARIOS, ids=[s["name"] for s in S.SCENARIOS])
-def test_stage_matches_reference_outcome(scn, tmp_path):
+def test_stage_matches_reference_outcome(scn, batch_bytes, tmp_path, monkeypatch):
+    """One device call per stage, and (4096-byte windows) one per image or two."""
+    from fir_1d.sim.vector import stage_io
+
+    monkeypatch.setattr(stage_io, "BATCH_BYTES", batch_bytes)
     got = S.run(scn, tmp_path, gf._generate_fixed_outputs_for_tap_map, gi._generate_ideal_outputs_for_tap_map)
     want = BY_NAME[scn["name"]]
     assert got["error"] == want["error"]

@@ -28,3 +28,56 @@ def test_device_free_scenarios_match_reference(name, tmp_path):
     got = S.run(scn, tmp_path, gf._generate_fixed_outputs_for_tap_map, gi._generate_ideal_outputs_for_tap_map)
     want = BY_NAME[name]
     assert (got["returned"], got["error"], got["files"]) == (want["returned"], want["error"], want["files"])
+
+
+def _oracle_batches(monkeypatch):
+    """The two image-batch C entries replaced by the oracle (same signatures, planes delivered
+    largest first through ``ready``): every scenario then runs on the CPU through the product's
+    stage driver -- planning, skip / error order, page-locked staging fallback, windows, ordered
+    concurrent writes -- with only the device call stood in for."""
+    import numpy as np
+
+    import fir_hip
+    from oracle import fir_oracle as fo
+
+    def deliver(xs, outs, nf, ready, timing):
+        order = sorted(((i, f) for i in range(len(xs)) for f in range(nf)), key=lambda p: -xs[p[0]].size)
+        for i, f in order:
+            if ready is not None:
+                ready(i, f)
+        if timing is not None:
+            timing.update({k: 0.0 for k in fir_hip.TIMING_KEYS})
+        return outs
+
+    def fixed(xs, hq2, frac_bits=12, acc_bits=32, out_stage=0, channels=1, device=0, outs=None, ready=None,
+              timing=None):
+        h2 = np.asarray(hq2, dtype=np.int64)
+        for x, planes in zip(xs, outs):
+            for h, y in zip(h2, planes):
+                y[...] = fo.fir1d_rows(x, h, frac_bits, acc_bits, fo.OUT_U8_SAT)
+        return deliver(xs, outs, len(h2), ready, timing)
+
+    def ideal(xs, hs, device=0, outs=None, ready=None, timing=None):
+        for x, planes in zip(xs, outs):
+            for h, y in zip(hs, planes):
+                y[...] = fo.fir1d_ideal_rows(x, h)
+        return deliver(xs, outs, len(hs), ready, timing)
+
+    monkeypatch.setattr(fir_hip, "fir1d_fixed_images_multi", fixed)
+    monkeypatch.setattr(fir_hip, "fir1d_ideal_images_multi", ideal)
+
+
+@pytest.mark.parametrize("batch_bytes", [1 << 30, 4096])
+@pytest.mark.parametrize("scn", S.SCENARIOS, ids=[s["name"] for s in S.SCENARIOS])
+def test_stage_driver_matches_reference_with_oracle_compute(scn, batch_bytes, tmp_path, monkeypatch):
+    """Every scenario through the product's stage driver with the device call replaced by the
+    oracle: the reference's return value, exception text and every file's SHA-256.  4096-byte
+    windows split each stage into one device call per image or two (stage_io.BATCH_BYTES)."""
+    from fir_1d.sim.vector import stage_io
+
+    _oracle_batches(monkeypatch)
+    monkeypatch.setattr(stage_io, "BATCH_BYTES", batch_bytes)
+    got = S.run(scn, tmp_path, gf._generate_fixed_outputs_for_tap_map, gi._generate_ideal_outputs_for_tap_map)
+    want = BY_NAME[scn["name"]]
+    assert (got["returned"], got["error"], got["files"]) == (want["returned"], want["error"], want["files"])
+    assert not list((tmp_path / "output").rglob(".*.part"))  # no temporary file left behind
