@@ -12,9 +12,13 @@ WLS=${*:-"fir1d_i16 cplx_i16 fir2d_u8 pipeline_fixed3"}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+# the dominant kernel of each workload (bench.KERNELS) and its algorithmic bytes per launch
 declare -A KERN=([fir1d_i16]=fir1d_reg_kernel [cplx_i16]=fir1d_reg_kernel [fir2d_u8]=fir2d_pk16_strip_kernel
-                 [pipeline_fixed3]=fir1d_reg_batch_kernel)
-declare -A ALG=([fir1d_i16]=1610612736 [cplx_i16]=1610612736 [fir2d_u8]=536870912 [pipeline_fixed3]=84969065)
+                 [pipeline_fixed3]=fir1d_reg_batch_kernel [fir1d_u8]=fir1d_reg_kernel [bank_u8]=fir1d_reg_kernel
+                 [ideal_u8]=fir1d_ideal_reg_kernel [restore_u8]=restore_map_kernel [metrics_u8]=metrics_leaf_kernel)
+declare -A ALG=([fir1d_i16]=1610612736 [cplx_i16]=1610612736 [fir2d_u8]=536870912 [pipeline_fixed3]=84969065
+                [fir1d_u8]=536870912 [bank_u8]=1342177280 [ideal_u8]=2415919104 [restore_u8]=2415919104
+                [metrics_u8]=2415919104)
 for wl in $WLS; do
     for c in FETCH_SIZE WRITE_SIZE; do
         echo "== $wl $c"
