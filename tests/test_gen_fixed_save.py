@@ -82,3 +82,18 @@ def test_npy_header_fast_path_accepts_only_2d_c_order_u8(tmp_path):
     assert stage_io.npy_u8_2d_shape(tmp_path / "trunc.npy") is None
     (tmp_path / "junk.npy").write_bytes(b"not an npy file")
     assert stage_io.npy_u8_2d_shape(tmp_path / "junk.npy") is None
+
+
+def test_links_are_written_through_like_np_save(tmp_path):
+    """np.save writes through a symlink and into a file other names share; the ordered writer
+    does the same for such targets (it does not replace the link by a new file)."""
+    target = tmp_path / "target.npy"
+    np.save(target, np.zeros(3, np.uint8))
+    (tmp_path / "y0.npy").symlink_to(target)
+    other = tmp_path / "other_name.npy"
+    np.save(other, np.zeros(2, np.uint8))
+    os.link(other, tmp_path / "y1.npy")
+    ys = [np.full(3, 5, np.uint8), np.full(2, 6, np.uint8)]
+    assert _save_all([(tmp_path / "y0.npy", ys[0]), (tmp_path / "y1.npy", ys[1])]) == 2
+    assert (tmp_path / "y0.npy").is_symlink() and np.array_equal(np.load(target), ys[0])
+    assert np.array_equal(np.load(other), ys[1])  # the shared file itself was rewritten

@@ -134,7 +134,8 @@ class OrderedSaver:
     write failed, or whose existing target the reference's open(path, "wb") would refuse, is
     redone as np.save(path, y) -- the reference's own call, which raises its error -- and every
     later temporary file is removed, so the directory holds what the reference's sequential loop
-    would have left."""
+    would have left.  A target that is a symlink or has other hard links is written by
+    np.save(path, y) too, as the reference writes it (through the link, into the shared file)."""
 
     def __init__(self, workers: int | None = None):
         self.pool = ThreadPoolExecutor(max_workers=workers or save_workers())
@@ -169,6 +170,8 @@ class OrderedSaver:
             for i in sorted(self.items):
                 path, y, tmp, fut = self.items[i]
                 ok = fut.exception() is None
+                if ok and (path.is_symlink() or (path.is_file() and path.stat().st_nlink > 1)):
+                    ok = False  # np.save writes through a link (every name of the file sees it): do that
                 if ok and path.exists():
                     try:  # the access check open(path, "wb") makes, without truncating the file
                         os.close(os.open(path, os.O_WRONLY))
