@@ -5,14 +5,24 @@ Mirrors the reference's twin modules ``fir_1d/sim/vector/gen_{3,5}tap_compare_re
 with ``..._fixed_Ntap_y_u8.npy``), validation lists and strict-mode error, CSV columns,
 summary-JSON sections (config / validation / overall / by_coeff / worst_cases_by_rmse /
 cases), console summary and return value.  The per-case metrics (:67-112 there) are one
-fused GPU reduction (``fir_hip.compare_metrics``) instead of seven NumPy passes; counts and
-max|d| are exact, the float64 sums agree with NumPy's to ~1e-15 relative.
+fused GPU reduction (``fir_hip.compare_metrics``) instead of seven NumPy passes, every value
+bit-identical to the reference's (the float64 sums added in NumPy's order).  The reference
+np.loads each pair in turn (:303-304); here a plain pair (C-order float64 ideal, uint8 fixed of
+the same shape, as the pipeline's stages write them) is read straight from its files into
+page-locked staging by a pool of readers running ahead of the metrics calls, so the ideal
+arrays' 544 MB per stage are neither page-faulted into fresh arrays nor staged again for the
+upload; any other file goes through np.load at its turn, so a file np.load refuses raises the
+reference's error in the reference's order (no report file is written before that point in
+either).  Pinned against 15 scenarios run through the reference's own report functions
+(tests/golden/report_contract.json).
 """
 from __future__ import annotations
 
 import csv
 import json
 import re
+import time
+from concurrent.futures import ThreadPoolExecutor
 from datetime import datetime, timezone
 from pathlib import Path
 from typing import Any
@@ -20,6 +30,7 @@ from typing import Any
 import numpy as np
 
 import fir_hip
+from fir_1d.sim.vector import stage_io
 
 THIS_FILE = Path(__file__).resolve()
 DEFAULT_OUTPUT_DIR = THIS_FILE.parent / "output"
@@ -63,6 +74,78 @@ def compute_metrics(y_ideal: np.ndarray, y_fixed: np.ndarray) -> dict[str, float
     return fir_hip.compare_metrics(y_ideal, y_fixed)
 
 
+class _Pair:
+    """One matched (ideal, fixed) pair of the report, planned in key order."""
+
+    def __init__(self, key, ip: Path, fp: Path):
+        self.key, self.ip, self.fp = key, ip, fp
+        self.yi = self.yf = None  # arrays (np.load, or views of the staging once read)
+        self.shapes = None  # (ideal shape, fixed shape) when the headers alone decide a mismatch
+        self.plain = None  # (shape, ideal offset, fixed offset): read into staging
+        self.reads = None
+
+
+def _plan_pair(key, ip: Path, fp: Path) -> _Pair:
+    """Headers first; np.load (the reference's call, raising its error) for anything but a plain pair."""
+    pr = _Pair(key, ip, fp)
+    hi, hf = stage_io.npy_header(ip), stage_io.npy_header(fp)
+    if hi is not None and hf is not None and not hi[1] and not hf[1] and hi[2] == np.dtype(np.float64) \
+            and hf[2] == np.dtype(np.uint8):
+        if hi[0] == hf[0]:
+            pr.plain = (hi[0], hi[3], hf[3])
+        else:
+            pr.shapes = (hi[0], hf[0])
+        return pr
+    pr.yi, pr.yf = np.load(ip), np.load(fp)
+    return pr
+
+
+def _pairs(shared, ideal_map, fixed_map, timings: dict | None):
+    """Yield the planned pairs in key order with their arrays in place: windows of at most
+    stage_io.BATCH_BYTES of plain pairs are read by a reader pool into page-locked staging
+    (float64 ideal arrays in one buffer, uint8 fixed arrays in another) while the metrics of the
+    pairs before them run."""
+    planned = [_plan_pair(k, ideal_map[k], fixed_map[k]) for k in shared]
+    t_read = 0.0
+    with ThreadPoolExecutor(max_workers=stage_io.save_workers()) as pool:
+        i0 = 0
+        while i0 < len(planned):
+            i1, nbytes = i0, 0
+            while i1 < len(planned):
+                pl = planned[i1].plain
+                b = 9 * stage_io._align(int(np.prod(pl[0], dtype=np.int64))) if pl else 0
+                if i1 > i0 and nbytes + b > stage_io.BATCH_BYTES:
+                    break
+                nbytes += b
+                i1 += 1
+            window = planned[i0:i1]
+            sizes = [int(np.prod(pr.plain[0], dtype=np.int64)) if pr.plain else 0 for pr in window]
+            ar = stage_io.arena()  # the ideal stage's output staging, reused: no new pinned memory
+            ibuf = ar.take("out", sum(stage_io._align(8 * n) for n in sizes))
+            fbuf = ar.take("aux", sum(stage_io._align(n) for n in sizes))
+            oi = of = 0
+            for pr, n in zip(window, sizes):
+                if pr.plain is None:
+                    continue
+                pr.yi = ibuf[oi:oi + 8 * n].view(np.float64).reshape(pr.plain[0])
+                pr.yf = fbuf[of:of + n].reshape(pr.plain[0])
+                oi += stage_io._align(8 * n)
+                of += stage_io._align(n)
+                pr.reads = (pool.submit(stage_io.read_into, pr.ip, pr.plain[1], pr.yi),
+                            pool.submit(stage_io.read_into, pr.fp, pr.plain[2], pr.yf))
+            for pr in window:
+                if pr.reads is not None:
+                    t0 = time.perf_counter()
+                    ok = all(f.result() for f in pr.reads)
+                    t_read += time.perf_counter() - t0
+                    if not ok:  # the data did not come: np.load judges the files, as the reference would
+                        pr.yi, pr.yf = np.load(pr.ip), np.load(pr.fp)
+                yield pr
+            i0 = i1
+    if timings is not None:
+        timings["read_wait_ms"] = round(t_read * 1e3, 3)
+
+
 def summarize_rows(rows: list[dict[str, Any]]) -> dict[str, Any]:
     out: dict[str, Any] = {"num_cases": len(rows),
                            "num_samples_total": int(sum(int(r["num_samples"]) for r in rows))}
@@ -74,7 +157,10 @@ def summarize_rows(rows: list[dict[str, Any]]) -> dict[str, Any]:
 
 
 def generate_compare_report(tap: str, *, ideal_dir: Path, fixed_dir: Path, report_dir: Path, top_k: int = 5,
-                            strict: bool = False, verbose: bool = True) -> dict[str, Any]:
+                            strict: bool = False, verbose: bool = True, timings: dict | None = None) -> dict[str, Any]:
+    """The report stage (gen_3tap_compare_report.py:263-400).  ``timings`` (a dict) receives
+    read_wait_ms (time the metrics calls waited for file reads), metrics_ms and wall_ms."""
+    t_start = time.perf_counter()
     ideal_dir, fixed_dir, report_dir = Path(ideal_dir).resolve(), Path(fixed_dir).resolve(), Path(report_dir).resolve()
     if not ideal_dir.exists():
         raise FileNotFoundError(f"Ideal output directory not found: {ideal_dir}")
@@ -88,15 +174,20 @@ def generate_compare_report(tap: str, *, ideal_dir: Path, fixed_dir: Path, repor
         raise ValueError(f"No matched {tap} ideal/fixed pairs found. ideal_dir={ideal_dir}, fixed_dir={fixed_dir}")
 
     rows, mismatched = [], []
-    for key in shared:
-        ip, fp = ideal_map[key], fixed_map[key]
-        yi, yf = np.load(ip), np.load(fp)
+    t_metrics = 0.0
+    for pr in _pairs(shared, ideal_map, fixed_map, timings):
+        key, ip, fp = pr.key, pr.ip, pr.fp
         name = f"{key[0]}__{key[1]}"
-        if yi.shape != yf.shape:
-            mismatched.append({"key": name, "ideal_shape": list(yi.shape), "fixed_shape": list(yf.shape),
+        si, sf = pr.shapes if pr.shapes is not None else (pr.yi.shape, pr.yf.shape)
+        if si != sf:
+            mismatched.append({"key": name, "ideal_shape": list(si), "fixed_shape": list(sf),
                                "ideal_file": ip.name, "fixed_file": fp.name})
             continue
+        yi, yf = pr.yi, pr.yf
+        t0 = time.perf_counter()
         m = compute_metrics(yi, yf)
+        t_metrics += time.perf_counter() - t0
+        pr.yi = pr.yf = None
         h, w = (int(yi.shape[0]), int(yi.shape[1])) if yi.ndim >= 2 else (1, int(yi.shape[0]))
         rows.append({"key": name, "case_stem": key[0], "coeff_name": key[1], "height": h, "width": w, **m,
                      "ideal_file": ip.name, "fixed_file": fp.name})
@@ -160,5 +251,8 @@ def generate_compare_report(tap: str, *, ideal_dir: Path, fixed_dir: Path, repor
                 print(f"{i}. key={r['key']}, rmse={r['rmse']:.6f}, mae={r['mae']:.6f}, "
                       f"max_abs_err={r['max_abs_err']:.6f}")
         print(f"[reports]\n- csv: {csv_path}\n- json: {json_path}")
+    if timings is not None:
+        timings["metrics_ms"] = round(t_metrics * 1e3, 3)
+        timings["wall_ms"] = round((time.perf_counter() - t_start) * 1e3, 3)
     return {"csv_path": str(csv_path), "json_path": str(json_path), "num_cases": overall["num_cases"],
             "num_samples_total": overall["num_samples_total"], "validation_has_issue": has_issue}

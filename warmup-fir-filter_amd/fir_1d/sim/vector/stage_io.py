@@ -75,9 +75,10 @@ def arena() -> _Arena:
     return _tls.arena
 
 
-def npy_u8_2d_shape(path: Path):
-    """(rows, cols, data offset) of a .npy file holding a 2-D C-order uint8 array, else None (the
-    caller then uses np.load, which reads -- or refuses -- the file as the reference does)."""
+def npy_header(path: Path):
+    """(shape, fortran_order, dtype, data offset) of a version 1.0 / 2.0 .npy file whose data is all
+    present, else None (the caller then uses np.load, which reads -- or refuses -- the file as the
+    reference does)."""
     try:
         with open(path, "rb") as f:
             version = np.lib.format.read_magic(f)
@@ -91,22 +92,28 @@ def npy_u8_2d_shape(path: Path):
             size = os.fstat(f.fileno()).st_size
     except Exception:  # noqa: BLE001 - anything np.load would judge: leave it to np.load
         return None
-    if dtype != np.dtype(np.uint8) or fortran or len(shape) != 2:
+    if dtype.hasobject or size - off < int(np.prod(shape, dtype=np.int64)) * dtype.itemsize:
         return None
-    if size - off < shape[0] * shape[1]:
-        return None
-    return int(shape[0]), int(shape[1]), off
+    return tuple(int(v) for v in shape), bool(fortran), dtype, off
 
 
-def read_u8_2d_into(path: Path, rows: int, cols: int, off: int, out: np.ndarray) -> bool:
-    """Read the array of a file npy_u8_2d_shape accepted into ``out`` (rows * cols bytes)."""
-    n = rows * cols
+def npy_u8_2d_shape(path: Path):
+    """(rows, cols, data offset) of a .npy file holding a 2-D C-order uint8 array, else None."""
+    h = npy_header(path)
+    if h is None or h[2] != np.dtype(np.uint8) or h[1] or len(h[0]) != 2:
+        return None
+    return h[0][0], h[0][1], h[3]
+
+
+def read_into(path: Path, off: int, out: np.ndarray) -> bool:
+    """Read out.nbytes bytes of ``path`` from byte ``off`` into the contiguous array ``out``."""
+    n = out.nbytes
     if n == 0:
         return True
     try:
         with open(path, "rb", buffering=0) as f:
             f.seek(off)
-            mv = memoryview(out)[:n]
+            mv = memoryview(out.reshape(-1).view(np.uint8))
             got = 0
             while got < n:
                 k = f.readinto(mv[got:])
@@ -116,6 +123,11 @@ def read_u8_2d_into(path: Path, rows: int, cols: int, off: int, out: np.ndarray)
     except OSError:
         return False
     return True
+
+
+def read_u8_2d_into(path: Path, rows: int, cols: int, off: int, out: np.ndarray) -> bool:
+    """Read the array of a file npy_u8_2d_shape accepted into ``out`` (rows * cols bytes)."""
+    return read_into(path, off, out.reshape(-1)[:rows * cols])
 
 
 def load_input_image_u8(path: Path) -> np.ndarray:
