@@ -97,3 +97,59 @@ def test_links_are_written_through_like_np_save(tmp_path):
     assert _save_all([(tmp_path / "y0.npy", ys[0]), (tmp_path / "y1.npy", ys[1])]) == 2
     assert (tmp_path / "y0.npy").is_symlink() and np.array_equal(np.load(target), ys[0])
     assert np.array_equal(np.load(other), ys[1])  # the shared file itself was rewritten
+
+
+def test_largest_first_pool_runs_the_largest_pending_job_first():
+    """LargestFirstPool (the restore stage's PNG writers): with its one worker held, the queued jobs
+    run largest first; results and exceptions come back through the futures."""
+    import threading
+
+    pool = stage_io.LargestFirstPool(1)
+    gate, order = threading.Event(), []
+    held = pool.submit(gate.wait, size=0)
+    futs = [pool.submit(order.append, s, size=s) for s in (3, 50, 7, 50, 1)]
+    bad = pool.submit(lambda: 1 / 0, size=2)
+    gate.set()
+    assert held.result(timeout=10) is True
+    for f in futs:
+        f.result(timeout=10)
+    with pytest.raises(ZeroDivisionError):
+        bad.result(timeout=10)
+    assert order == [50, 50, 7, 3, 1]  # equal sizes in submission order
+    pool.shutdown()
+    with pytest.raises(RuntimeError):
+        pool.submit(print)
+
+
+def test_largest_first_pool_uses_its_workers():
+    import threading
+
+    pool = stage_io.LargestFirstPool(4)
+    barrier = threading.Barrier(4, timeout=10)
+    futs = [pool.submit(barrier.wait, size=i) for i in range(4)]  # only completes with 4 threads at once
+    assert sorted(f.result(timeout=10) for f in futs) == [0, 1, 2, 3]
+    pool.shutdown()
+
+
+def test_ordered_saver_with_another_writer(tmp_path):
+    """OrderedSaver with a writer / redo pair (the PNG restore): bytes are the writer's, the first
+    failing item is redone by ``redo`` and raises, later items are not left behind."""
+    def writer(f, y):
+        if y == b"boom":
+            raise OSError("writer failed")
+        f.write(y)
+
+    def redo(path, y):
+        raise ValueError(f"redo {path.name}")
+
+    saver = stage_io.OrderedSaver(workers=2, writer=writer, redo=redo, largest_first=True)
+    paths = [tmp_path / f"f{i}.bin" for i in range(4)]
+    for i, (p, y) in enumerate(zip(paths, [b"a", b"bb", b"boom", b"dddd"])):
+        saver.submit(i, p, y, size=len(y))
+    with pytest.raises(ValueError, match="redo f2.bin"):
+        saver.commit()
+    assert saver.failed_index == 2
+    saver.close()
+    assert paths[0].read_bytes() == b"a" and paths[1].read_bytes() == b"bb"
+    assert not paths[2].exists() and not paths[3].exists()
+    assert not list(tmp_path.glob(".*.part"))

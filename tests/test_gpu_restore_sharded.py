@@ -239,7 +239,11 @@ def test_halo_gate_two_streams_and_timeout():
     rb = torch.empty(hr, dtype=torch.int16, device=DEV)  # b's right halo = a's head
     st_a = torch.full((1,), -1, dtype=torch.int32, device=DEV)
     st_b = torch.full((1,), -1, dtype=torch.int32, device=DEV)
-    s1, s2 = torch.cuda.Stream(device=DEV), torch.cuda.Stream(device=DEV)
+    # the two gates wait on each other, so they must run at the same time: two streams of one
+    # priority may share a hardware queue (GPU_MAX_HW_QUEUES, after the streams other tests made),
+    # where the second gate would queue behind the first until it times out (seen once in a
+    # subset run); a high-priority stream is served by a queue of its own priority
+    s1, s2 = torch.cuda.Stream(device=DEV), torch.cuda.Stream(device=DEV, priority=-1)
     torch.cuda.synchronize()
     for step in range(5):
         a.add_(step + 1)

@@ -134,6 +134,10 @@ for s in $STEPS; do
                  SQ_INSTS_MFMA --kernel-trace -d "$OUT/sq_lt257b" -o run --output-format csv -- \
                  python tools/long_taps_one.py 257 u8 6; fatal $? ;;
         asan) run asan 600 make -C warmup-fir-filter_amd/csrc asan-check; fatal $? ;;
+        stagemicro) run stage_micro 200 tools/microbench/stage_micro 15; fatal $? ;;
+        pipetime) run pipeline_timing 300 python tools/pipeline_timing.py; fatal $? ;;
+        restoreprobe) run restore_probe 300 python tools/restore_stage_probe.py; fatal $? ;;
+        reportprobe) run report_probe 300 python tools/report_stage_probe.py; fatal $? ;;
         micro) run micro 300 tools/microbench/fir_micro 28 20; fatal $? ;;
         micro2d) run micro2d 300 tools/microbench/fir2d_micro 15; fatal $? ;;
         microideal) run microideal 300 tools/microbench/ideal_micro 15; fatal $? ;;

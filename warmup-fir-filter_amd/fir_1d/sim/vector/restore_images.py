@@ -5,9 +5,16 @@ file-name pattern, output sub-directories ``{kind}_{tap}tap[_{policy}]``, skip /
 behaviour and summary dict).  The u8 conversions run on the GPU (``fir_restore_u8``,
 SURVEY §8(f) 4) with the reference's arithmetic: ``clip`` = rint + clip to [0,255]
 (:51-54), ``normalize`` = min/max rescale (:57-64); fixed outputs are already uint8.
-PNG encoding is host I/O (Pillow, whose zlib step releases the GIL): the files are
-encoded on a small thread pool while the next arrays convert on the GPU; the summary and
-its order are the reference's.
+PNG encoding is host I/O (Pillow, whose zlib step releases the GIL) and most of the stage's
+time (7 s of single-core encoding for the pipeline's 112 images, 272 M pixels): the main thread
+walks the inputs in the reference's order -- name checks, np.load, the u8 conversion, the
+skip-if-exists check, each where the reference does them -- and hands every image to a pool of
+PNG writers that takes the largest pending image first (stage_io.OrderedSaver on a
+LargestFirstPool), so the 13.5 M-pixel images start early and the small ones fill the tail.  The
+files are encoded under temporary names and renamed into place in the reference's order; the
+first image whose encoding fails is redone as the reference's own save call, which raises its
+error after every image before it and none after it.  The summary and its order are the
+reference's.
 """
 from __future__ import annotations
 
@@ -15,7 +22,6 @@ import argparse
 import json
 import os
 import re
-from concurrent.futures import ThreadPoolExecutor
 from datetime import datetime, timezone
 from pathlib import Path
 from time import perf_counter
@@ -24,6 +30,8 @@ from typing import Any
 import numpy as np
 
 import fir_hip
+
+from . import stage_io
 
 THIS_FILE = Path(__file__).resolve()
 DEFAULT_VECTOR_OUTPUT_DIR = THIS_FILE.parent / "output"
@@ -61,6 +69,32 @@ def _selected(value: str, valid: tuple[str, ...]) -> list[str]:
     return list(valid) if value == "all" else [value]
 
 
+def png_workers() -> int:
+    """PNG encoder threads: FIR_RESTORE_WRITERS, else the CPUs this process may run on, at most 16."""
+    env = os.environ.get("FIR_RESTORE_WRITERS")
+    if env:
+        return max(1, int(env))
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def _png_write(f, img: np.ndarray) -> None:
+    from PIL import Image
+    Image.fromarray(img, mode="L").save(f, format="PNG")
+
+
+def _png_redo(path: Path, img: np.ndarray) -> None:
+    from PIL import Image
+    Image.fromarray(img, mode="L").save(path)  # the reference's call (restore_images.py:194-195)
+
+
+def _pixel_range(rec: dict, img: np.ndarray) -> None:
+    rec["pixel_min"], rec["pixel_max"] = int(img.min()), int(img.max())
+
+
 def restore_images(*, vector_output_dir: Path = DEFAULT_VECTOR_OUTPUT_DIR, output_img_dir: Path = DEFAULT_OUTPUT_IMG_DIR,
                    kind: str = "all", tap: str = "all", ideal_policy: str = "clip", overwrite: bool = False,
                    strict: bool = False) -> dict[str, Any]:
@@ -69,22 +103,33 @@ def restore_images(*, vector_output_dir: Path = DEFAULT_VECTOR_OUTPUT_DIR, outpu
         raise FileNotFoundError(f"Vector output directory not found: {vector_output_dir}")
     kinds, taps = _selected(kind, VALID_KINDS), _selected(tap, VALID_TAPS)
     try:
-        from PIL import Image
+        from PIL import Image  # noqa: F401 - the reference's backend check
     except ModuleNotFoundError as exc:
         raise RuntimeError("Pillow is required to write PNG images.") from exc
-    converted, skipped, pending = [], [], []
-    pool = ThreadPoolExecutor(max_workers=max(1, min(8, os.cpu_count() or 1)))
+    converted, skipped = [], []
+    made: list = []  # (items submitted before, directory) for each directory the walk created
+    ranges: list = []
+    saver = stage_io.OrderedSaver(workers=png_workers(), writer=_png_write, redo=_png_redo, largest_first=True)
     try:
-        _restore_all(kinds, taps, vector_output_dir, output_img_dir, ideal_policy, overwrite, strict, Image, pool,
-                     converted, skipped, pending)
-    except BaseException:
-        for f in pending:  # let the queued writes finish, then raise the stage's own error
-            f.exception()
-        pool.shutdown()
-        raise
-    for f in pending:  # every PNG written (or its write error raised) before returning
-        f.result()
-    pool.shutdown()
+        try:
+            _restore_all(kinds, taps, vector_output_dir, output_img_dir, ideal_policy, overwrite, strict, saver,
+                         converted, skipped, made, ranges)
+        finally:  # every image before the walk's end (or its error) is put in place, in order
+            try:
+                saver.commit()
+            except BaseException:
+                # the reference stopped at the failing image: the directories it never reached go
+                for before, d in reversed(made):
+                    if before > saver.failed_index:
+                        try:
+                            d.rmdir()
+                        except OSError:
+                            pass
+                raise
+            for f in ranges:
+                f.result()
+    finally:
+        saver.close()
     return {"generated_at_utc": datetime.now(timezone.utc).isoformat(),
             "config": {"vector_output_dir": str(vector_output_dir), "output_img_dir": str(output_img_dir),
                        "kind": kind, "tap": tap, "ideal_policy": ideal_policy, "overwrite": bool(overwrite),
@@ -92,8 +137,10 @@ def restore_images(*, vector_output_dir: Path = DEFAULT_VECTOR_OUTPUT_DIR, outpu
             "num_converted": len(converted), "num_skipped": len(skipped), "converted": converted, "skipped": skipped}
 
 
-def _restore_all(kinds, taps, vector_output_dir, output_img_dir, ideal_policy, overwrite, strict, Image, pool,
-                 converted, skipped, pending):
+def _restore_all(kinds, taps, vector_output_dir, output_img_dir, ideal_policy, overwrite, strict, saver,
+                 converted, skipped, made, ranges):
+    """The reference's loop (restore_images.py:128-213) with the PNG writes handed to ``saver``."""
+    pending: set[Path] = set()  # outputs written by earlier items (not yet renamed into place)
     for k in kinds:
         for t in taps:
             src = vector_output_dir / f"{k}_{t}tap"
@@ -104,7 +151,9 @@ def _restore_all(kinds, taps, vector_output_dir, output_img_dir, ideal_policy, o
                 continue
             dst = output_img_dir / (f"{k}_{t}tap_{ideal_policy}" if k == "ideal" and ideal_policy != "clip"
                                     else f"{k}_{t}tap")
+            new = [a for a in [dst, *dst.parents] if not a.exists()]
             dst.mkdir(parents=True, exist_ok=True)
+            made.extend((len(saver.items), a) for a in reversed(new))
             for p in sorted((q for q in src.glob("*.npy") if q.is_file()), key=lambda q: q.name.lower()):
                 m = FILENAME_RE.match(p.name)
                 if m is None:
@@ -118,16 +167,23 @@ def _restore_all(kinds, taps, vector_output_dir, output_img_dir, ideal_policy, o
                     if strict:
                         raise ValueError(f"Kind/tap mismatch in filename={p.name}, expected {k}_{t}tap")
                     continue
+                # load and convert first, as the reference does: an unreadable or non-2-D input
+                # raises even where its image already exists
+                img = _to_image_u8(np.load(p), k, ideal_policy)
                 out = dst / f"{p.stem}.png"
-                if out.exists() and not overwrite:
+                if (out.exists() or out in pending) and not overwrite:
                     skipped.append({"reason": "exists", "path": str(out)})
                     continue
-                img = _to_image_u8(np.load(p), k, ideal_policy)
-                pending.append(pool.submit(lambda im, o: Image.fromarray(im, mode="L").save(o), img, out))
-                converted.append({"input_npy": str(p), "output_img": str(out), "kind": k, "tap": f"{t}tap",
-                                  "ideal_policy": ideal_policy if k == "ideal" else "n/a",
-                                  "height": int(img.shape[0]), "width": int(img.shape[1]), "dtype": str(img.dtype),
-                                  "pixel_min": int(img.min()), "pixel_max": int(img.max())})
+                rec = {"input_npy": str(p), "output_img": str(out), "kind": k, "tap": f"{t}tap",
+                       "ideal_policy": ideal_policy if k == "ideal" else "n/a",
+                       "height": int(img.shape[0]), "width": int(img.shape[1]), "dtype": str(img.dtype),
+                       "pixel_min": None, "pixel_max": None}
+                index = len(saver.items)
+                saver.submit(index, out, img, size=img.size)
+                if img.size:  # the writer pool fills the pixel range (NumPy's reductions release the GIL)
+                    ranges.append(saver.pool.submit(_pixel_range, rec, img, size=img.size))
+                pending.add(out)
+                converted.append(rec)
 
 
 def _build_argparser() -> argparse.ArgumentParser:

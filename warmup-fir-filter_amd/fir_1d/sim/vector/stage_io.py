@@ -22,10 +22,11 @@ raises the reference's error (or succeeds, and the stage goes on).
 """
 from __future__ import annotations
 
+import heapq
 import os
 import threading
 import time
-from concurrent.futures import ThreadPoolExecutor
+from concurrent.futures import Future, ThreadPoolExecutor
 from pathlib import Path
 
 import numpy as np
@@ -138,34 +139,104 @@ def load_input_image_u8(path: Path) -> np.ndarray:
     return x if x.dtype == np.uint8 else x.astype(np.uint8)
 
 
+class LargestFirstPool:
+    """A thread pool whose idle workers take the LARGEST pending job first (submit(fn, *args,
+    size=n)): a stage's long jobs start early and the short ones fill the tail, instead of one long
+    job submitted late running alone at the end.  Same submit / shutdown surface as
+    ThreadPoolExecutor; workers start on demand."""
+
+    def __init__(self, max_workers: int):
+        self.max_workers = max(1, int(max_workers))
+        self._heap: list = []
+        self._seq = 0
+        self._cv = threading.Condition()
+        self._threads: list[threading.Thread] = []
+        self._idle = 0
+        self._closed = False
+
+    def submit(self, fn, *args, size: int = 0) -> Future:
+        fut: Future = Future()
+        with self._cv:
+            if self._closed:
+                raise RuntimeError("cannot submit after shutdown")
+            heapq.heappush(self._heap, (-int(size), self._seq, fut, fn, args))
+            self._seq += 1
+            if len(self._heap) > self._idle and len(self._threads) < self.max_workers:
+                t = threading.Thread(target=self._work, daemon=True)
+                self._threads.append(t)
+                t.start()
+            self._cv.notify()
+        return fut
+
+    def _work(self) -> None:
+        while True:
+            with self._cv:
+                self._idle += 1
+                while not self._heap and not self._closed:
+                    self._cv.wait()
+                self._idle -= 1
+                if not self._heap:
+                    return
+                _, _, fut, fn, args = heapq.heappop(self._heap)
+            if not fut.set_running_or_notify_cancel():
+                continue
+            try:
+                fut.set_result(fn(*args))
+            except BaseException as exc:  # noqa: BLE001 - handed to the future's owner
+                fut.set_exception(exc)
+
+    def shutdown(self, wait: bool = True) -> None:
+        with self._cv:
+            self._closed = True
+            self._cv.notify_all()
+        if wait:
+            for t in self._threads:
+                t.join()
+
+
+def _npy_write(f, y) -> None:
+    np.save(f, y)
+
+
 class OrderedSaver:
-    """np.save of a stage's outputs on a thread pool, committed in the stage's order.
+    """np.save (or another ``writer``) of a stage's outputs on a thread pool, committed in the
+    stage's order.
 
     submit(i, path, y) starts writing y (which must stay untouched until commit) to a temporary
     file beside ``path``; commit() renames them into place in index order.  The first item whose
     write failed, or whose existing target the reference's open(path, "wb") would refuse, is
-    redone as np.save(path, y) -- the reference's own call, which raises its error -- and every
-    later temporary file is removed, so the directory holds what the reference's sequential loop
-    would have left.  A target that is a symlink or has other hard links is written by
-    np.save(path, y) too, as the reference writes it (through the link, into the shared file)."""
+    redone as ``redo(path, y)`` -- the reference's own call (np.save(path, y) by default), which
+    raises its error -- and every later temporary file is removed, so the directory holds what the
+    reference's sequential loop would have left.  A target that is a symlink or has other hard
+    links is written by ``redo(path, y)`` too, as the reference writes it (through the link, into
+    the shared file).  ``writer(f, y)`` writes y to the open binary file f; ``largest_first`` runs
+    the writes on a LargestFirstPool (submit's ``size`` orders them)."""
 
-    def __init__(self, workers: int | None = None):
-        self.pool = ThreadPoolExecutor(max_workers=workers or save_workers())
+    def __init__(self, workers: int | None = None, writer=_npy_write, redo=None, largest_first: bool = False):
+        n = workers or save_workers()
+        self.pool = LargestFirstPool(n) if largest_first else ThreadPoolExecutor(max_workers=n)
+        self.writer = writer
+        self.redo = redo if redo is not None else np.save
         self.items: dict[int, tuple] = {}
+        self.failed_index = None  # the item whose redo raised in commit()
         self.write_s = 0.0
         self.commit_s = 0.0
         self._mu = threading.Lock()
 
-    def _write(self, tmp: Path, y: np.ndarray) -> None:
+    def _write(self, tmp: Path, y) -> None:
         t0 = time.perf_counter()
         with open(tmp, "wb") as f:
-            np.save(f, y)
+            self.writer(f, y)
         with self._mu:
             self.write_s += time.perf_counter() - t0
 
-    def submit(self, index: int, path: Path, y: np.ndarray) -> None:
+    def submit(self, index: int, path: Path, y, size: int = 0) -> None:
         tmp = path.with_name(f".{path.name}.{os.getpid()}.{threading.get_ident()}.{index}.part")
-        self.items[index] = (path, y, tmp, self.pool.submit(self._write, tmp, y))
+        if isinstance(self.pool, LargestFirstPool):
+            fut = self.pool.submit(self._write, tmp, y, size=size)
+        else:
+            fut = self.pool.submit(self._write, tmp, y)
+        self.items[index] = (path, y, tmp, fut)
 
     def commit(self) -> int:
         """Rename every submitted file into place in index order; returns how many were written.
@@ -199,7 +270,11 @@ class OrderedSaver:
                             pass
                     os.replace(tmp, path)
                 else:
-                    np.save(path, y)  # the reference's call: raises its error (or writes the file)
+                    try:
+                        self.redo(path, y)  # the reference's call: raises its error (or writes the file)
+                    except BaseException:
+                        self.failed_index = i
+                        raise
                 done += 1
         finally:
             self.discard()  # the temporary files of the items after a failure
