@@ -105,8 +105,13 @@ def test_largest_first_pool_runs_the_largest_pending_job_first():
     import threading
 
     pool = stage_io.LargestFirstPool(1)
-    gate, order = threading.Event(), []
-    held = pool.submit(gate.wait, size=0)
+    gate, started, order = threading.Event(), threading.Event(), []
+
+    def hold():
+        started.set()
+        return gate.wait()
+    held = pool.submit(hold, size=0)
+    assert started.wait(10)  # the one worker is busy before the others are queued
     futs = [pool.submit(order.append, s, size=s) for s in (3, 50, 7, 50, 1)]
     bad = pool.submit(lambda: 1 / 0, size=2)
     gate.set()

@@ -9,7 +9,8 @@ filtering it, so a halo read that is not ordered against the neighbours' writes 
 * ``xgmi``: fir_hip.sharded.XgmiHalo — the halo gate (csrc/halo_gate.hip) hands the edges over
   through IPC-mapped mailboxes with device atomics, then ONE FIR launch reads them;
 * ``xgmi_overlap``: the same gate on a high-priority side stream while the bulk kernel runs
-  (XgmiHalo.gate_async / join), then the edge kernel (bench.py's default N > 1 step);
+  (XgmiHalo.gate_async / join), then the edge kernel (bench.py with FIR_GATE_MODE=overlap; serial is
+  its default);
 * ``rccl``: fir_hip.sharded.HaloExchange — the message path (on this box over gloo, staged
   through the host, since RCCL refuses several ranks on one GPU; across GPUs the same op list
   runs on RCCL), bulk kernel then edge kernel.

@@ -69,6 +69,10 @@ def _selected(value: str, valid: tuple[str, ...]) -> list[str]:
     return list(valid) if value == "all" else [value]
 
 
+# Converted images waiting for (or in) their PNG encoding, at most this many pixels (bytes).
+INFLIGHT_BYTES = int(os.environ.get("FIR_RESTORE_INFLIGHT_BYTES", str(1 << 30)))
+
+
 def png_workers() -> int:
     """PNG encoder threads: FIR_RESTORE_WRITERS, else the CPUs this process may run on, at most 16."""
     env = os.environ.get("FIR_RESTORE_WRITERS")
@@ -115,19 +119,19 @@ def restore_images(*, vector_output_dir: Path = DEFAULT_VECTOR_OUTPUT_DIR, outpu
             _restore_all(kinds, taps, vector_output_dir, output_img_dir, ideal_policy, overwrite, strict, saver,
                          converted, skipped, made, ranges)
         finally:  # every image before the walk's end (or its error) is put in place, in order
-            try:
-                saver.commit()
-            except BaseException:
-                # the reference stopped at the failing image: the directories it never reached go
-                for before, d in reversed(made):
-                    if before > saver.failed_index:
-                        try:
-                            d.rmdir()
-                        except OSError:
-                            pass
-                raise
-            for f in ranges:
-                f.result()
+            saver.commit()
+        for f in ranges:
+            f.result()
+    except BaseException:
+        if saver.failed_index is not None:
+            # the reference stopped at the failing image: the directories it never reached go
+            for before, d in reversed(made):
+                if before > saver.failed_index:
+                    try:
+                        d.rmdir()
+                    except OSError:
+                        pass
+        raise
     finally:
         saver.close()
     return {"generated_at_utc": datetime.now(timezone.utc).isoformat(),
@@ -153,7 +157,7 @@ def _restore_all(kinds, taps, vector_output_dir, output_img_dir, ideal_policy, o
                                     else f"{k}_{t}tap")
             new = [a for a in [dst, *dst.parents] if not a.exists()]
             dst.mkdir(parents=True, exist_ok=True)
-            made.extend((len(saver.items), a) for a in reversed(new))
+            made.extend((saver.submitted, a) for a in reversed(new))
             for p in sorted((q for q in src.glob("*.npy") if q.is_file()), key=lambda q: q.name.lower()):
                 m = FILENAME_RE.match(p.name)
                 if m is None:
@@ -178,8 +182,10 @@ def _restore_all(kinds, taps, vector_output_dir, output_img_dir, ideal_policy, o
                        "ideal_policy": ideal_policy if k == "ideal" else "n/a",
                        "height": int(img.shape[0]), "width": int(img.shape[1]), "dtype": str(img.dtype),
                        "pixel_min": None, "pixel_max": None}
-                index = len(saver.items)
-                saver.submit(index, out, img, size=img.size)
+                while saver.items and saver.pending_size() + img.size > INFLIGHT_BYTES:
+                    saver.wait_oldest()  # bounded memory: the reference holds one image at a time
+                    saver.commit(ready_only=True)
+                saver.submit(saver.submitted, out, img, size=img.size)
                 if img.size:  # the writer pool fills the pixel range (NumPy's reductions release the GIL)
                     ranges.append(saver.pool.submit(_pixel_range, rec, img, size=img.size))
                 pending.add(out)

@@ -217,7 +217,8 @@ class OrderedSaver:
         self.pool = LargestFirstPool(n) if largest_first else ThreadPoolExecutor(max_workers=n)
         self.writer = writer
         self.redo = redo if redo is not None else np.save
-        self.items: dict[int, tuple] = {}
+        self.items: dict[int, tuple] = {}  # uncommitted: index -> (path, y, tmp, future, size)
+        self.submitted = 0
         self.failed_index = None  # the item whose redo raised in commit()
         self.write_s = 0.0
         self.commit_s = 0.0
@@ -236,11 +237,14 @@ class OrderedSaver:
             fut = self.pool.submit(self._write, tmp, y, size=size)
         else:
             fut = self.pool.submit(self._write, tmp, y)
-        self.items[index] = (path, y, tmp, fut)
+        self.items[index] = (path, y, tmp, fut, size)
+        self.submitted += 1
 
-    def commit(self) -> int:
+    def commit(self, ready_only: bool = False) -> int:
         """Rename every submitted file into place in index order; returns how many were written.
         Raises the first failing item's error (the reference's np.save), after the items before it.
+        ``ready_only``: commit only the leading items whose writes have finished (the rest stay
+        pending), so a long stage does not hold every output until its end.
 
         A replaced file's old contents are released by the pool, not here: the old file gets a
         second name first, so the rename only moves a link, and the pool unlinks the second names
@@ -249,43 +253,61 @@ class OrderedSaver:
         the stage's time)."""
         done, old = 0, []
         t0 = time.perf_counter()
+        failed = True
         try:
             for i in sorted(self.items):
-                path, y, tmp, fut = self.items[i]
-                ok = fut.exception() is None
-                if ok and (path.is_symlink() or (path.is_file() and path.stat().st_nlink > 1)):
-                    ok = False  # np.save writes through a link (every name of the file sees it): do that
-                if ok and path.exists():
-                    try:  # the access check open(path, "wb") makes, without truncating the file
-                        os.close(os.open(path, os.O_WRONLY))
-                    except OSError:
-                        ok = False
-                if ok:
-                    if path.is_file():
-                        keep = tmp.with_name(tmp.name + ".old")
-                        try:
-                            os.link(path, keep)
-                            old.append(keep)
-                        except OSError:  # no hard links here: the rename frees the old file itself
-                            pass
-                    os.replace(tmp, path)
-                else:
-                    try:
-                        self.redo(path, y)  # the reference's call: raises its error (or writes the file)
-                    except BaseException:
-                        self.failed_index = i
-                        raise
+                if ready_only and not self.items[i][3].done():
+                    break
+                self._commit_item(i, old)
                 done += 1
+            failed = False
         finally:
-            self.discard()  # the temporary files of the items after a failure
+            if failed or not ready_only:
+                self.discard()  # the temporary files of the items after a failure
             for f in [self.pool.submit(os.unlink, p) for p in old]:
                 f.exception()
             self.commit_s += time.perf_counter() - t0
         return done
 
+    def _commit_item(self, i: int, old: list) -> None:
+        path, y, tmp, fut, _ = self.items[i]
+        ok = fut.exception() is None
+        if ok and (path.is_symlink() or (path.is_file() and path.stat().st_nlink > 1)):
+            ok = False  # np.save writes through a link (every name of the file sees it): do that
+        if ok and path.exists():
+            try:  # the access check open(path, "wb") makes, without truncating the file
+                os.close(os.open(path, os.O_WRONLY))
+            except OSError:
+                ok = False
+        if ok:
+            if path.is_file():
+                keep = tmp.with_name(tmp.name + ".old")
+                try:
+                    os.link(path, keep)
+                    old.append(keep)
+                except OSError:  # no hard links here: the rename frees the old file itself
+                    pass
+            os.replace(tmp, path)
+        else:
+            try:
+                self.redo(path, y)  # the reference's call: raises its error (or writes the file)
+            except BaseException:
+                self.failed_index = i
+                raise
+        del self.items[i]  # committed: its buffer is released
+
+    def pending_size(self) -> int:
+        """Sum of the ``size`` of the submitted, uncommitted items."""
+        return sum(it[4] for it in self.items.values())
+
+    def wait_oldest(self) -> None:
+        """Block until the first uncommitted item's write has finished (or failed)."""
+        if self.items:
+            self.items[min(self.items)][3].exception()
+
     def discard(self) -> None:
         """Drop every uncommitted item (a device error ended the stage): wait, remove its file."""
-        for path, y, tmp, fut in self.items.values():
+        for path, y, tmp, fut, _ in self.items.values():
             fut.exception()
             try:
                 tmp.unlink()
@@ -443,7 +465,7 @@ def _run_window(window: list, compute, out_dtype, saver: OrderedSaver, tm: dict)
         tm[k] += timing.get(k, 0.0)
     tm["device_calls"] += timing.get("calls", 1)
     t1 = time.perf_counter()
-    for *_, fut in saver.items.values():
-        fut.exception()
+    for it in saver.items.values():
+        it[3].exception()
     tm["save_tail_ms"] += (time.perf_counter() - t1) * 1e3
     return stop
