@@ -15,6 +15,8 @@
 
 static int failures = 0;
 
+static void count_plane(void* ctx, int plane) { ++((int*)ctx)[plane]; }
+
 static void expect(int cond, const char* what) {
     if (!cond) {
         fprintf(stderr, "FAIL: %s (%s)\n", what, fir_last_error());
@@ -112,6 +114,79 @@ int main(void) {
         free(x8);
         free(y8);
     }
+    /* the stage entries (ABI 6): 8 ragged images x 3 filters from page-locked and pageable memory,
+     * every plane reported once by the callback, results equal to the per-image bank call */
+    {
+        enum { NI = 8, NF = 3 };
+        const int64_t rows[NI] = {3, 1, 5, 2, 7, 1, 4, 2}, widths[NI] = {4499, 64, 17, 1, 640, 4096, 33, 0};
+        const int32_t bank[NF * 3] = {1365, 1365, 1365, -4096, 0, 4096, -512, 5120, -512};
+        const double hd[NF * 3] = {0.25, 0.5, 0.25, -1.0, 0.0, 1.0, -0.125, 1.25, -0.125};
+        void* pinned = NULL;
+        expect(fir_host_alloc(0, &pinned) == FIR_OK && pinned == NULL, "host alloc 0");
+        int64_t total = 0;
+        for (int i = 0; i < NI; ++i) total += rows[i] * widths[i];
+        expect(fir_host_alloc(total, &pinned) == FIR_OK && pinned != NULL, "host alloc");
+        const void* xs[NI];
+        void* yp[NI * NF];
+        void* yd[NI * NF];
+        uint8_t* xpage = malloc((size_t)total);
+        int64_t off = 0;
+        for (int i = 0; i < NI; ++i) {
+            const int64_t n = rows[i] * widths[i];
+            for (int64_t k = 0; k < n; ++k) ((uint8_t*)pinned)[off + k] = xpage[off + k] = (uint8_t)(k * 29 + i);
+            xs[i] = (const uint8_t*)pinned + off;
+            for (int f = 0; f < NF; ++f) {
+                yp[i * NF + f] = malloc((size_t)(n ? n : 1));
+                yd[i * NF + f] = malloc((size_t)(n ? n : 1) * 8);
+            }
+            off += n;
+        }
+        int seen[NI * NF] = {0};
+        double tm[FIR_TIMING_SLOTS] = {0};
+        expect(fir1d_fixed_images_multi(NI, xs, rows, widths, FIR_IN_U8, 1, bank, 3, NF, 12, 32, FIR_OUT_U8_SAT, yp, 0,
+                                        count_plane, seen, tm) == FIR_OK, "fixed images multi");
+        for (int p = 0; p < NI * NF; ++p) expect(seen[p] == 1, "every plane reported once");
+        expect(tm[3] > 0.0, "timing");
+        /* each image against the per-image fused bank */
+        off = 0;
+        for (int i = 0; i < NI; ++i) {
+            const int64_t n = rows[i] * widths[i];
+            if (n) {
+                uint8_t* ref = malloc((size_t)n * NF);
+                expect(fir1d_fixed_rows_multi(xpage + off, FIR_IN_U8, rows[i], widths[i], 1, bank, 3, NF, 12, 32,
+                                              FIR_OUT_U8_SAT, ref, 0) == FIR_OK, "bank per image");
+                for (int f = 0; f < NF; ++f)
+                    expect(memcmp(ref + f * n, yp[i * NF + f], (size_t)n) == 0, "batch plane == bank plane");
+                free(ref);
+            }
+            off += n;
+        }
+        /* pageable inputs, no callback, no timing */
+        off = 0;
+        for (int i = 0; i < NI; ++i) {
+            xs[i] = xpage + off;
+            off += rows[i] * widths[i];
+        }
+        expect(fir1d_fixed_images_multi(NI, xs, rows, widths, FIR_IN_U8, 1, bank, 3, NF, 12, 32, FIR_OUT_U8_SAT, yp, 0,
+                                        NULL, NULL, NULL) == FIR_OK, "fixed images multi pageable");
+        memset(seen, 0, sizeof seen);
+        expect(fir1d_ideal_images_multi(NI, (const uint8_t* const*)xs, rows, widths, hd, 3, NF, (double* const*)yd, 0,
+                                        count_plane, seen, tm) == FIR_OK, "ideal images multi");
+        for (int p = 0; p < NI * NF; ++p) expect(seen[p] == 1, "every ideal plane reported once");
+        expect(fir1d_fixed_images_multi(0, xs, rows, widths, FIR_IN_U8, 1, bank, 3, NF, 12, 32, FIR_OUT_U8_SAT, yp, 0,
+                                        NULL, NULL, NULL) == FIR_OK, "no images");
+        expect(fir1d_fixed_images_multi(NI, xs, rows, widths, FIR_IN_U8, 1, bank, 3, NF, 12, 32, FIR_OUT_U8_SAT, NULL,
+                                        0, NULL, NULL, NULL) == FIR_EINVAL, "null planes");
+        for (int p = 0; p < NI * NF; ++p) {
+            free(yp[p]);
+            free(yd[p]);
+        }
+        free(xpage);
+        expect(fir_host_free(pinned) == FIR_OK, "host free");
+        expect(fir_host_free(NULL) == FIR_OK, "host free null");
+    }
+    expect(fir_build_id() != NULL && strlen(fir_build_id()) > 0, "build id");
+    expect(fir_metrics_work_bytes(1 << 20) > 0 && fir_restore_work_bytes() > 0, "work sizes");
     static uint8_t one = 1;
     expect(fir1d_fixed_rows_sharded(&one, 0, 1, 1, 1, h3, 3, 12, 32, 0, NULL, devs, 1) == FIR_EINVAL, "null y");
     printf("capi_check: device present, %d failure(s)\n", failures);

@@ -134,6 +134,8 @@ for s in $STEPS; do
                  SQ_INSTS_MFMA --kernel-trace -d "$OUT/sq_lt257b" -o run --output-format csv -- \
                  python tools/long_taps_one.py 257 u8 6; fatal $? ;;
         asan) run asan 600 make -C warmup-fir-filter_amd/csrc asan-check; fatal $? ;;
+        asanbin) run asan 300 env LD_LIBRARY_PATH=tools/asan_bin ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 \
+                 tools/asan_bin/capi_check; fatal $? ;;
         stagemicro) run stage_micro 200 tools/microbench/stage_micro 15; fatal $? ;;
         pipetime) run pipeline_timing 300 python tools/pipeline_timing.py; fatal $? ;;
         restoreprobe) run restore_probe 300 python tools/restore_stage_probe.py; fatal $? ;;
