@@ -99,8 +99,10 @@ def test_u8_list_fast_path_rate():
 
     row = np.random.default_rng(3).integers(0, 256, 4499).astype(np.uint8).tolist()
     _prepare_x_u8(row)
-    t0 = time.perf_counter()
-    for _ in range(200):
-        _prepare_x_u8(row)
-    per_call = (time.perf_counter() - t0) / 200
-    assert per_call < 40e-6, per_call
+    best = float("inf")
+    for _ in range(10):  # best of 10 batches: other processes sharing the CPU only slow some batches
+        t0 = time.perf_counter()
+        for _ in range(50):
+            _prepare_x_u8(row)
+        best = min(best, (time.perf_counter() - t0) / 50)
+    assert best < 40e-6, best

@@ -83,3 +83,33 @@ def test_stage_driver_matches_reference_with_oracle_compute(scn, batch_bytes, re
     want = BY_NAME[scn["name"]]
     assert (got["returned"], got["error"], got["files"]) == (want["returned"], want["error"], want["files"])
     assert not list((tmp_path / "output").rglob(".*.part"))  # no temporary file left behind
+
+
+def test_device_error_in_a_later_window_keeps_the_earlier_windows(tmp_path, monkeypatch):
+    """A device call that fails in window 3 of a pipelined stage (the next window's reads and the
+    previous window's writes run under each call): the outputs of the windows before it are put
+    in place -- the reference's files for those images -- the failing window's planes are not, no
+    temporary file is left, and the device error is raised."""
+    import fir_hip
+    from fir_1d.sim.vector import stage_io
+
+    _oracle_batches(monkeypatch)
+    good = fir_hip.fir1d_fixed_images_multi
+    calls = []
+
+    def failing(xs, *a, **kw):
+        calls.append(len(xs))
+        if len(calls) == 3:
+            raise fir_hip.FirHipError("injected device failure")
+        return good(xs, *a, **kw)
+
+    monkeypatch.setattr(fir_hip, "fir1d_fixed_images_multi", failing)
+    monkeypatch.setattr(stage_io, "BATCH_BYTES", 4096)  # one image per window
+    scn = next(s for s in S.SCENARIOS if s["name"] == "fixed_ten_images")
+    got = S.run(scn, tmp_path, gf._generate_fixed_outputs_for_tap_map, gi._generate_ideal_outputs_for_tap_map)
+    assert got["error"] == ["FirHipError", "injected device failure"]
+    want = BY_NAME["fixed_ten_images"]["files"]
+    nsets = len(want) // 10
+    first_two = dict(sorted(want.items())[:2 * nsets])  # the images of windows 1 and 2
+    assert got["files"] == first_two
+    assert not list((tmp_path / "output").rglob(".*.part"))

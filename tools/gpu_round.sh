@@ -140,6 +140,7 @@ for s in $STEPS; do
         pipetime) run pipeline_timing 300 python tools/pipeline_timing.py; fatal $? ;;
         stagewall) run stage_wall 300 python tools/stage_wall_probe.py; fatal $? ;;
         stagewall1) run stage_wall_1reader 300 env FIR_STAGE_READERS=1 FIR_STAGE_READ_CHUNK=0 python tools/stage_wall_probe.py; fatal $? ;;
+        bigstage) run big_stage 300 python tools/big_stage_probe.py 40; fatal $? ;;
         restoreprobe) run restore_probe 300 python tools/restore_stage_probe.py; fatal $? ;;
         reportprobe) run report_probe 300 python tools/report_stage_probe.py; fatal $? ;;
         micro) run micro 300 tools/microbench/fir_micro 28 20; fatal $? ;;

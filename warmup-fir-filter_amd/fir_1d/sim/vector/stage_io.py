@@ -270,11 +270,12 @@ class OrderedSaver:
         self.items[index] = (path, y, tmp, fut, size)
         self.submitted += 1
 
-    def commit(self, ready_only: bool = False) -> int:
+    def commit(self, ready_only: bool = False, limit: int | None = None) -> int:
         """Rename every submitted file into place in index order; returns how many were written.
         Raises the first failing item's error (the reference's np.save), after the items before it.
         ``ready_only``: commit only the leading items whose writes have finished (the rest stay
-        pending), so a long stage does not hold every output until its end.
+        pending), so a long stage does not hold every output until its end.  ``limit``: commit only
+        the items with an index below it (the rest stay pending).
 
         A replaced file's old contents are released by the pool, not here: the old file gets a
         second name first, so the rename only moves a link, and the pool unlinks the second names
@@ -286,13 +287,13 @@ class OrderedSaver:
         failed = True
         try:
             for i in sorted(self.items):
-                if ready_only and not self.items[i][3].done():
+                if (limit is not None and i >= limit) or (ready_only and not self.items[i][3].done()):
                     break
                 self._commit_item(i, old)
                 done += 1
             failed = False
         finally:
-            if failed or not ready_only:
+            if failed or not (ready_only or limit is not None):
                 self.discard()  # the temporary files of the items after a failure
             for f in [self.pool.submit(os.unlink, p) for p in old]:
                 f.exception()
@@ -402,27 +403,32 @@ def run_image_stage(inputs: list[Path], stem_of, plan_items, compute, out_dtype,
     tm["plan_ms"] = (time.perf_counter() - t_start) * 1e3
     saver = OrderedSaver()
     written = 0
+    windows = _windows(planned, out_dtype)
+    # the first output of each window (None: the window writes nothing)
+    firsts = [min((o for im in w for o, _, _ in im.items), default=None) for w in windows]
+    pre = None
     try:
-        i0 = 0
-        while i0 < len(planned):
-            # one device call's window of images: image-aligned, <= BATCH_BYTES of staging
-            i1, nbytes = i0, 0
-            while i1 < len(planned):
-                im = planned[i1]
-                keys = {k for _, _, k in im.items}
-                b = _align(im.shape[0] * im.shape[1]) * (1 + 8 * len(keys))
-                if i1 > i0 and nbytes + b > BATCH_BYTES:
-                    break
-                nbytes += b
-                i1 += 1
-            window = planned[i0:i1]
-            stop = _run_window(window, compute, out_dtype, saver, tm)
-            written += saver.commit()
+        if windows:
+            pre = _prefetch(windows[0], 0, tm)
+        for k, window in enumerate(windows):
+            xs_all, cut, stop = _judge(pre, tm)
+            pre = None
+            if stop is None and k + 1 < len(windows):  # the next window's reads run under this call
+                pre = _prefetch(windows[k + 1], (k + 1) % 2, tm)
+            try:
+                _compute_window(window[:cut], xs_all, compute, out_dtype, saver, tm, k % 2)
+            finally:  # the previous window's writes ran under this call: put them in place
+                if k > 0:
+                    _wait_writes(saver, firsts[k], tm)
+                    written += saver.commit(limit=firsts[k])
             if stop is not None:  # an input np.load refuses, found at its turn
                 error = stop
                 break
-            i0 = i1
+        _wait_writes(saver, None, tm)
+        written += saver.commit()
     finally:
+        if pre is not None:  # no read may still be filling the staging
+            _drain(pre)
         saver.close()
         tm["files"] = written
         tm["save_write_ms"] = saver.write_s * 1e3
@@ -435,15 +441,42 @@ def run_image_stage(inputs: list[Path], stem_of, plan_items, compute, out_dtype,
     return written
 
 
-def _run_window(window: list, compute, out_dtype, saver: OrderedSaver, tm: dict):
-    """Load, compute and submit one window of planned images; returns the load error that cuts
-    the window short (the images before it are still computed and saved), else None."""
-    ar = arena()
+def _windows(planned: list, out_dtype) -> list:
+    """The stage's device calls: image-aligned windows of planned images, each needing its input and
+    one plane of out_dtype per coefficient set in page-locked staging.  A stage that fits in
+    BATCH_BYTES is one window; a larger one is cut into windows of at most BATCH_BYTES / 2, so two of
+    them (the one on the device, the next one being read) share the same staging budget."""
+    isz = np.dtype(out_dtype).itemsize
+
+    def need(im):
+        n = im.shape[0] * im.shape[1]
+        return _align(n) + _align(n * isz) * len({k for _, _, k in im.items})
+
+    cap = BATCH_BYTES if sum(need(im) for im in planned) <= BATCH_BYTES else BATCH_BYTES // 2
+    out, i0 = [], 0
+    while i0 < len(planned):
+        i1, nbytes = i0, 0
+        while i1 < len(planned):
+            b = need(planned[i1])
+            if i1 > i0 and nbytes + b > cap:
+                break
+            nbytes += b
+            i1 += 1
+        out.append(planned[i0:i1])
+        i0 = i1
+    return out
+
+
+def _slot(name: str, slot: int) -> str:
+    return name if slot == 0 else f"{name}{slot}"
+
+
+def _prefetch(window: list, slot: int, tm: dict):
+    """Start reading a window's plain inputs into its staging slot (reader pool, in pieces)."""
     t0 = time.perf_counter()
     fast = [im for im in window if im.array is None]
-    in_buf = ar.take("in", sum(_align(im.shape[0] * im.shape[1]) for im in fast))
-    off, stop, cut = 0, None, len(window)
-    reads = []  # every plain input read at once, by the reader pool, in pieces
+    in_buf = arena().take(_slot("in", slot), sum(_align(im.shape[0] * im.shape[1]) for im in fast))
+    off, reads = 0, []
     for im in window:
         if im.array is not None:
             reads.append(None)
@@ -452,9 +485,26 @@ def _run_window(window: list, compute, out_dtype, saver: OrderedSaver, tm: dict)
         view = in_buf[off:off + n].reshape(im.shape)
         off += _align(n)
         reads.append((view, read_into_async(im.path, im.off, view)))
-    xs_all = []
+    tm["load_ms"] += (time.perf_counter() - t0) * 1e3
+    return window, reads
+
+
+def _drain(pre) -> None:
+    for r in pre[1]:
+        if r is not None:
+            for f in r[1]:
+                f.exception()
+
+
+def _judge(pre, tm: dict):
+    """Wait for a window's reads and judge its inputs in the stage's order: (arrays, cut, error) --
+    an input whose data did not come is np.load'ed (the reference's call), and one np.load refuses
+    cuts the window there (the images before it are still computed and saved)."""
+    window, reads = pre
+    t0 = time.perf_counter()
+    xs_all, stop, cut = [], None, len(window)
     try:
-        for k, im in enumerate(window):  # judged in the stage's order
+        for k, im in enumerate(window):
             if im.array is not None:
                 xs_all.append(im.array)
                 continue
@@ -466,13 +516,23 @@ def _run_window(window: list, compute, out_dtype, saver: OrderedSaver, tm: dict)
                     stop, cut = exc, k
                     break
             xs_all.append(view)
-    finally:  # no read may still be filling the staging when it is reused
-        for r in reads:
-            if r is not None:
-                for f in r[1]:
-                    f.exception()
+    finally:
+        _drain(pre)
     tm["load_ms"] += (time.perf_counter() - t0) * 1e3
-    window, xs_all = window[:cut], xs_all[:cut]
+    return xs_all, cut, stop
+
+
+def _wait_writes(saver: OrderedSaver, limit, tm: dict) -> None:
+    """Wait for the writes of the items before ``limit`` (all: None)."""
+    t1 = time.perf_counter()
+    for i, it in list(saver.items.items()):
+        if limit is None or i < limit:
+            it[3].exception()
+    tm["save_tail_ms"] += (time.perf_counter() - t1) * 1e3
+
+
+def _compute_window(window: list, xs_all: list, compute, out_dtype, saver: OrderedSaver, tm: dict, slot: int):
+    """Compute one judged window and hand its planes to the saver as they land (not waited for)."""
     gpu = [(im, x) for im, x in zip(window, xs_all) if im.items and x.size]
     for im, x in zip(window, xs_all):  # empty images: the reference writes empty arrays, no compute
         if im.items and not x.size:
@@ -485,9 +545,9 @@ def _run_window(window: list, compute, out_dtype, saver: OrderedSaver, tm: dict)
             if k not in keys:
                 keys.append(k)
     if not gpu or not keys:
-        return stop
+        return
     isz = np.dtype(out_dtype).itemsize
-    out_buf = ar.take("out", sum(_align(x.size * isz) * len(keys) for _, x in gpu))
+    out_buf = arena().take(_slot("out", slot), sum(_align(x.size * isz) * len(keys) for _, x in gpu))
     outs, off = [], 0
     for _, x in gpu:
         planes = []
@@ -507,8 +567,3 @@ def _run_window(window: list, compute, out_dtype, saver: OrderedSaver, tm: dict)
     for k in ("h2d_ms", "kernel_ms", "d2h_ms", "call_ms"):
         tm[k] += timing.get(k, 0.0)
     tm["device_calls"] += timing.get("calls", 1)
-    t1 = time.perf_counter()
-    for it in saver.items.values():
-        it[3].exception()
-    tm["save_tail_ms"] += (time.perf_counter() - t1) * 1e3
-    return stop
