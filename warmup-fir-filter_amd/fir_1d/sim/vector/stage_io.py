@@ -250,6 +250,7 @@ class OrderedSaver:
         self.items: dict[int, tuple] = {}  # uncommitted: index -> (path, y, tmp, future, size)
         self.submitted = 0
         self.failed_index = None  # the item whose redo raised in commit()
+        self._side = None  # commit's own jobs when the writes run on a FIFO pool
         self.write_s = 0.0
         self.commit_s = 0.0
         self._mu = threading.Lock()
@@ -295,7 +296,7 @@ class OrderedSaver:
         finally:
             if failed or not (ready_only or limit is not None):
                 self.discard()  # the temporary files of the items after a failure
-            for f in [self.pool.submit(os.unlink, p) for p in old]:
+            for f in [self._submit_first(os.unlink, p) for p in old]:
                 f.exception()
             self.commit_s += time.perf_counter() - t0
         return done
@@ -327,6 +328,15 @@ class OrderedSaver:
                 raise
         del self.items[i]  # committed: its buffer is released
 
+    def _submit_first(self, fn, *args):
+        """A job the committing thread waits for, ahead of every queued write (a pipelined stage
+        commits one window while the next window's writes are queued)."""
+        if isinstance(self.pool, LargestFirstPool):
+            return self.pool.submit(fn, *args, size=1 << 62)
+        if self._side is None:
+            self._side = ThreadPoolExecutor(max_workers=save_workers(), thread_name_prefix="fir-unlink")
+        return self._side.submit(fn, *args)
+
     def pending_size(self) -> int:
         """Sum of the ``size`` of the submitted, uncommitted items."""
         return sum(it[4] for it in self.items.values())
@@ -349,6 +359,8 @@ class OrderedSaver:
     def close(self) -> None:
         self.discard()
         self.pool.shutdown(wait=True)
+        if self._side is not None:
+            self._side.shutdown(wait=True)
 
 
 class PlannedImage:
