@@ -6,12 +6,10 @@ GPU metrics reduction) is fir_1d.sim.vector.gen_compare_report.
 """
 from __future__ import annotations
 
-import argparse
 from pathlib import Path
-from time import perf_counter
 from typing import Any
 
-from fir_1d.sim.vector.gen_compare_report import DEFAULT_OUTPUT_DIR, generate_compare_report
+from fir_1d.sim.vector.gen_compare_report import DEFAULT_OUTPUT_DIR, generate_compare_report, run_cli
 
 DEFAULT_IDEAL_5TAP_DIR = DEFAULT_OUTPUT_DIR / "ideal_5tap"
 DEFAULT_FIXED_5TAP_DIR = DEFAULT_OUTPUT_DIR / "fixed_5tap"
@@ -26,18 +24,8 @@ def generate_5tap_compare_report(*, ideal_dir: Path = DEFAULT_IDEAL_5TAP_DIR,
 
 
 def main(argv=None) -> int:
-    ap = argparse.ArgumentParser(description="Generate 5tap ideal/fixed comparison report (CSV/JSON + console summary).")
-    ap.add_argument("--ideal-dir", type=Path, default=DEFAULT_IDEAL_5TAP_DIR)
-    ap.add_argument("--fixed-dir", type=Path, default=DEFAULT_FIXED_5TAP_DIR)
-    ap.add_argument("--report-dir", type=Path, default=DEFAULT_REPORT_DIR)
-    ap.add_argument("--top-k", type=int, default=5)
-    ap.add_argument("--strict", action="store_true")
-    a = ap.parse_args(argv)
-    t0 = perf_counter()
-    r = generate_5tap_compare_report(ideal_dir=a.ideal_dir, fixed_dir=a.fixed_dir, report_dir=a.report_dir,
-                                      top_k=a.top_k, strict=a.strict)
-    print(f"[OK] gen_5tap_compare_report cases={r['num_cases']} elapsed={perf_counter() - t0:.2f}s")
-    return 0
+    return run_cli("5tap", generate_5tap_compare_report,
+                   (DEFAULT_IDEAL_5TAP_DIR, DEFAULT_FIXED_5TAP_DIR, DEFAULT_REPORT_DIR), argv)
 
 
 if __name__ == "__main__":

@@ -256,3 +256,30 @@ def generate_compare_report(tap: str, *, ideal_dir: Path, fixed_dir: Path, repor
         timings["wall_ms"] = round((time.perf_counter() - t_start) * 1e3, 3)
     return {"csv_path": str(csv_path), "json_path": str(json_path), "num_cases": overall["num_cases"],
             "num_samples_total": overall["num_samples_total"], "validation_has_issue": has_issue}
+
+
+def run_cli(tap: str, generate, defaults: tuple[Path, Path, Path], argv=None) -> int:
+    """The report programs' command line (gen_3tap_compare_report.py:404-475 and its 5-tap twin):
+    flags, the console summary, and the ``[OK]`` / ``[FAIL]`` status line, which names the CSV on
+    success and the report folder on failure; the error is raised after its line."""
+    import argparse
+
+    ap = argparse.ArgumentParser(description=f"Generate {tap} ideal/fixed comparison report (CSV/JSON + console summary).")
+    ap.add_argument("--ideal-dir", type=Path, default=defaults[0])
+    ap.add_argument("--fixed-dir", type=Path, default=defaults[1])
+    ap.add_argument("--report-dir", type=Path, default=defaults[2])
+    ap.add_argument("--top-k", type=int, default=5)
+    ap.add_argument("--strict", action="store_true")
+    a = ap.parse_args(argv)
+    name = f"gen_{tap}_compare_report"
+    t0 = time.perf_counter()
+    try:
+        r = generate(ideal_dir=a.ideal_dir, fixed_dir=a.fixed_dir, report_dir=a.report_dir, top_k=a.top_k,
+                     strict=a.strict)
+    except Exception as exc:
+        print(f"[FAIL] {name} file={name}.py generated=0 skipped=0 failed=1 "
+              f"elapsed={time.perf_counter() - t0:.2f}s out={a.report_dir.resolve()} error=\"{exc}\"")
+        raise
+    print(f"[OK] {name} file={name}.py generated={r['num_cases']} skipped=0 failed=0 "
+          f"elapsed={time.perf_counter() - t0:.2f}s out={r['csv_path']} validation_has_issue={r['validation_has_issue']}")
+    return 0

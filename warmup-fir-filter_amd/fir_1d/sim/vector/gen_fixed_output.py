@@ -246,8 +246,9 @@ def main(argv=None) -> int:
             expected += len(_iter_input_npy_files(in_dir)) * len(h_coeff_5tap_map)
             counts["fixed_5tap"] = generate_fixed_5tap_output_vector(**kw)
     except Exception as exc:
+        # the default folder, as the reference prints (:246-253)
         print(f"[FAIL] gen_fixed_output file=gen_fixed_output.py generated=0 skipped=0 failed=1 "
-              f"elapsed={perf_counter() - t0:.2f}s out={out_dir} error=\"{exc}\"")
+              f"elapsed={perf_counter() - t0:.2f}s out={DEFAULT_OUTPUT_DIR.resolve()} error=\"{exc}\"")
         raise
     total = sum(counts.values())
     print(f"[OK] gen_fixed_output file=gen_fixed_output.py generated={total} "

@@ -141,8 +141,9 @@ def main(argv=None) -> int:
             counts["ideal_5tap"] = generate_ideal_5tap_output_vector(in_dir, out_dir, overwrite=args.overwrite,
                                                                          devices=args.devices)
     except Exception as exc:
+        # the default folder, as the reference prints (:191-198)
         print(f"[FAIL] gen_ideal_output file=gen_ideal_output.py generated=0 skipped=0 failed=1 "
-              f"elapsed={perf_counter() - t0:.2f}s out={out_dir} error=\"{exc}\"")
+              f"elapsed={perf_counter() - t0:.2f}s out={DEFAULT_OUTPUT_DIR.resolve()} error=\"{exc}\"")
         raise
     total = sum(counts.values())
     print(f"[OK] gen_ideal_output file=gen_ideal_output.py generated={total} "
