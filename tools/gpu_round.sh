@@ -138,6 +138,7 @@ for s in $STEPS; do
                  tools/asan_bin/capi_check; fatal $? ;;
         stagemicro) run stage_micro 200 tools/microbench/stage_micro 15; fatal $? ;;
         pipetime) run pipeline_timing 300 python tools/pipeline_timing.py; fatal $? ;;
+        pipecold) run pipeline_timing_cold 300 python tools/pipeline_timing.py --cold; fatal $? ;;
         stagewall) run stage_wall 300 python tools/stage_wall_probe.py; fatal $? ;;
         stagewall1) run stage_wall_1reader 300 env FIR_STAGE_READERS=1 FIR_STAGE_READ_CHUNK=0 python tools/stage_wall_probe.py; fatal $? ;;
         bigstage) run big_stage 300 python tools/big_stage_probe.py 40; fatal $? ;;

@@ -16,6 +16,7 @@ SURVEY Appendix A).
 from __future__ import annotations
 
 import argparse
+import os
 import sys
 from pathlib import Path
 from time import perf_counter
@@ -54,6 +55,28 @@ def _log_stage(message: str) -> None:
     print(f"[pipeline] {message}")
 
 
+def _start_devices(devices):
+    """Bring the devices the vector stages will use up on a side thread (the HIP runtime, the
+    library's per-device state, its code objects: about 0.16 s per process) while the input stage
+    decodes on this one.  Best effort: a failure here is left for the stage itself to report."""
+    import threading
+
+    def warm():
+        try:
+            import numpy as np
+
+            import fir_hip
+
+            for d in dict.fromkeys(fir_hip.parse_devices(devices)):
+                fir_hip.fir1d_fixed_rows(np.zeros((1, 64), np.uint8), [1], device=d)
+        except Exception:  # noqa: BLE001 - the stages raise the real error
+            pass
+
+    t = threading.Thread(target=warm, name="fir-device-start", daemon=True)
+    t.start()
+    return t
+
+
 def run_pipeline(*, tap: str, overwrite_vectors: bool, skip_input: bool, skip_ideal: bool, skip_fixed: bool,
                  skip_report: bool, skip_restore: bool, restore_kind: str, ideal_policy: str, overwrite_images: bool,
                  strict_report: bool, strict_restore: bool, top_k: int, image_dir: Path | None = None,
@@ -63,10 +86,18 @@ def run_pipeline(*, tap: str, overwrite_vectors: bool, skip_input: bool, skip_id
     vector_dir = Path(vector_dir)
     in_dir, out_dir = vector_dir / "input", vector_dir / "output"
     results: dict[str, Any] = {"selected_taps": taps}
+    starting = None
     if not skip_input:
+        if not (skip_ideal and skip_fixed and skip_report and skip_restore) and \
+                os.environ.get("FIR_PIPELINE_START_DEVICES", "1") != "0":
+            starting = _start_devices(devices)
         _log_stage("Generate input vectors")
-        results["input_manifest"] = generate_input_vector_jsons(image_dir or default_image_source(), in_dir,
-                                                                overwrite=overwrite_vectors)
+        try:
+            results["input_manifest"] = generate_input_vector_jsons(image_dir or default_image_source(), in_dir,
+                                                                    overwrite=overwrite_vectors)
+        finally:
+            if starting is not None:
+                starting.join()
     if not skip_ideal:
         _log_stage("Generate ideal outputs")
         gen = {"3": generate_ideal_3tap_output_vector, "5": generate_ideal_5tap_output_vector}
