@@ -45,13 +45,19 @@ struct Batch {
     int n;
 };
 
-__device__ __forceinline__ void st_nt(void* p, u32x4 v) {
-    asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+// store cache policy: 0 nt (the product's), 1 plain, 2 sc0 sc1, 3 sc1, 4 nt sc1
+template <int POL>
+__device__ __forceinline__ void st_pol(void* p, u32x4 v) {
+    if constexpr (POL == 0) asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 1) asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 3) asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+    else asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
 // MODE 0: copy to F planes; 1: stores only; 2: loads only (one sink store per wave if a value
 // matches a pattern no input has); 3: copy to one plane.  U chunks of 64 vectors per wave.
-template <int MODE, int U>
+template <int MODE, int U, int POL = 0>
 __global__ __launch_bounds__(256) void twin(Batch b) {
     const int64_t tile = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int i = 0;
@@ -89,7 +95,7 @@ __global__ __launch_bounds__(256) void twin(Batch b) {
         for (int f = 0; f < NF; ++f) {
             uint8_t* p = b.y[i][f] + 16 * v;
             if (16 * v + 16 <= total)
-                st_nt(p, d[u] + (uint32_t)f);
+                st_pol<POL>(p, d[u] + (uint32_t)f);
             else if (MODE == 1)
                 for (int k = 0; k < (int)(total - 16 * v); ++k) p[k] = (uint8_t)k;
             else
@@ -115,19 +121,19 @@ static Batch make_batch(uint8_t* const* x, uint8_t* const (*y)[kF], int U) {
 
 struct V {
     std::string name;
-    int mode, u;
+    int mode, u, pol;
     double bytes;
     std::vector<float> hbm, mall;
 };
 
-template <int MODE, int U>
+template <int MODE, int U, int POL = 0>
 static void launch(const Batch& b, hipStream_t s) {
     const int64_t blocks = (b.tile0[b.n] + 3) / 4;
-    hipLaunchKernelGGL((twin<MODE, U>), dim3((unsigned)blocks), dim3(256), 0, s, b);
+    hipLaunchKernelGGL((twin<MODE, U, POL>), dim3((unsigned)blocks), dim3(256), 0, s, b);
 }
 
 static void run(const V& v, const Batch& b, hipStream_t s) {
-    switch (v.mode * 10 + v.u) {
+    switch (v.pol * 100 + v.mode * 10 + v.u) {
         case 1: launch<0, 1>(b, s); break;
         case 2: launch<0, 2>(b, s); break;
         case 4: launch<0, 4>(b, s); break;
@@ -135,6 +141,12 @@ static void run(const V& v, const Batch& b, hipStream_t s) {
         case 21: launch<2, 1>(b, s); break;
         case 24: launch<2, 4>(b, s); break;
         case 31: launch<3, 1>(b, s); break;
+        case 101: launch<0, 1, 1>(b, s); break;
+        case 201: launch<0, 1, 2>(b, s); break;
+        case 301: launch<0, 1, 3>(b, s); break;
+        case 401: launch<0, 1, 4>(b, s); break;
+        case 111: launch<1, 1, 1>(b, s); break;
+        case 211: launch<1, 1, 2>(b, s); break;
         default: fprintf(stderr, "bad variant\n"); exit(1);
     }
 }
@@ -165,13 +177,19 @@ int main(int argc, char** argv) {
     for (int s = 0; s < kSets; ++s)
         for (int k = 0; k < 3; ++k) bs[s][k] = make_batch(x[s], y[s], 1 << k);
     std::vector<V> vs = {
-        {"copy4 U=1 (batch layout)", 0, 1, px * 5.0, {}, {}},
-        {"copy4 U=2", 0, 2, px * 5.0, {}, {}},
-        {"copy4 U=4", 0, 4, px * 5.0, {}, {}},
-        {"write4 only", 1, 1, px * 4.0, {}, {}},
-        {"read only U=1", 2, 1, px * 1.0, {}, {}},
-        {"read only U=4", 2, 4, px * 1.0, {}, {}},
-        {"copy to one plane", 3, 1, px * 2.0, {}, {}},
+        {"copy4 U=1 (batch layout)", 0, 1, 0, px * 5.0, {}, {}},
+        {"copy4 U=2", 0, 2, 0, px * 5.0, {}, {}},
+        {"copy4 U=4", 0, 4, 0, px * 5.0, {}, {}},
+        {"write4 only", 1, 1, 0, px * 4.0, {}, {}},
+        {"read only U=1", 2, 1, 0, px * 1.0, {}, {}},
+        {"read only U=4", 2, 4, 0, px * 1.0, {}, {}},
+        {"copy to one plane", 3, 1, 0, px * 2.0, {}, {}},
+        {"copy4 U=1 plain stores", 0, 1, 1, px * 5.0, {}, {}},
+        {"copy4 U=1 sc0 sc1 stores", 0, 1, 2, px * 5.0, {}, {}},
+        {"copy4 U=1 sc1 stores", 0, 1, 3, px * 5.0, {}, {}},
+        {"copy4 U=1 nt sc1 stores", 0, 1, 4, px * 5.0, {}, {}},
+        {"write4 only plain", 1, 1, 1, px * 4.0, {}, {}},
+        {"write4 only sc0 sc1", 1, 1, 2, px * 4.0, {}, {}},
     };
     auto bidx = [](int u) { return u == 1 ? 0 : (u == 2 ? 1 : 2); };
     hipStream_t st;
