@@ -33,11 +33,11 @@ def test_every_scenario_has_a_reference_record():
     assert sorted(BY_NAME) == sorted(s["name"] for s in S.SCENARIOS)
 
 
-@pytest.mark.parametrize("workers,inflight,ahead", [(1, 1 << 30, 512 << 20), (3, 1 << 30, 512 << 20), (3, 64, 1)])
+@pytest.mark.parametrize("workers,inflight", [(1, 1 << 30), (3, 1 << 30), (3, 64)])
 @pytest.mark.parametrize("scn", S.SCENARIOS, ids=[s["name"] for s in S.SCENARIOS])
-def test_restore_matches_reference_with_oracle_conversions(scn, workers, inflight, ahead, tmp_path, monkeypatch):
+def test_restore_matches_reference_with_oracle_conversions(scn, workers, inflight, tmp_path, monkeypatch):
     """inflight = 64 pixels: every image waits for the ones before it to be written and committed
-    (the memory bound of a long restore); ahead = 1 byte: one input loaded ahead at a time."""
+    (the memory bound of a long restore)."""
     import numpy as np
 
     import fir_hip
@@ -45,7 +45,6 @@ def test_restore_matches_reference_with_oracle_conversions(scn, workers, infligh
     from oracle import fir_oracle as fo
 
     monkeypatch.setattr(ri, "INFLIGHT_BYTES", inflight)
-    monkeypatch.setattr(ri, "LOAD_AHEAD_BYTES", ahead)
 
     def restore_u8(a, policy=fir_hip.RESTORE_CLIP, device=0):
         arr = np.ascontiguousarray(a, dtype=np.float64)

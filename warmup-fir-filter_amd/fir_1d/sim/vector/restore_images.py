@@ -71,8 +71,6 @@ def _selected(value: str, valid: tuple[str, ...]) -> list[str]:
 
 # Converted images waiting for (or in) their PNG encoding, at most this many pixels (bytes).
 INFLIGHT_BYTES = int(os.environ.get("FIR_RESTORE_INFLIGHT_BYTES", str(1 << 30)))
-# Input files being loaded and converted ahead of the walk, at most this many bytes.
-LOAD_AHEAD_BYTES = int(os.environ.get("FIR_RESTORE_LOAD_AHEAD_BYTES", str(512 << 20)))
 
 
 def png_workers() -> int:
@@ -143,121 +141,55 @@ def restore_images(*, vector_output_dir: Path = DEFAULT_VECTOR_OUTPUT_DIR, outpu
             "num_converted": len(converted), "num_skipped": len(skipped), "converted": converted, "skipped": skipped}
 
 
-class _Loads:
-    """np.load + the u8 conversion of the walk's inputs, started ahead of the walk on a few threads
-    (at most LOAD_AHEAD_BYTES of files in flight) so the largest images reach the PNG writers
-    early; take(p) returns p's image or raises its error -- at p's turn in the walk, as the
-    reference's own np.load and conversion would."""
-
-    def __init__(self, todo: list, ideal_policy: str):
-        from concurrent.futures import ThreadPoolExecutor
-
-        self.todo, self.policy, self.next, self.ahead = todo, ideal_policy, 0, 0
-        self.futs: dict = {}
-        self.pool = ThreadPoolExecutor(max_workers=4, thread_name_prefix="fir-restore-load")
-        self._fill()
-
-    def _job(self, p: Path, k: str) -> np.ndarray:
-        return _to_image_u8(np.load(p), k, self.policy)
-
-    def _fill(self) -> None:
-        while self.next < len(self.todo) and (not self.futs or self.ahead < LOAD_AHEAD_BYTES):
-            p, k = self.todo[self.next]
-            try:
-                n = p.stat().st_size
-            except OSError:
-                n = 0
-            self.futs[p] = (self.pool.submit(self._job, p, k), n)
-            self.ahead += n
-            self.next += 1
-
-    def take(self, p: Path) -> np.ndarray:
-        fut, n = self.futs.pop(p)
-        self.ahead -= n
-        try:
-            return fut.result()
-        finally:
-            self._fill()
-
-    def close(self) -> None:
-        self.pool.shutdown(wait=True, cancel_futures=True)
-
-
-def _groups(kinds, taps, vector_output_dir):
-    """The walk's (kind, tap, input folder, its sorted .npy files or None when missing)."""
-    out = []
+def _restore_all(kinds, taps, vector_output_dir, output_img_dir, ideal_policy, overwrite, strict, saver,
+                 converted, skipped, made, ranges):
+    """The reference's loop (restore_images.py:128-213) with the PNG writes handed to ``saver``."""
+    pending: set[Path] = set()  # outputs written by earlier items (not yet renamed into place)
     for k in kinds:
         for t in taps:
             src = vector_output_dir / f"{k}_{t}tap"
-            files = sorted((q for q in src.glob("*.npy") if q.is_file()), key=lambda q: q.name.lower()) \
-                if src.exists() else None
-            out.append((k, t, src, files))
-    return out
-
-
-def _loadable(p: Path, k: str, t: str) -> bool:
-    m = FILENAME_RE.match(p.name)
-    return m is not None and m.group("kind") == k and m.group("tap") == t
-
-
-def _restore_all(kinds, taps, vector_output_dir, output_img_dir, ideal_policy, overwrite, strict, saver,
-                 converted, skipped, made, ranges):
-    """The reference's loop (restore_images.py:128-213) with the loads started ahead (_Loads) and
-    the PNG writes handed to ``saver``."""
-    groups = _groups(kinds, taps, vector_output_dir)
-    loads = _Loads([(p, k) for k, t, _, files in groups for p in (files or ()) if _loadable(p, k, t)], ideal_policy)
-    try:
-        _walk(groups, output_img_dir, ideal_policy, overwrite, strict, saver, converted, skipped, made, ranges,
-              loads)
-    finally:
-        loads.close()
-
-
-def _walk(groups, output_img_dir, ideal_policy, overwrite, strict, saver, converted, skipped, made, ranges, loads):
-    pending: set[Path] = set()  # outputs written by earlier items (not yet renamed into place)
-    for k, t, src, files in groups:
-        if files is None:
-            skipped.append({"reason": "missing_input_subdir", "kind": k, "tap": f"{t}tap", "path": str(src)})
-            if strict:
-                raise FileNotFoundError(f"Expected input subdir not found: {src}")
-            continue
-        dst = output_img_dir / (f"{k}_{t}tap_{ideal_policy}" if k == "ideal" and ideal_policy != "clip"
-                                else f"{k}_{t}tap")
-        new = [a for a in [dst, *dst.parents] if not a.exists()]
-        dst.mkdir(parents=True, exist_ok=True)
-        made.extend((saver.submitted, a) for a in reversed(new))
-        for p in files:
-            m = FILENAME_RE.match(p.name)
-            if m is None:
-                skipped.append({"reason": "invalid_filename", "path": str(p)})
+            if not src.exists():
+                skipped.append({"reason": "missing_input_subdir", "kind": k, "tap": f"{t}tap", "path": str(src)})
                 if strict:
-                    raise ValueError(f"Invalid vector filename: {p.name}")
+                    raise FileNotFoundError(f"Expected input subdir not found: {src}")
                 continue
-            if m.group("kind") != k or m.group("tap") != t:
-                skipped.append({"reason": "kind_tap_mismatch", "path": str(p), "expected_kind": k,
-                                "expected_tap": t, "file_kind": m.group("kind"), "file_tap": m.group("tap")})
-                if strict:
-                    raise ValueError(f"Kind/tap mismatch in filename={p.name}, expected {k}_{t}tap")
-                continue
-            # loaded and converted first, as the reference does: an unreadable or non-2-D input
-            # raises even where its image already exists
-            img = loads.take(p)
-            out = dst / f"{p.stem}.png"
-            if (out.exists() or out in pending) and not overwrite:
-                skipped.append({"reason": "exists", "path": str(out)})
-                continue
-            rec = {"input_npy": str(p), "output_img": str(out), "kind": k, "tap": f"{t}tap",
-                   "ideal_policy": ideal_policy if k == "ideal" else "n/a",
-                   "height": int(img.shape[0]), "width": int(img.shape[1]), "dtype": str(img.dtype),
-                   "pixel_min": None, "pixel_max": None}
-            while saver.items and saver.pending_size() + img.size > INFLIGHT_BYTES:
-                saver.wait_oldest()  # bounded memory: the reference holds one image at a time
-                saver.commit(ready_only=True)
-            saver.submit(saver.submitted, out, img, size=img.size)
-            if img.size:  # the writer pool fills the pixel range (NumPy's reductions release the GIL)
-                ranges.append(saver.pool.submit(_pixel_range, rec, img, size=img.size))
-            pending.add(out)
-            converted.append(rec)
+            dst = output_img_dir / (f"{k}_{t}tap_{ideal_policy}" if k == "ideal" and ideal_policy != "clip"
+                                    else f"{k}_{t}tap")
+            new = [a for a in [dst, *dst.parents] if not a.exists()]
+            dst.mkdir(parents=True, exist_ok=True)
+            made.extend((saver.submitted, a) for a in reversed(new))
+            for p in sorted((q for q in src.glob("*.npy") if q.is_file()), key=lambda q: q.name.lower()):
+                m = FILENAME_RE.match(p.name)
+                if m is None:
+                    skipped.append({"reason": "invalid_filename", "path": str(p)})
+                    if strict:
+                        raise ValueError(f"Invalid vector filename: {p.name}")
+                    continue
+                if m.group("kind") != k or m.group("tap") != t:
+                    skipped.append({"reason": "kind_tap_mismatch", "path": str(p), "expected_kind": k,
+                                    "expected_tap": t, "file_kind": m.group("kind"), "file_tap": m.group("tap")})
+                    if strict:
+                        raise ValueError(f"Kind/tap mismatch in filename={p.name}, expected {k}_{t}tap")
+                    continue
+                # load and convert first, as the reference does: an unreadable or non-2-D input
+                # raises even where its image already exists
+                img = _to_image_u8(np.load(p), k, ideal_policy)
+                out = dst / f"{p.stem}.png"
+                if (out.exists() or out in pending) and not overwrite:
+                    skipped.append({"reason": "exists", "path": str(out)})
+                    continue
+                rec = {"input_npy": str(p), "output_img": str(out), "kind": k, "tap": f"{t}tap",
+                       "ideal_policy": ideal_policy if k == "ideal" else "n/a",
+                       "height": int(img.shape[0]), "width": int(img.shape[1]), "dtype": str(img.dtype),
+                       "pixel_min": None, "pixel_max": None}
+                while saver.items and saver.pending_size() + img.size > INFLIGHT_BYTES:
+                    saver.wait_oldest()  # bounded memory: the reference holds one image at a time
+                    saver.commit(ready_only=True)
+                saver.submit(saver.submitted, out, img, size=img.size)
+                if img.size:  # the writer pool fills the pixel range (NumPy's reductions release the GIL)
+                    ranges.append(saver.pool.submit(_pixel_range, rec, img, size=img.size))
+                pending.add(out)
+                converted.append(rec)
 
 
 def _build_argparser() -> argparse.ArgumentParser:
