@@ -12,7 +12,7 @@ from fir_1d.sim.vector import stage_io
 from fir_1d.sim.vector.gen_fixed_output import _save_all
 
 
-def test_saves_every_file(tmp_path, write_chunk):
+def test_saves_every_file(tmp_path):
     ys = [np.full((3, 5), i, np.uint8) for i in range(4)]
     paths = [tmp_path / f"y{i}.npy" for i in range(4)]
     assert _save_all(list(zip(paths, ys))) == 4
@@ -32,14 +32,7 @@ def _npy_bytes(tmp_path, y):
     return b
 
 
-@pytest.fixture(params=[16 << 20, 1], ids=["whole", "pieces"])
-def write_chunk(request, monkeypatch):
-    """Outputs written whole, or every output in 1-byte pieces by several writers (WRITE_CHUNK)."""
-    monkeypatch.setattr(stage_io, "WRITE_CHUNK", request.param)
-    return request.param
-
-
-def test_first_failure_stops_the_group_like_the_reference(tmp_path, write_chunk):
+def test_first_failure_stops_the_group_like_the_reference(tmp_path):
     ys = [np.full((2, 2), i, np.uint8) for i in range(3)]
     bad = tmp_path / "missing_dir" / "y1.npy"  # parent does not exist
     items = [(tmp_path / "y0.npy", ys[0]), (bad, ys[1]), (tmp_path / "y2.npy", ys[2])]
@@ -53,7 +46,7 @@ def test_first_failure_stops_the_group_like_the_reference(tmp_path, write_chunk)
     assert sorted(p.name for p in tmp_path.iterdir()) == ["y0.npy"]  # no temporary files left
 
 
-def test_later_existing_files_keep_their_contents(tmp_path, write_chunk):
+def test_later_existing_files_keep_their_contents(tmp_path):
     old = np.full((2, 2), 9, np.uint8)
     np.save(tmp_path / "y2.npy", old)
     (tmp_path / "y1.npy").mkdir()  # np.save(dir) fails: IsADirectoryError

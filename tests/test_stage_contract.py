@@ -67,22 +67,18 @@ def _oracle_batches(monkeypatch):
     monkeypatch.setattr(fir_hip, "fir1d_ideal_images_multi", ideal)
 
 
-@pytest.mark.parametrize("batch_bytes,read_chunk,write_chunk",
-                         [(1 << 30, 4 << 20, 16 << 20), (4096, 4 << 20, 16 << 20), (1 << 30, 1000, 1000)])
+@pytest.mark.parametrize("batch_bytes,read_chunk", [(1 << 30, 4 << 20), (4096, 4 << 20), (1 << 30, 1000)])
 @pytest.mark.parametrize("scn", S.SCENARIOS, ids=[s["name"] for s in S.SCENARIOS])
-def test_stage_driver_matches_reference_with_oracle_compute(scn, batch_bytes, read_chunk, write_chunk, tmp_path,
-                                                            monkeypatch):
+def test_stage_driver_matches_reference_with_oracle_compute(scn, batch_bytes, read_chunk, tmp_path, monkeypatch):
     """Every scenario through the product's stage driver with the device call replaced by the
     oracle: the reference's return value, exception text and every file's SHA-256.  4096-byte
     windows split each stage into one device call per image or two (stage_io.BATCH_BYTES);
-    1000-byte pieces read every larger input and write every larger output in several parallel
-    pieces (stage_io.READ_CHUNK, WRITE_CHUNK) -- the files still np.save's bytes."""
+    1000-byte read pieces read every larger input in several parallel pieces (stage_io.READ_CHUNK)."""
     from fir_1d.sim.vector import stage_io
 
     _oracle_batches(monkeypatch)
     monkeypatch.setattr(stage_io, "BATCH_BYTES", batch_bytes)
     monkeypatch.setattr(stage_io, "READ_CHUNK", read_chunk)
-    monkeypatch.setattr(stage_io, "WRITE_CHUNK", write_chunk)
     got = S.run(scn, tmp_path, gf._generate_fixed_outputs_for_tap_map, gi._generate_ideal_outputs_for_tap_map)
     want = BY_NAME[scn["name"]]
     assert (got["returned"], got["error"], got["files"]) == (want["returned"], want["error"], want["files"])

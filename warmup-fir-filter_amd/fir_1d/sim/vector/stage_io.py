@@ -228,49 +228,6 @@ def _npy_write(f, y) -> None:
     np.save(f, y)
 
 
-# An .npy output larger than this is written by several writer threads at once, in pieces of
-# WRITE_CHUNK bytes at their offsets in the file (np.save's exact bytes: its header, then the raw
-# C-order data), so one large plane does not leave a single thread writing at the end of a stage.
-WRITE_CHUNK = 16 << 20
-
-
-def _npy_header(y: np.ndarray) -> bytes:
-    import io
-
-    b = io.BytesIO()
-    np.lib.format._write_array_header(b, np.lib.format.header_data_from_array_1_0(y), None)  # np.save's own
-    return b.getvalue()
-
-
-def _pwrite_all(fd: int, mv, off: int) -> None:
-    while len(mv):
-        n = os.pwrite(fd, mv, off)
-        mv, off = mv[n:], off + n
-
-
-class _Joined(Future):
-    """A future that completes when all of its parts have (the first part's error, if any)."""
-
-    def __init__(self, parts: list):
-        super().__init__()
-        self._left, self._err, self._mu = len(parts), None, threading.Lock()
-        self.set_running_or_notify_cancel()
-        for f in parts:
-            f.add_done_callback(self._one)
-
-    def _one(self, f) -> None:
-        with self._mu:
-            if self._err is None and f.exception() is not None:
-                self._err = f.exception()
-            self._left -= 1
-            last = self._left == 0
-        if last:
-            if self._err is not None:
-                self.set_exception(self._err)
-            else:
-                self.set_result(None)
-
-
 class OrderedSaver:
     """np.save (or another ``writer``) of a stage's outputs on a thread pool, committed in the
     stage's order.
@@ -309,39 +266,10 @@ class OrderedSaver:
         tmp = path.with_name(f".{path.name}.{os.getpid()}.{threading.get_ident()}.{index}.part")
         if isinstance(self.pool, LargestFirstPool):
             fut = self.pool.submit(self._write, tmp, y, size=size)
-        elif self.writer is _npy_write and isinstance(y, np.ndarray) and y.nbytes > WRITE_CHUNK \
-                and y.flags.c_contiguous and not y.dtype.hasobject:
-            fut = self._submit_pieces(tmp, y)
         else:
             fut = self.pool.submit(self._write, tmp, y)
         self.items[index] = (path, y, tmp, fut, size)
         self.submitted += 1
-
-    def _submit_pieces(self, tmp: Path, y: np.ndarray) -> Future:
-        """np.save(tmp, y) by several writers: the header and the file's length first, then each
-        piece of the data at its offset."""
-        try:
-            head = _npy_header(y)
-            with open(tmp, "wb") as f:
-                f.write(head)
-                f.truncate(len(head) + y.nbytes)
-        except BaseException as exc:  # noqa: BLE001 - reported through the item's future (redo raises it)
-            fut: Future = Future()
-            fut.set_exception(exc)
-            return fut
-        data = memoryview(y.reshape(-1).view(np.uint8))
-        n = len(data)
-
-        def piece(lo: int) -> None:
-            t0 = time.perf_counter()
-            fd = os.open(tmp, os.O_WRONLY)
-            try:
-                _pwrite_all(fd, data[lo:min(lo + WRITE_CHUNK, n)], len(head) + lo)
-            finally:
-                os.close(fd)
-            with self._mu:
-                self.write_s += time.perf_counter() - t0
-        return _Joined([self.pool.submit(piece, lo) for lo in range(0, n, WRITE_CHUNK)])
 
     def commit(self, ready_only: bool = False, limit: int | None = None) -> int:
         """Rename every submitted file into place in index order; returns how many were written.
